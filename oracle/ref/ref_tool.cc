@@ -1,0 +1,246 @@
+// ref_tool.cc -- drives the REFERENCE library (compiled from /root/reference by
+// oracle/ref/Makefile) to produce golden vectors and the CPU baseline.
+//
+// TEST/BENCH INFRASTRUCTURE ONLY.  This is our own harness; it calls the
+// reference's public EVP_AEAD API (include/openssl/aead.h) exactly the way
+// bench/aead.cc:41-133 does (EVP_AEAD_CTX_init_with_direction, then
+// EVP_AEAD_CTX_seal_scatter with a 13-byte AD).
+//
+//   ref_tool edge                          edge-case vectors (JSON, stdout)
+//   ref_tool digest AEAD NKEYS RPK LEN [T] batch digests over the synthetic
+//                                          workload (oracle/synth.h); LEN is a
+//                                          byte count or "mixed"
+//   ref_tool bench AEAD LEN NREC T SECS    CPU baseline: T threads seal a
+//                                          resident sample of NREC synthetic
+//                                          records for about SECS seconds
+#include <openssl/aead.h>
+#include <openssl/sha.h>
+#include <omp.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "synth.h"
+
+namespace {
+
+const EVP_AEAD *aead_by_name(const std::string &n, size_t *key_len) {
+  if (n == "aes-128-gcm") { *key_len = 16; return EVP_aead_aes_128_gcm(); }
+  if (n == "aes-192-gcm") { *key_len = 24; return EVP_aead_aes_192_gcm(); }
+  if (n == "aes-256-gcm") { *key_len = 32; return EVP_aead_aes_256_gcm(); }
+  if (n == "chacha20-poly1305") { *key_len = 32; return EVP_aead_chacha20_poly1305(); }
+  fprintf(stderr, "unknown aead %s\n", n.c_str());
+  exit(2);
+}
+
+std::string hex(const uint8_t *p, size_t n) {
+  static const char *d = "0123456789abcdef";
+  std::string s(2 * n, '0');
+  for (size_t i = 0; i < n; i++) {
+    s[2 * i] = d[p[i] >> 4];
+    s[2 * i + 1] = d[p[i] & 15];
+  }
+  return s;
+}
+
+void fill_stream(uint64_t seed, uint8_t *p, size_t n) {
+  for (size_t i = 0; i < n; i++)
+    p[i] = (uint8_t)(synth_splitmix(seed * 0x10001 + i / 8) >> (8 * (i % 8)));
+}
+
+int cmd_edge() {
+  const char *names[] = {"aes-128-gcm", "aes-192-gcm", "aes-256-gcm", "chacha20-poly1305"};
+  const size_t lens[] = {0, 1, 2, 15, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 129,
+                         255, 256, 257, 1000, 1023, 1024, 1025, 1350, 4095, 4096,
+                         4097, 16383, 16384, 16385};
+  const size_t ad_lens[] = {0, 1, 13, 15, 16, 17, 31, 64, 100, 1000, 4097};
+  const size_t gcm_nonce_lens[] = {1, 8, 12, 15, 16, 17, 60, 128, 1024};
+  const size_t tag_lens[] = {1, 4, 8, 12, 13, 15, 16};
+  printf("[\n");
+  bool first = true;
+  uint64_t seed = 1000;
+  for (const char *name : names) {
+    size_t key_len;
+    const EVP_AEAD *aead = aead_by_name(name, &key_len);
+    bool gcm = std::string(name) != "chacha20-poly1305";
+    struct Case { size_t len, ad, nonce, tag; };
+    std::vector<Case> cases;
+    for (size_t l : lens) cases.push_back({l, 13, 12, 16});
+    if (std::string(name) == "aes-128-gcm") cases.push_back({65543, 13, 12, 16});
+    for (size_t a : ad_lens) cases.push_back({100, a, 12, 16});
+    for (size_t a : ad_lens) cases.push_back({1350, a, 12, 16});
+    for (size_t t : tag_lens) cases.push_back({333, 13, 12, t});
+    if (gcm)
+      for (size_t nl : gcm_nonce_lens) {
+        cases.push_back({100, 13, nl, 16});
+        cases.push_back({4097, 20, nl, 16});
+      }
+    for (const Case &c : cases) {
+      seed++;
+      std::vector<uint8_t> key(key_len), nonce(c.nonce), ad(c.ad), pt(c.len),
+          ct(c.len + 1), tag(16);
+      fill_stream(seed * 4 + 0, key.data(), key.size());
+      fill_stream(seed * 4 + 1, nonce.data(), nonce.size());
+      fill_stream(seed * 4 + 2, ad.data(), ad.size());
+      fill_stream(seed * 4 + 3, pt.data(), pt.size());
+      bssl::ScopedEVP_AEAD_CTX ctx;
+      if (!EVP_AEAD_CTX_init(ctx.get(), aead, key.data(), key.size(), c.tag, nullptr)) return 1;
+      size_t tag_out = 0;
+      if (!EVP_AEAD_CTX_seal_scatter(ctx.get(), ct.data(), tag.data(), &tag_out, tag.size(),
+                                     nonce.data(), nonce.size(), pt.data(), pt.size(),
+                                     nullptr, 0, ad.data(), ad.size()))
+        return 1;
+      printf("%s{\"aead\": \"%s\", \"key\": \"%s\", \"nonce\": \"%s\", \"ad\": \"%s\", "
+             "\"pt\": \"%s\", \"ct\": \"%s\", \"tag\": \"%s\"}",
+             first ? "" : ",\n", name, hex(key.data(), key.size()).c_str(),
+             hex(nonce.data(), nonce.size()).c_str(), hex(ad.data(), ad.size()).c_str(),
+             hex(pt.data(), pt.size()).c_str(), hex(ct.data(), c.len).c_str(),
+             hex(tag.data(), tag_out).c_str());
+      first = false;
+    }
+  }
+  printf("\n]\n");
+  return 0;
+}
+
+// Digest definitions (mirrored by tests/golden_digest.py):
+//   tags_sha256 = SHA-256(tag_0 || tag_1 || ... )
+//   ct_sha256   = SHA-256(SHA-256(ct of records [0,1024)) || SHA-256(ct of
+//                 records [1024,2048)) || ...)   ("checksum of checksums")
+int cmd_digest(int argc, char **argv) {
+  if (argc < 6) return 2;
+  size_t key_len;
+  const char *name = argv[2];
+  const EVP_AEAD *aead = aead_by_name(name, &key_len);
+  uint64_t nkeys = strtoull(argv[3], nullptr, 0);
+  uint64_t rpk = strtoull(argv[4], nullptr, 0);
+  bool mixed = std::string(argv[5]) == "mixed";
+  uint64_t fixed_len = mixed ? 0 : strtoull(argv[5], nullptr, 0);
+  int threads = argc > 6 ? atoi(argv[6]) : 8;
+  uint64_t n = nkeys * rpk;
+  const uint64_t kChunk = 1024;
+  uint64_t nchunks = (n + kChunk - 1) / kChunk;
+  std::vector<uint8_t> tags(n * 16);
+  std::vector<uint8_t> chunk_digests(nchunks * 32);
+  uint64_t total_bytes = 0;
+#pragma omp parallel num_threads(threads) reduction(+ : total_bytes)
+  {
+    std::vector<uint8_t> pt, ct;
+    bssl::ScopedEVP_AEAD_CTX ctx;
+    uint64_t cur_key = UINT64_MAX;
+#pragma omp for schedule(dynamic, 1)
+    for (long long c = 0; c < (long long)nchunks; c++) {
+      SHA256_CTX sha;
+      SHA256_Init(&sha);
+      uint64_t lo = c * kChunk, hi = lo + kChunk < n ? lo + kChunk : n;
+      for (uint64_t i = lo; i < hi; i++) {
+        uint64_t k = i / rpk;
+        if (k != cur_key) {
+          std::vector<uint8_t> key(key_len);
+          synth_key(k, key_len, key.data());
+          ctx.Reset();
+          if (!EVP_AEAD_CTX_init(ctx.get(), aead, key.data(), key_len, 16, nullptr)) abort();
+          cur_key = k;
+        }
+        uint64_t len = mixed ? synth_mixed_len(i) : fixed_len;
+        pt.resize(len + 1);
+        ct.resize(len + 1);
+        synth_pt(i, len, pt.data());
+        uint8_t nonce[12], ad[13];
+        synth_nonce(i, nonce);
+        synth_ad(i, len, ad);
+        size_t tag_out = 0;
+        if (!EVP_AEAD_CTX_seal_scatter(ctx.get(), ct.data(), &tags[16 * i], &tag_out, 16, nonce,
+                                       12, pt.data(), len, nullptr, 0, ad, 13))
+          abort();
+        SHA256_Update(&sha, ct.data(), len);
+        total_bytes += len;
+      }
+      SHA256_Final(&chunk_digests[32 * c], &sha);
+    }
+  }
+  uint8_t tags_d[32], ct_d[32];
+  SHA256(tags.data(), tags.size(), tags_d);
+  SHA256(chunk_digests.data(), chunk_digests.size(), ct_d);
+  printf("{\"aead\": \"%s\", \"nkeys\": %llu, \"records_per_key\": %llu, \"len\": \"%s\", "
+         "\"records\": %llu, \"bytes\": %llu, \"tags_sha256\": \"%s\", \"ct_sha256\": \"%s\", "
+         "\"tag_first\": \"%s\", \"tag_last\": \"%s\"}\n",
+         name, (unsigned long long)nkeys, (unsigned long long)rpk, argv[5],
+         (unsigned long long)n, (unsigned long long)total_bytes, hex(tags_d, 32).c_str(),
+         hex(ct_d, 32).c_str(), hex(&tags[0], 16).c_str(), hex(&tags[16 * (n - 1)], 16).c_str());
+  return 0;
+}
+
+int cmd_bench(int argc, char **argv) {
+  if (argc < 7) return 2;
+  size_t key_len;
+  const char *name = argv[2];
+  const EVP_AEAD *aead = aead_by_name(name, &key_len);
+  uint64_t len = strtoull(argv[3], nullptr, 0);
+  uint64_t nrec = strtoull(argv[4], nullptr, 0);
+  int threads = atoi(argv[5]);
+  double secs = atof(argv[6]);
+  const uint64_t stride = (len + 63) / 64 * 64;
+  std::vector<uint8_t> pt(nrec * stride), ct(nrec * stride), tags(nrec * 16);
+  std::vector<uint8_t> nonces(nrec * 12), ads(nrec * 13);
+  for (uint64_t i = 0; i < nrec; i++) {
+    synth_pt(i, len, &pt[i * stride]);
+    synth_nonce(i, &nonces[12 * i]);
+    synth_ad(i, len, &ads[13 * i]);
+  }
+  std::vector<uint8_t> key(key_len);
+  synth_key(0, key_len, key.data());
+  bssl::ScopedEVP_AEAD_CTX ctx;
+  if (!EVP_AEAD_CTX_init_with_direction(ctx.get(), aead, key.data(), key_len,
+                                        EVP_AEAD_DEFAULT_TAG_LENGTH, evp_aead_seal))
+    return 1;
+  std::vector<uint64_t> done(threads, 0);
+  auto t0 = std::chrono::steady_clock::now();
+  double elapsed = 0;
+#pragma omp parallel num_threads(threads)
+  {
+    int t = omp_get_thread_num();
+    uint64_t lo = nrec * t / threads, hi = nrec * (t + 1) / threads;
+    uint64_t count = 0;
+    for (;;) {
+      for (uint64_t i = lo; i < hi; i++) {
+        size_t tag_out;
+        if (!EVP_AEAD_CTX_seal_scatter(ctx.get(), &ct[i * stride], &tags[16 * i], &tag_out, 16,
+                                       &nonces[12 * i], 12, &pt[i * stride], len, nullptr, 0,
+                                       &ads[13 * i], 13))
+          abort();
+        count++;
+      }
+      double e = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (e >= secs) break;
+    }
+    done[t] = count;
+  }
+  elapsed = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  uint64_t recs = 0;
+  for (uint64_t c : done) recs += c;
+  double bytes = (double)recs * (double)len;
+  printf("{\"aead\": \"%s\", \"len\": %llu, \"sample_records\": %llu, \"threads\": %d, "
+         "\"records_sealed\": %llu, \"seconds\": %.4f, \"gib_per_s\": %.4f}\n",
+         name, (unsigned long long)len, (unsigned long long)nrec, threads,
+         (unsigned long long)recs, elapsed, bytes / elapsed / (1024.0 * 1024 * 1024));
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+  if (argc < 2) {
+    fprintf(stderr, "usage: ref_tool edge|digest|bench ...\n");
+    return 2;
+  }
+  std::string cmd = argv[1];
+  if (cmd == "edge") return cmd_edge();
+  if (cmd == "digest") return cmd_digest(argc, argv);
+  if (cmd == "bench") return cmd_bench(argc, argv);
+  return 2;
+}

@@ -1,0 +1,20 @@
+import os
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (HERE, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+    config.addinivalue_line("markers", "slow: long-running (full BASELINE-size batches)")
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return os.path.join(HERE, "golden")

@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Regenerates the committed fixtures under tests/golden/.
+
+Run in the build container (where /root/reference exists); the GPU box only
+reads the committed JSON.  Three kinds of fixture are produced:
+
+* kat_*.json      -- the reference's OWN known-answer data, converted (not
+                     copied: re-encoded as JSON records) from
+                       crypto/cipher/test/aes_{128,192,256}_gcm_tests.txt
+                       crypto/cipher/test/chacha20_poly1305_tests.txt
+                       third_party/wycheproof_testvectors/aes_gcm_test.txt
+                       third_party/wycheproof_testvectors/chacha20_poly1305_test.txt
+                       crypto/fipsmodule/aes/aes_tests.txt
+                       crypto/poly1305/poly1305_tests.txt
+                     The field semantics follow crypto/cipher/aead_test.cc:188-281
+                     (TestVector: tag_len = len(TAG)) and :1493-1564
+                     (RunWycheproofTestCase: tagSize instruction, result).
+* ref_edge.json   -- edge-case records sealed by the reference library built
+                     from source into oracle/_ref/ (oracle/ref/Makefile):
+                     `oracle/_ref/ref_tool edge`.
+* ref_digests.json-- batch digests of the synthetic workloads of SURVEY.md
+                     section 8(d) sealed by the reference library:
+                     `oracle/_ref/ref_tool digest ...`.
+
+Usage: python tests/golden/make_golden.py [--skip-full]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get("BSSL_REFERENCE", "/root/reference")
+REF_TOOL = os.path.join(ROOT, "oracle", "_ref", "ref_tool")
+
+
+def parse_filetest(path):
+    """Minimal reader for the reference FileTest format (KEY: value blocks,
+    '[instr = v]' instruction lines, blank-line separated)."""
+    cases, cur, instr = [], {}, {}
+    with open(path) as f:
+        for raw in f:
+            line = raw.strip()
+            if line.startswith("#"):
+                continue
+            if not line:
+                if cur:
+                    cur["_instr"] = dict(instr)
+                    cases.append(cur)
+                    cur = {}
+                continue
+            if line.startswith("[") and line.endswith("]"):
+                if cur:
+                    cur["_instr"] = dict(instr)
+                    cases.append(cur)
+                    cur = {}
+                k, _, v = line[1:-1].partition("=")
+                instr[k.strip()] = v.strip()
+                continue
+            if ":" in line and (line.split(":")[0].isupper() or line.split(":")[0][:1].isupper()):
+                k, _, v = line.partition(":")
+            else:
+                k, _, v = line.partition("=")
+            cur[k.strip()] = v.strip()
+    if cur:
+        cur["_instr"] = dict(instr)
+        cases.append(cur)
+    return cases
+
+
+def unq(v):
+    v = v.strip()
+    if v.startswith('"') and v.endswith('"'):
+        return v[1:-1].encode().hex()
+    return v
+
+
+def convert_aead():
+    out = []
+    files = [
+        ("crypto/cipher/test/aes_128_gcm_tests.txt", "aes-128-gcm"),
+        ("crypto/cipher/test/aes_192_gcm_tests.txt", "aes-192-gcm"),
+        ("crypto/cipher/test/aes_256_gcm_tests.txt", "aes-256-gcm"),
+        ("crypto/cipher/test/chacha20_poly1305_tests.txt", "chacha20-poly1305"),
+    ]
+    for rel, aead in files:
+        for i, c in enumerate(parse_filetest(os.path.join(REF, rel))):
+            out.append({
+                "source": f"{rel}#{i}", "aead": aead, "key": unq(c["KEY"]),
+                "nonce": unq(c["NONCE"]), "ad": unq(c["AD"]), "pt": unq(c["IN"]),
+                "ct": unq(c["CT"]), "tag": unq(c["TAG"]), "valid": True,
+            })
+    wfiles = [
+        ("third_party/wycheproof_testvectors/aes_gcm_test.txt", "gcm"),
+        ("third_party/wycheproof_testvectors/chacha20_poly1305_test.txt", "chacha"),
+    ]
+    for rel, kind in wfiles:
+        for c in parse_filetest(os.path.join(REF, rel)):
+            ins = c["_instr"]
+            if kind == "gcm":
+                aead = {"128": "aes-128-gcm", "192": "aes-192-gcm", "256": "aes-256-gcm"}[ins["keySize"]]
+            else:
+                aead = "chacha20-poly1305"
+            tag_len = int(ins["tagSize"]) // 8
+            out.append({
+                "source": f"{rel}#tcId={c.get('tcId', '?')}", "aead": aead, "key": c["key"],
+                "nonce": c["iv"], "ad": c["aad"], "pt": c["msg"], "ct": c["ct"],
+                "tag": c["tag"], "tag_len": tag_len, "valid": c["result"] == "valid",
+                "flags": c.get("flags", ""),
+            })
+    return out
+
+
+def _tcids(path):
+    ids = []
+    with open(path) as f:
+        for line in f:
+            if line.startswith("# tcId"):
+                ids.append(line.split("=")[1].strip())
+    return ids
+
+
+def convert_aes():
+    out = []
+    for i, c in enumerate(parse_filetest(os.path.join(REF, "crypto/fipsmodule/aes/aes_tests.txt"))):
+        out.append({"source": f"crypto/fipsmodule/aes/aes_tests.txt#{i}", "mode": c["Mode"],
+                    "key": c["Key"], "pt": c["Plaintext"], "ct": c["Ciphertext"]})
+    return out
+
+
+def convert_poly():
+    out = []
+    for i, c in enumerate(parse_filetest(os.path.join(REF, "crypto/poly1305/poly1305_tests.txt"))):
+        out.append({"source": f"crypto/poly1305/poly1305_tests.txt#{i}", "key": unq(c["Key"]),
+                    "input": unq(c["Input"]), "mac": unq(c["MAC"])})
+    return out
+
+
+# Batch-digest workloads; "parity" sizes are checked in full by
+# the GPU tests, "config" sizes are the BASELINE.json configs themselves.
+DIGESTS = [
+    ("parity_aes128_16k", "aes-128-gcm", 1, 4096, "16384"),
+    ("parity_aes256_mixed", "aes-256-gcm", 1, 8192, "mixed"),
+    ("parity_chacha_1350", "chacha20-poly1305", 1, 16384, "1350"),
+    ("parity_multikey_aes128", "aes-128-gcm", 256, 16, "16384"),
+    ("config2_aes128_16k", "aes-128-gcm", 1, 1048576, "16384"),
+    ("config3_chacha_1350", "chacha20-poly1305", 1, 1048576, "1350"),
+    ("config4_aes256_mixed", "aes-256-gcm", 1, 4194304, "mixed"),
+    ("config5_multikey_aes128", "aes-128-gcm", 65536, 64, "16384"),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--skip-full", action="store_true")
+    args = ap.parse_args()
+    aead = convert_aead()
+    # attach Wycheproof tcIds (comment lines precede each record in file order)
+    for rel in ("third_party/wycheproof_testvectors/aes_gcm_test.txt",
+                "third_party/wycheproof_testvectors/chacha20_poly1305_test.txt"):
+        ids = _tcids(os.path.join(REF, rel))
+        recs = [r for r in aead if r["source"].startswith(rel)]
+        assert len(ids) == len(recs), (rel, len(ids), len(recs))
+        for r, t in zip(recs, ids):
+            r["source"] = f"{rel}#tcId={t}"
+    with open(os.path.join(HERE, "kat_aead.json"), "w") as f:
+        json.dump(aead, f, indent=0)
+    with open(os.path.join(HERE, "kat_aes.json"), "w") as f:
+        json.dump(convert_aes(), f, indent=0)
+    with open(os.path.join(HERE, "kat_poly1305.json"), "w") as f:
+        json.dump(convert_poly(), f, indent=0)
+    print(f"kat_aead.json: {len(aead)} cases")
+
+    if not os.path.exists(REF_TOOL):
+        subprocess.check_call(["make", "-j8", "-C", os.path.join(ROOT, "oracle", "ref")])
+    edge = json.loads(subprocess.check_output([REF_TOOL, "edge"]))
+    with open(os.path.join(HERE, "ref_edge.json"), "w") as f:
+        json.dump(edge, f, indent=0)
+    print(f"ref_edge.json: {len(edge)} cases")
+
+    path = os.path.join(HERE, "ref_digests.json")
+    digests = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            digests = json.load(f)
+    for name, aead_name, nkeys, rpk, length in DIGESTS:
+        if args.skip_full and name.startswith("config"):
+            continue
+        res = json.loads(subprocess.check_output(
+            [REF_TOOL, "digest", aead_name, str(nkeys), str(rpk), length, "8"]))
+        digests[name] = res
+        print(name, res["tags_sha256"][:16], res["ct_sha256"][:16], flush=True)
+        with open(path, "w") as f:
+            json.dump(digests, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
