@@ -1,0 +1,943 @@
+// aead_api.cc -- the C ABI of include/bssl_amd/aead.h.
+//
+// Mirrors the reference's AEAD dispatch layer
+// (crypto/fipsmodule/cipher/aead.cc.inc): argument and alias checks, the
+// zero-on-error cleanup of every entry point, the per-AEAD vtable limits
+// (e_aes.cc.inc:733-924, 1040-1230; e_chacha20poly1305.cc:45-400) and the
+// CIPHER_R_* error queue.  All record arithmetic runs in the HIP kernels
+// (gcm.hip, chacha.hip): single-record calls upload their host buffers, run a
+// one-record batch and download the result.
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <new>
+#include <vector>
+
+#include "bssl_amd/aead.h"
+#include "internal.h"
+
+using namespace bssl_amd;
+
+// ---------------------------------------------------------------------------
+// Error queue (reference crypto/err/err.cc semantics: thread-local,
+// ERR_NUM_ERRORS = 16 deep, oldest dropped on overflow).
+namespace {
+constexpr int kNumErrors = 16;
+thread_local uint32_t t_err[kNumErrors];
+thread_local int t_err_top = 0, t_err_bottom = 0;
+
+void put_error(int reason) {
+  t_err_top = (t_err_top + 1) % kNumErrors;
+  if (t_err_top == t_err_bottom) t_err_bottom = (t_err_bottom + 1) % kNumErrors;
+  t_err[t_err_top] = ((uint32_t)(ERR_LIB_CIPHER & 0xff) << 24) | ((uint32_t)reason & 0xfff);
+}
+}  // namespace
+
+#define PUT_ERROR(reason) put_error(reason)
+
+extern "C" uint32_t ERR_get_error(void) {
+  if (t_err_top == t_err_bottom) return 0;
+  t_err_bottom = (t_err_bottom + 1) % kNumErrors;
+  uint32_t e = t_err[t_err_bottom];
+  t_err[t_err_bottom] = 0;
+  return e;
+}
+
+extern "C" uint32_t ERR_peek_error(void) {
+  if (t_err_top == t_err_bottom) return 0;
+  return t_err[(t_err_bottom + 1) % kNumErrors];
+}
+
+extern "C" uint32_t ERR_peek_last_error(void) {
+  if (t_err_top == t_err_bottom) return 0;
+  return t_err[t_err_top];
+}
+
+extern "C" void ERR_clear_error(void) {
+  t_err_top = t_err_bottom = 0;
+  memset(t_err, 0, sizeof(t_err));
+}
+
+// ---------------------------------------------------------------------------
+// AEAD method objects (the reference's struct evp_aead_st vtable,
+// crypto/fipsmodule/cipher/internal.h:40-78, reduced to the parameters the
+// GPU path needs).
+struct evp_aead_st {
+  uint8_t key_len;
+  uint8_t nonce_len;
+  uint8_t overhead;
+  uint8_t max_tag_len;
+  AeadKind kind;
+  int tls;  // 0, 12 or 13: the tls12 / tls13 monotonic-nonce variants
+};
+
+namespace {
+const evp_aead_st kAes128Gcm = {16, 12, 16, 16, kAeadAesGcm, 0};
+const evp_aead_st kAes192Gcm = {24, 12, 16, 16, kAeadAesGcm, 0};
+const evp_aead_st kAes256Gcm = {32, 12, 16, 16, kAeadAesGcm, 0};
+const evp_aead_st kChaChaPoly = {32, 12, 16, 16, kAeadChaChaPoly, 0};
+const evp_aead_st kAes128GcmTls12 = {16, 12, 16, 16, kAeadAesGcm, 12};
+const evp_aead_st kAes256GcmTls12 = {32, 12, 16, 16, kAeadAesGcm, 12};
+const evp_aead_st kAes128GcmTls13 = {16, 12, 16, 16, kAeadAesGcm, 13};
+const evp_aead_st kAes256GcmTls13 = {32, 12, 16, 16, kAeadAesGcm, 13};
+
+// Device-resident key material for one or more keys.
+struct KeyMaterial {
+  const EVP_AEAD *aead;
+  int device;
+  size_t num_keys;
+  int nr;
+  void *dev;  // GcmKeyDev[num_keys] or ChaChaKeyDev[num_keys]
+};
+
+// State kept in EVP_AEAD_CTX.state (560 bytes, reference aead.h:222-235).
+struct CtxState {
+  KeyMaterial *km;
+  uint64_t min_next_nonce;  // tls12/tls13 (e_aes.cc.inc:1041-1044, 1130-1134)
+  uint64_t mask;
+};
+static_assert(sizeof(CtxState) <= sizeof(((EVP_AEAD_CTX *)nullptr)->state), "state");
+
+CtxState *state_of(const EVP_AEAD_CTX *ctx) {
+  return reinterpret_cast<CtxState *>(const_cast<uint8_t *>(ctx->state.opaque));
+}
+
+KeyMaterial *make_keys(const EVP_AEAD *aead, const uint8_t *keys, size_t num_keys) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  KeyMaterial *km = new (std::nothrow) KeyMaterial{aead, dev, num_keys, 0, nullptr};
+  if (!km) return nullptr;
+  size_t bytes;
+  std::vector<uint8_t> host;
+  if (aead->kind == kAeadAesGcm) {
+    bytes = num_keys * sizeof(GcmKeyDev);
+    host.resize(bytes);
+    GcmKeyDev *h = reinterpret_cast<GcmKeyDev *>(host.data());
+    for (size_t i = 0; i < num_keys; i++) {
+      if (!gcm_key_setup(keys + i * aead->key_len, aead->key_len, &h[i])) {
+        delete km;
+        return nullptr;
+      }
+    }
+    km->nr = (int)h[0].nr;
+  } else {
+    bytes = num_keys * sizeof(ChaChaKeyDev);
+    host.resize(bytes);
+    ChaChaKeyDev *h = reinterpret_cast<ChaChaKeyDev *>(host.data());
+    for (size_t i = 0; i < num_keys; i++) chacha_key_setup(keys + i * aead->key_len, &h[i]);
+  }
+  if (hipMalloc(&km->dev, bytes) != hipSuccess) {
+    delete km;
+    return nullptr;
+  }
+  if (hipMemcpy(km->dev, host.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+    hipFree(km->dev);
+    delete km;
+    return nullptr;
+  }
+  return km;
+}
+
+void free_keys(KeyMaterial *km) {
+  if (!km) return;
+  if (km->dev) hipFree(km->dev);
+  delete km;
+}
+
+thread_local bool t_timing = false;
+thread_local double t_last_ms = 0;
+thread_local const char *t_last_name = "";
+
+// Launch a batch over device buffers.  Returns 1 on success.
+int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch, bool open,
+              bool use_key_index, void *stream) {
+  BatchDesc d;
+  d.in = batch->in;
+  d.out = batch->out;
+  d.offsets = batch->offsets;
+  d.lengths = batch->lengths;
+  d.record_stride = batch->record_stride;
+  d.record_len = batch->record_len;
+  d.nonces = batch->nonces;
+  d.nonce_len = batch->nonce_len;
+  d.ad = batch->ad;
+  d.ad_offsets = batch->ad_offsets;
+  d.ad_lengths = batch->ad_lengths;
+  d.ad_stride = batch->ad_stride;
+  d.ad_len = batch->ad_len;
+  d.tags = batch->tags;
+  d.status = batch->status;
+  d.key_index = use_key_index ? batch->key_index : nullptr;
+  d.num_records = batch->num_records;
+  d.tag_len = (uint32_t)tag_len;
+  d.num_keys = (uint32_t)km->num_keys;
+  float ms = 0;
+  int rc;
+  if (km->aead->kind == kAeadAesGcm) {
+    rc = launch_gcm(static_cast<const GcmKeyDev *>(km->dev), d, open, km->nr, stream,
+                    t_timing ? &ms : nullptr);
+    t_last_name = "gcm_kernel";
+  } else {
+    rc = launch_chacha(static_cast<const ChaChaKeyDev *>(km->dev), d, open, stream,
+                       t_timing ? &ms : nullptr);
+    t_last_name = "chacha_poly_kernel";
+  }
+  t_last_ms = ms;
+  if (rc != 0) {
+    PUT_ERROR(ERR_R_INTERNAL_ERROR);
+    return 0;
+  }
+  return 1;
+}
+
+bool check_batch(const EVP_AEAD *aead, const BSSL_AMD_BATCH *b) {
+  if (!b) {
+    PUT_ERROR(ERR_R_SHOULD_NOT_HAVE_BEEN_CALLED);
+    return false;
+  }
+  if (b->num_records == 0) return true;
+  if (!b->in || !b->out || !b->nonces || !b->tags || (!b->ad && (b->ad_lengths || b->ad_len))) {
+    PUT_ERROR(ERR_R_SHOULD_NOT_HAVE_BEEN_CALLED);
+    return false;
+  }
+  if (aead->kind == kAeadAesGcm) {
+    if (b->nonce_len == 0) {  // e_aes.cc.inc:790-793
+      PUT_ERROR(CIPHER_R_INVALID_NONCE_SIZE);
+      return false;
+    }
+  } else if (b->nonce_len != 12) {  // e_chacha20poly1305.cc:127-130
+    PUT_ERROR(CIPHER_R_UNSUPPORTED_NONCE_SIZE);
+    return false;
+  }
+  if (aead->tls) {
+    // The stateful tls12/tls13 variants check nonce monotonicity record by
+    // record in order on the host; batches of them are not supported.
+    PUT_ERROR(CIPHER_R_CTRL_NOT_IMPLEMENTED);
+    return false;
+  }
+  return true;
+}
+
+// ---- single-record helper: host buffers -> one-record device batch --------
+
+struct Scratch {
+  int device = -1;
+  uint8_t *dev = nullptr;
+  size_t cap = 0;
+  hipStream_t stream = nullptr;
+  ~Scratch() {
+    if (dev) hipFree(dev);
+    if (stream) hipStreamDestroy(stream);
+  }
+};
+thread_local Scratch t_scratch;
+
+uint8_t *scratch(size_t bytes, hipStream_t *stream) {
+  int dev = 0;
+  hipGetDevice(&dev);
+  if (t_scratch.device != dev) {
+    t_scratch.dev = nullptr;  // buffers of another device are kept until exit
+    t_scratch.cap = 0;
+    t_scratch.stream = nullptr;
+    t_scratch.device = dev;
+  }
+  if (!t_scratch.stream && hipStreamCreateWithFlags(&t_scratch.stream, hipStreamNonBlocking) != hipSuccess)
+    return nullptr;
+  if (t_scratch.cap < bytes) {
+    if (t_scratch.dev) hipFree(t_scratch.dev);
+    size_t cap = bytes < (1u << 20) ? (1u << 20) : bytes;
+    if (hipMalloc(&t_scratch.dev, cap) != hipSuccess) {
+      t_scratch.dev = nullptr;
+      t_scratch.cap = 0;
+      return nullptr;
+    }
+    t_scratch.cap = cap;
+  }
+  *stream = t_scratch.stream;
+  return t_scratch.dev;
+}
+
+size_t round16(size_t n) { return (n + 15) & ~size_t(15); }
+
+// Seal or open one record held in host memory.  `in`/`out` may be equal.
+// For open, `tag` is read; for seal it is written (tag_len bytes).
+int one_record(const EVP_AEAD_CTX *ctx, bool open, const uint8_t *in, uint8_t *out,
+               size_t len, const uint8_t *nonce, size_t nonce_len, const uint8_t *ad,
+               size_t ad_len, uint8_t *tag, size_t tag_len) {
+  CtxState *st = state_of(ctx);
+  const size_t o_in = 0, o_nonce = round16(len), o_ad = o_nonce + round16(nonce_len),
+               o_tag = o_ad + round16(ad_len), o_status = o_tag + 16,
+               total = o_status + 16;
+  hipStream_t s;
+  uint8_t *d = scratch(total, &s);
+  if (!d) {
+    PUT_ERROR(ERR_R_MALLOC_FAILURE);
+    return 0;
+  }
+  bool ok = true;
+  if (len) ok &= hipMemcpyAsync(d + o_in, in, len, hipMemcpyHostToDevice, s) == hipSuccess;
+  if (nonce_len)
+    ok &= hipMemcpyAsync(d + o_nonce, nonce, nonce_len, hipMemcpyHostToDevice, s) == hipSuccess;
+  if (ad_len) ok &= hipMemcpyAsync(d + o_ad, ad, ad_len, hipMemcpyHostToDevice, s) == hipSuccess;
+  if (open && tag_len)
+    ok &= hipMemcpyAsync(d + o_tag, tag, tag_len, hipMemcpyHostToDevice, s) == hipSuccess;
+  if (!ok) {
+    PUT_ERROR(ERR_R_INTERNAL_ERROR);
+    return 0;
+  }
+  BSSL_AMD_BATCH b;
+  memset(&b, 0, sizeof(b));
+  b.num_records = 1;
+  b.in = d + o_in;
+  b.out = d + o_in;
+  b.record_len = len;
+  b.nonces = d + o_nonce;
+  b.nonce_len = nonce_len;
+  b.ad = d + o_ad;
+  b.ad_len = ad_len;
+  b.tags = d + o_tag;
+  b.status = d + o_status;
+  if (!run_batch(st->km, tag_len, &b, open, false, s)) return 0;
+  uint8_t status = 0;
+  ok = hipMemcpyAsync(&status, d + o_status, 1, hipMemcpyDeviceToHost, s) == hipSuccess;
+  if (len) ok &= hipMemcpyAsync(out, d + o_in, len, hipMemcpyDeviceToHost, s) == hipSuccess;
+  if (!open && tag_len)
+    ok &= hipMemcpyAsync(tag, d + o_tag, tag_len, hipMemcpyDeviceToHost, s) == hipSuccess;
+  ok &= hipStreamSynchronize(s) == hipSuccess;
+  if (!ok) {
+    PUT_ERROR(ERR_R_INTERNAL_ERROR);
+    return 0;
+  }
+  if (!status) {
+    PUT_ERROR(open ? CIPHER_R_BAD_DECRYPT : CIPHER_R_TOO_LARGE);
+    return 0;
+  }
+  return 1;
+}
+
+int buffers_alias(const void *a, size_t a_len, const void *b, size_t b_len) {
+  // crypto/internal.h:187-196
+  uintptr_t au = (uintptr_t)a, bu = (uintptr_t)b;
+  return au + a_len > bu && bu + b_len > au;
+}
+
+bool check_alias(const uint8_t *in, size_t in_len, const uint8_t *out, size_t out_len) {
+  if (!buffers_alias(in, in_len, out, out_len)) return true;
+  return in == out;
+}
+
+// iovec helpers (crypto/fipsmodule/cipher/internal.h:162-236).
+bool iovec_total(const CRYPTO_IOVEC *v, size_t n, size_t *total) {
+  size_t t = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (t + v[i].len < t) return false;
+    t += v[i].len;
+  }
+  *total = t;
+  return true;
+}
+
+bool ivec_total(const CRYPTO_IVEC *v, size_t n, size_t *total) {
+  size_t t = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (t + v[i].len < t) return false;
+    t += v[i].len;
+  }
+  *total = t;
+  return true;
+}
+
+void clear_iovec(const CRYPTO_IOVEC *v, size_t n) {
+  for (size_t i = 0; i < n; i++)
+    if (v[i].len) memset(v[i].out, 0, v[i].len);
+}
+
+bool iovec_internal_alias_ok(const CRYPTO_IOVEC *v, size_t n) {
+  for (size_t i = 0; i < n; i++)
+    if (!check_alias(v[i].in, v[i].len, v[i].out, v[i].len)) return false;
+  return true;
+}
+
+// Gather iovec inputs into one contiguous host buffer.
+std::vector<uint8_t> gather_in(const CRYPTO_IOVEC *v, size_t n, size_t total) {
+  std::vector<uint8_t> buf(total);
+  size_t o = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (v[i].len) memcpy(buf.data() + o, v[i].in, v[i].len);
+    o += v[i].len;
+  }
+  return buf;
+}
+
+void scatter_out(const CRYPTO_IOVEC *v, size_t n, const uint8_t *src, size_t total) {
+  size_t o = 0;
+  for (size_t i = 0; i < n && o < total; i++) {
+    size_t take = v[i].len < total - o ? v[i].len : total - o;
+    if (take) memcpy(v[i].out, src + o, take);
+    o += v[i].len;
+  }
+}
+
+std::vector<uint8_t> gather_ad(const CRYPTO_IVEC *v, size_t n, size_t total) {
+  std::vector<uint8_t> buf(total);
+  size_t o = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (v[i].len) memcpy(buf.data() + o, v[i].in, v[i].len);
+    o += v[i].len;
+  }
+  return buf;
+}
+
+uint64_t load_be64(const uint8_t *p) {
+  uint64_t v = 0;
+  for (int i = 0; i < 8; i++) v = (v << 8) | p[i];
+  return v;
+}
+
+// The stateful TLS nonce checks of aead_aes_gcm_tls12_sealv /
+// aead_aes_gcm_tls13_sealv (e_aes.cc.inc:1071-1100, 1162-1202).
+bool tls_nonce_check(const EVP_AEAD_CTX *ctx, const uint8_t *nonce, size_t nonce_len) {
+  const EVP_AEAD *aead = ctx->aead;
+  if (!aead->tls) return true;
+  CtxState *st = state_of(ctx);
+  if (nonce_len != 12) {
+    PUT_ERROR(CIPHER_R_UNSUPPORTED_NONCE_SIZE);
+    return false;
+  }
+  uint64_t given = load_be64(nonce + 4);
+  if (aead->tls == 12) {
+    if (given == UINT64_MAX || given < st->min_next_nonce) {
+      PUT_ERROR(CIPHER_R_INVALID_NONCE);
+      return false;
+    }
+    st->min_next_nonce = given + 1;
+    return true;
+  }
+  if (st->min_next_nonce == 0) {
+    st->mask = given;
+    st->min_next_nonce = 1;
+    return true;
+  }
+  given ^= st->mask;
+  if (given == UINT64_MAX || given < st->min_next_nonce) {
+    PUT_ERROR(CIPHER_R_INVALID_NONCE);
+    return false;
+  }
+  st->min_next_nonce = given + 1;
+  return true;
+}
+
+// Common per-AEAD record checks before any device work (sealv/openv paths).
+bool aead_record_checks(const EVP_AEAD_CTX *ctx, size_t nonce_len, size_t in_len) {
+  const EVP_AEAD *aead = ctx->aead;
+  if (aead->kind == kAeadAesGcm) {
+    if (nonce_len == 0) {
+      PUT_ERROR(CIPHER_R_INVALID_NONCE_SIZE);
+      return false;
+    }
+  } else {
+    if (nonce_len != 12) {
+      PUT_ERROR(CIPHER_R_UNSUPPORTED_NONCE_SIZE);
+      return false;
+    }
+    if ((uint64_t)in_len >= (UINT64_C(1) << 32) * 64 - 64) {
+      PUT_ERROR(CIPHER_R_TOO_LARGE);
+      return false;
+    }
+  }
+  return true;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Method getters and sizes.
+extern "C" {
+
+const EVP_AEAD *EVP_aead_aes_128_gcm(void) { return &kAes128Gcm; }
+const EVP_AEAD *EVP_aead_aes_192_gcm(void) { return &kAes192Gcm; }
+const EVP_AEAD *EVP_aead_aes_256_gcm(void) { return &kAes256Gcm; }
+const EVP_AEAD *EVP_aead_chacha20_poly1305(void) { return &kChaChaPoly; }
+const EVP_AEAD *EVP_aead_aes_128_gcm_tls12(void) { return &kAes128GcmTls12; }
+const EVP_AEAD *EVP_aead_aes_256_gcm_tls12(void) { return &kAes256GcmTls12; }
+const EVP_AEAD *EVP_aead_aes_128_gcm_tls13(void) { return &kAes128GcmTls13; }
+const EVP_AEAD *EVP_aead_aes_256_gcm_tls13(void) { return &kAes256GcmTls13; }
+
+size_t EVP_AEAD_key_length(const EVP_AEAD *aead) { return aead->key_len; }
+size_t EVP_AEAD_nonce_length(const EVP_AEAD *aead) { return aead->nonce_len; }
+size_t EVP_AEAD_max_overhead(const EVP_AEAD *aead) { return aead->overhead; }
+size_t EVP_AEAD_max_tag_len(const EVP_AEAD *aead) { return aead->max_tag_len; }
+
+void EVP_AEAD_CTX_zero(EVP_AEAD_CTX *ctx) { memset(ctx, 0, sizeof(*ctx)); }
+
+EVP_AEAD_CTX *EVP_AEAD_CTX_new(const EVP_AEAD *aead, const uint8_t *key, size_t key_len,
+                               size_t tag_len) {
+  EVP_AEAD_CTX *ctx = static_cast<EVP_AEAD_CTX *>(calloc(1, sizeof(EVP_AEAD_CTX)));
+  if (!ctx) return nullptr;
+  if (!EVP_AEAD_CTX_init(ctx, aead, key, key_len, tag_len, nullptr)) {
+    free(ctx);
+    return nullptr;
+  }
+  return ctx;
+}
+
+void EVP_AEAD_CTX_free(EVP_AEAD_CTX *ctx) {
+  if (!ctx) return;
+  EVP_AEAD_CTX_cleanup(ctx);
+  free(ctx);
+}
+
+int EVP_AEAD_CTX_init(EVP_AEAD_CTX *ctx, const EVP_AEAD *aead, const uint8_t *key,
+                      size_t key_len, size_t tag_len, ENGINE *impl) {
+  (void)impl;
+  return EVP_AEAD_CTX_init_with_direction(ctx, aead, key, key_len, tag_len, evp_aead_open);
+}
+
+int EVP_AEAD_CTX_init_with_direction(EVP_AEAD_CTX *ctx, const EVP_AEAD *aead,
+                                     const uint8_t *key, size_t key_len, size_t tag_len,
+                                     enum evp_aead_direction_t dir) {
+  (void)dir;
+  // aead.cc.inc:82-106
+  if (key_len != aead->key_len) {
+    PUT_ERROR(CIPHER_R_UNSUPPORTED_KEY_SIZE);
+    ctx->aead = nullptr;
+    return 0;
+  }
+  // e_aes.cc.inc:742-749 / e_chacha20poly1305.cc:51-57
+  if (tag_len == EVP_AEAD_DEFAULT_TAG_LENGTH) tag_len = aead->max_tag_len;
+  if (tag_len > aead->max_tag_len) {
+    PUT_ERROR(aead->kind == kAeadAesGcm ? CIPHER_R_TAG_TOO_LARGE : CIPHER_R_TOO_LARGE);
+    ctx->aead = nullptr;
+    return 0;
+  }
+  KeyMaterial *km = make_keys(aead, key, 1);
+  if (!km) {
+    PUT_ERROR(ERR_R_MALLOC_FAILURE);
+    ctx->aead = nullptr;
+    return 0;
+  }
+  memset(&ctx->state, 0, sizeof(ctx->state));
+  CtxState *st = state_of(ctx);
+  st->km = km;
+  ctx->aead = aead;
+  ctx->tag_len = (uint8_t)tag_len;
+  return 1;
+}
+
+void EVP_AEAD_CTX_cleanup(EVP_AEAD_CTX *ctx) {
+  if (ctx->aead == nullptr) return;
+  free_keys(state_of(ctx)->km);
+  state_of(ctx)->km = nullptr;
+  ctx->aead = nullptr;
+}
+
+const EVP_AEAD *EVP_AEAD_CTX_aead(const EVP_AEAD_CTX *ctx) { return ctx->aead; }
+
+// aead.cc.inc:316-361
+int EVP_AEAD_CTX_sealv(const EVP_AEAD_CTX *ctx, const CRYPTO_IOVEC *iovec, size_t num_iovec,
+                       uint8_t *out_tag, size_t *out_tag_len, size_t max_out_tag_len,
+                       const uint8_t *nonce, size_t nonce_len, const CRYPTO_IVEC *aadvec,
+                       size_t num_aadvec) {
+  bool ok = false;
+  size_t total = 0, ad_total = 0;
+  struct Cleanup {
+    bool &ok;
+    const CRYPTO_IOVEC *v;
+    size_t n;
+    uint8_t *tag;
+    size_t tag_max;
+    size_t *tag_len;
+    ~Cleanup() {
+      if (!ok) {
+        clear_iovec(v, n);
+        if (tag_max) memset(tag, 0, tag_max);
+        *tag_len = 0;
+      }
+    }
+  } cleanup{ok, iovec, num_iovec, out_tag, max_out_tag_len, out_tag_len};
+
+  if (!iovec_total(iovec, num_iovec, &total) || !ivec_total(aadvec, num_aadvec, &ad_total)) {
+    PUT_ERROR(CIPHER_R_TOO_LARGE);
+    return 0;
+  }
+  if (!iovec_internal_alias_ok(iovec, num_iovec)) {
+    PUT_ERROR(CIPHER_R_OUTPUT_ALIASES_INPUT);
+    return 0;
+  }
+  for (size_t i = 0; i < num_iovec; i++)
+    if (buffers_alias(iovec[i].out, iovec[i].len, out_tag, max_out_tag_len)) {
+      PUT_ERROR(CIPHER_R_OUTPUT_ALIASES_INPUT);
+      return 0;
+    }
+  if (max_out_tag_len < ctx->tag_len) {  // e_aes.cc.inc:785-788
+    PUT_ERROR(CIPHER_R_BUFFER_TOO_SMALL);
+    return 0;
+  }
+  if (ctx->aead->tls) {
+    if (!tls_nonce_check(ctx, nonce, nonce_len)) return 0;
+  } else if (!aead_record_checks(ctx, nonce_len, total)) {
+    return 0;
+  }
+  std::vector<uint8_t> in = gather_in(iovec, num_iovec, total);
+  std::vector<uint8_t> ad = gather_ad(aadvec, num_aadvec, ad_total);
+  uint8_t tag[16];
+  if (!one_record(ctx, false, in.data(), in.data(), total, nonce, nonce_len, ad.data(),
+                  ad_total, tag, ctx->tag_len))
+    return 0;
+  scatter_out(iovec, num_iovec, in.data(), total);
+  memcpy(out_tag, tag, ctx->tag_len);
+  *out_tag_len = ctx->tag_len;
+  ok = true;
+  return 1;
+}
+
+// aead.cc.inc:531-584
+int EVP_AEAD_CTX_openv_detached(const EVP_AEAD_CTX *ctx, const CRYPTO_IOVEC *iovec,
+                                size_t num_iovec, const uint8_t *nonce, size_t nonce_len,
+                                const uint8_t *in_tag, size_t in_tag_len,
+                                const CRYPTO_IVEC *aadvec, size_t num_aadvec) {
+  bool ok = false;
+  struct Cleanup {
+    bool &ok;
+    const CRYPTO_IOVEC *v;
+    size_t n;
+    ~Cleanup() {
+      if (!ok) clear_iovec(v, n);
+    }
+  } cleanup{ok, iovec, num_iovec};
+  size_t total = 0, ad_total = 0;
+  if (!iovec_total(iovec, num_iovec, &total) || !ivec_total(aadvec, num_aadvec, &ad_total)) {
+    PUT_ERROR(CIPHER_R_TOO_LARGE);
+    return 0;
+  }
+  if (in_tag_len > EVP_AEAD_MAX_OPEN_OVERHEAD) {
+    PUT_ERROR(CIPHER_R_UNSUPPORTED_TAG_SIZE);
+    return 0;
+  }
+  if (!iovec_internal_alias_ok(iovec, num_iovec)) {
+    PUT_ERROR(CIPHER_R_OUTPUT_ALIASES_INPUT);
+    return 0;
+  }
+  if (ctx->aead->kind == kAeadAesGcm) {
+    if (nonce_len == 0) {
+      PUT_ERROR(CIPHER_R_INVALID_NONCE_SIZE);
+      return 0;
+    }
+    if (ctx->aead->tls && nonce_len != 12) {
+      // The tls variants share aead_aes_gcm_openv_detached, which accepts any
+      // non-empty nonce (e_aes.cc.inc:869-882).
+    }
+  } else if (!aead_record_checks(ctx, nonce_len, total)) {
+    return 0;
+  }
+  if (in_tag_len != ctx->tag_len) {  // e_aes.cc.inc:838-841
+    PUT_ERROR(CIPHER_R_BAD_DECRYPT);
+    return 0;
+  }
+  std::vector<uint8_t> in = gather_in(iovec, num_iovec, total);
+  std::vector<uint8_t> ad = gather_ad(aadvec, num_aadvec, ad_total);
+  uint8_t tag[16];
+  memcpy(tag, in_tag, in_tag_len);
+  if (!one_record(ctx, true, in.data(), in.data(), total, nonce, nonce_len, ad.data(),
+                  ad_total, tag, in_tag_len))
+    return 0;
+  scatter_out(iovec, num_iovec, in.data(), total);
+  ok = true;
+  return 1;
+}
+
+// aead.cc.inc:460-529 (the openv_detached fallback with the tag as a suffix).
+int EVP_AEAD_CTX_openv(const EVP_AEAD_CTX *ctx, const CRYPTO_IOVEC *iovec, size_t num_iovec,
+                       size_t *out_total_bytes, const uint8_t *nonce, size_t nonce_len,
+                       const CRYPTO_IVEC *aadvec, size_t num_aadvec) {
+  bool ok = false;
+  struct Cleanup {
+    bool &ok;
+    const CRYPTO_IOVEC *v;
+    size_t n;
+    size_t *out;
+    ~Cleanup() {
+      if (!ok) {
+        clear_iovec(v, n);
+        *out = 0;
+      }
+    }
+  } cleanup{ok, iovec, num_iovec, out_total_bytes};
+  size_t total = 0, ad_total = 0;
+  if (!iovec_total(iovec, num_iovec, &total) || !ivec_total(aadvec, num_aadvec, &ad_total)) {
+    PUT_ERROR(CIPHER_R_TOO_LARGE);
+    return 0;
+  }
+  if (!iovec_internal_alias_ok(iovec, num_iovec)) {
+    PUT_ERROR(CIPHER_R_OUTPUT_ALIASES_INPUT);
+    return 0;
+  }
+  if (total < ctx->tag_len) {
+    PUT_ERROR(CIPHER_R_BAD_DECRYPT);
+    return 0;
+  }
+  std::vector<uint8_t> in = gather_in(iovec, num_iovec, total);
+  const size_t pt_len = total - ctx->tag_len;
+  // Split the iovecs at pt_len: the plaintext goes to the prefix of the
+  // output space (aead.cc.inc:488-512).
+  std::vector<CRYPTO_IOVEC> det;
+  size_t o = 0;
+  for (size_t i = 0; i < num_iovec && o < pt_len; i++) {
+    CRYPTO_IOVEC v = iovec[i];
+    if (v.len > pt_len - o) v.len = pt_len - o;
+    det.push_back(v);
+    o += v.len;
+  }
+  // Build detached iovecs that read from the gathered copy (the tag bytes may
+  // sit in an iovec that is also written).
+  std::vector<CRYPTO_IOVEC> det2 = det;
+  o = 0;
+  for (auto &v : det2) {
+    v.in = in.data() + o;
+    o += v.len;
+  }
+  if (!EVP_AEAD_CTX_openv_detached(ctx, det2.data(), det2.size(), nonce, nonce_len,
+                                   in.data() + pt_len, ctx->tag_len, aadvec, num_aadvec))
+    return 0;
+  *out_total_bytes = pt_len;
+  ok = true;
+  return 1;
+}
+
+// aead.cc.inc:127-161
+int EVP_AEAD_CTX_seal(const EVP_AEAD_CTX *ctx, uint8_t *out, size_t *out_len,
+                      size_t max_out_len, const uint8_t *nonce, size_t nonce_len,
+                      const uint8_t *in, size_t in_len, const uint8_t *ad, size_t ad_len) {
+  bool ok = false;
+  struct Cleanup {
+    bool &ok;
+    uint8_t *out;
+    size_t max;
+    size_t *len;
+    ~Cleanup() {
+      if (!ok) {
+        if (max) memset(out, 0, max);
+        *len = 0;
+      }
+    }
+  } cleanup{ok, out, max_out_len, out_len};
+  if (max_out_len < in_len) {
+    PUT_ERROR(CIPHER_R_BUFFER_TOO_SMALL);
+    return 0;
+  }
+  CRYPTO_IOVEC iov = {out, in, in_len};
+  CRYPTO_IVEC aiv = {ad, ad_len};
+  if (!EVP_AEAD_CTX_sealv(ctx, &iov, 1, out + in_len, out_len, max_out_len - in_len, nonce,
+                          nonce_len, &aiv, 1)) {
+    *out_len = 0;
+    return 0;
+  }
+  *out_len += in_len;
+  ok = true;
+  return 1;
+}
+
+// aead.cc.inc:163-209
+int EVP_AEAD_CTX_seal_scatter(const EVP_AEAD_CTX *ctx, uint8_t *out, uint8_t *out_tag,
+                              size_t *out_tag_len, size_t max_out_tag_len,
+                              const uint8_t *nonce, size_t nonce_len, const uint8_t *in,
+                              size_t in_len, const uint8_t *extra_in, size_t extra_in_len,
+                              const uint8_t *ad, size_t ad_len) {
+  bool ok = false;
+  struct Cleanup {
+    bool &ok;
+    uint8_t *out;
+    size_t in_len;
+    uint8_t *tag;
+    size_t tag_max;
+    size_t *tag_len;
+    ~Cleanup() {
+      if (!ok) {
+        if (in_len) memset(out, 0, in_len);
+        if (tag_max) memset(tag, 0, tag_max);
+        *tag_len = 0;
+      }
+    }
+  } cleanup{ok, out, in_len, out_tag, max_out_tag_len, out_tag_len};
+  if (max_out_tag_len < extra_in_len) {
+    PUT_ERROR(CIPHER_R_BUFFER_TOO_SMALL);
+    return 0;
+  }
+  CRYPTO_IOVEC iov[2] = {{out, in, in_len}, {out_tag, extra_in, extra_in_len}};
+  CRYPTO_IVEC aiv = {ad, ad_len};
+  if (!EVP_AEAD_CTX_sealv(ctx, iov, extra_in_len ? 2 : 1, out_tag + extra_in_len, out_tag_len,
+                          max_out_tag_len - extra_in_len, nonce, nonce_len, &aiv, 1)) {
+    *out_tag_len = 0;
+    return 0;
+  }
+  *out_tag_len += extra_in_len;
+  ok = true;
+  return 1;
+}
+
+// aead.cc.inc:363-428
+int EVP_AEAD_CTX_open(const EVP_AEAD_CTX *ctx, uint8_t *out, size_t *out_len,
+                      size_t max_out_len, const uint8_t *nonce, size_t nonce_len,
+                      const uint8_t *in, size_t in_len, const uint8_t *ad, size_t ad_len) {
+  bool ok = false;
+  struct Cleanup {
+    bool &ok;
+    uint8_t *out;
+    size_t max;
+    size_t *len;
+    ~Cleanup() {
+      if (!ok) {
+        if (max) memset(out, 0, max);
+        *len = 0;
+      }
+    }
+  } cleanup{ok, out, max_out_len, out_len};
+  if (in_len < ctx->tag_len) {
+    PUT_ERROR(CIPHER_R_BAD_DECRYPT);
+    return 0;
+  }
+  size_t pt_len = in_len - ctx->tag_len;
+  if (max_out_len < pt_len) {
+    PUT_ERROR(CIPHER_R_BUFFER_TOO_SMALL);
+    return 0;
+  }
+  CRYPTO_IOVEC iov = {out, in, pt_len};
+  CRYPTO_IVEC aiv = {ad, ad_len};
+  if (!EVP_AEAD_CTX_openv_detached(ctx, &iov, 1, nonce, nonce_len, in + pt_len, ctx->tag_len,
+                                   &aiv, 1))
+    return 0;
+  *out_len = pt_len;
+  ok = true;
+  return 1;
+}
+
+// aead.cc.inc:430-458
+int EVP_AEAD_CTX_open_gather(const EVP_AEAD_CTX *ctx, uint8_t *out, const uint8_t *nonce,
+                             size_t nonce_len, const uint8_t *in, size_t in_len,
+                             const uint8_t *in_tag, size_t in_tag_len, const uint8_t *ad,
+                             size_t ad_len) {
+  bool ok = false;
+  struct Cleanup {
+    bool &ok;
+    uint8_t *out;
+    size_t len;
+    ~Cleanup() {
+      if (!ok && len) memset(out, 0, len);
+    }
+  } cleanup{ok, out, in_len};
+  CRYPTO_IOVEC iov = {out, in, in_len};
+  CRYPTO_IVEC aiv = {ad, ad_len};
+  if (!EVP_AEAD_CTX_openv_detached(ctx, &iov, 1, nonce, nonce_len, in_tag, in_tag_len, &aiv,
+                                   1))
+    return 0;
+  ok = true;
+  return 1;
+}
+
+// aead.cc.inc:598-619
+int EVP_AEAD_CTX_tag_len(const EVP_AEAD_CTX *ctx, size_t *out_tag_len, size_t in_len,
+                         size_t extra_in_len) {
+  (void)in_len;
+  size_t tag_len = ctx->tag_len;
+  if (extra_in_len + tag_len < extra_in_len) {
+    PUT_ERROR(ERR_R_OVERFLOW);
+    *out_tag_len = 0;
+    return 0;
+  }
+  *out_tag_len = extra_in_len + tag_len;
+  return 1;
+}
+
+// aead.cc.inc:586-596: none of the AEADs here implement get_iv.
+int EVP_AEAD_CTX_get_iv(const EVP_AEAD_CTX *ctx, const uint8_t **out_iv, size_t *out_len) {
+  (void)ctx;
+  (void)out_iv;
+  (void)out_len;
+  PUT_ERROR(ERR_R_SHOULD_NOT_HAVE_BEEN_CALLED);
+  return 0;
+}
+
+// ---- batch extension --------------------------------------------------------
+
+int EVP_AEAD_CTX_seal_batch_device(const EVP_AEAD_CTX *ctx, const BSSL_AMD_BATCH *batch,
+                                   void *hip_stream) {
+  if (!ctx || !ctx->aead || !check_batch(ctx->aead, batch)) return 0;
+  if (batch->num_records == 0) return 1;
+  return run_batch(state_of(ctx)->km, ctx->tag_len, batch, false, false, hip_stream);
+}
+
+int EVP_AEAD_CTX_open_batch_device(const EVP_AEAD_CTX *ctx, const BSSL_AMD_BATCH *batch,
+                                   void *hip_stream) {
+  if (!ctx || !ctx->aead || !check_batch(ctx->aead, batch)) return 0;
+  if (batch->num_records == 0) return 1;
+  return run_batch(state_of(ctx)->km, ctx->tag_len, batch, true, false, hip_stream);
+}
+
+struct bssl_amd_keyset_st {
+  KeyMaterial *km;
+  size_t tag_len;
+};
+
+BSSL_AMD_KEYSET *BSSL_AMD_KEYSET_new(const EVP_AEAD *aead, const uint8_t *keys,
+                                     size_t num_keys, size_t tag_len) {
+  if (!aead || !keys || num_keys == 0 || num_keys > 0xfffffffeu) {
+    PUT_ERROR(ERR_R_SHOULD_NOT_HAVE_BEEN_CALLED);
+    return nullptr;
+  }
+  if (tag_len == EVP_AEAD_DEFAULT_TAG_LENGTH) tag_len = aead->max_tag_len;
+  if (tag_len > aead->max_tag_len) {
+    PUT_ERROR(CIPHER_R_TAG_TOO_LARGE);
+    return nullptr;
+  }
+  KeyMaterial *km = make_keys(aead, keys, num_keys);
+  if (!km) {
+    PUT_ERROR(ERR_R_MALLOC_FAILURE);
+    return nullptr;
+  }
+  BSSL_AMD_KEYSET *ks = new (std::nothrow) bssl_amd_keyset_st{km, tag_len};
+  if (!ks) free_keys(km);
+  return ks;
+}
+
+void BSSL_AMD_KEYSET_free(BSSL_AMD_KEYSET *ks) {
+  if (!ks) return;
+  free_keys(ks->km);
+  delete ks;
+}
+
+size_t BSSL_AMD_KEYSET_num_keys(const BSSL_AMD_KEYSET *ks) { return ks ? ks->km->num_keys : 0; }
+
+int BSSL_AMD_KEYSET_seal_batch_device(const BSSL_AMD_KEYSET *ks, const BSSL_AMD_BATCH *batch,
+                                      void *hip_stream) {
+  if (!ks || !check_batch(ks->km->aead, batch)) return 0;
+  if (batch->num_records == 0) return 1;
+  return run_batch(ks->km, ks->tag_len, batch, false, true, hip_stream);
+}
+
+int BSSL_AMD_KEYSET_open_batch_device(const BSSL_AMD_KEYSET *ks, const BSSL_AMD_BATCH *batch,
+                                      void *hip_stream) {
+  if (!ks || !check_batch(ks->km->aead, batch)) return 0;
+  if (batch->num_records == 0) return 1;
+  return run_batch(ks->km, ks->tag_len, batch, true, true, hip_stream);
+}
+
+int BSSL_AMD_set_device(int device) { return hipSetDevice(device) == hipSuccess; }
+
+int BSSL_AMD_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int BSSL_AMD_synth_fill_device(uint64_t first_record, size_t n, const uint64_t *offsets,
+                               const uint64_t *lengths, uint8_t *pt, uint8_t *nonces,
+                               uint8_t *ads, void *hip_stream) {
+  return launch_synth(first_record, n, offsets, lengths, pt, nonces, ads, hip_stream) == 0;
+}
+
+void BSSL_AMD_set_kernel_timing(int enable) { t_timing = enable != 0; }
+double BSSL_AMD_last_kernel_ms(void) { return t_last_ms; }
+const char *BSSL_AMD_last_kernel_name(void) { return t_last_name; }
+
+}  // extern "C"

@@ -1,0 +1,431 @@
+// chacha.hip -- ChaCha20-Poly1305 seal/open over device-resident record
+// batches (gfx950).
+//
+// Replaces chacha20_poly1305_sealv / _openv_detached
+// (crypto/cipher/e_chacha20poly1305.cc:117-333) -> CRYPTO_chacha_20
+// (crypto/chacha/chacha.cc:100-224) + CRYPTO_poly1305_* (crypto/poly1305/
+// poly1305.cc) / the fused chacha20_poly1305_seal_avx2 (chacha20_poly1305_
+// x86_64.pl:861).  Design:
+//
+// * 16 lanes per record, 4 records per wave.  Lane q owns the record's 64-byte
+//   ChaCha blocks u = q, q+16, ... (block counter 1+u, RFC 8439): one lane per
+//   64-byte block, keystream XORed with the input in registers.
+// * Poly1305: the four 16-byte Poly blocks of ChaCha block u form one unit
+//   U_u = ((M0 r + M1) r + M2) r + M3.  A lane folds its units with Horner's
+//   rule in R = r^4 at stride 16 (multiplier R^16 = r^64); the 16 lane
+//   accumulators are rotated into exponent order and tree-combined with R,
+//   R^2, R^4, R^8 -- the same lane algebra as the GHASH of gcm.hip, here in
+//   GF(2^130-5) with 26-bit limbs.  A trailing partial unit and the AD are
+//   folded in afterwards; the tag is (((Z r) + L) r mod p + s) mod 2^128.
+#include <hip/hip_runtime.h>
+
+#include "internal.h"
+
+namespace bssl_amd {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kRecPerBlock = kThreads / 16;
+constexpr uint32_t kM26 = 0x3ffffff;
+
+__device__ __forceinline__ uint32_t rotl(uint32_t v, int n) {
+  return __builtin_amdgcn_alignbit(v, v, 32 - n);
+}
+
+struct ChaState {
+  uint32_t x[16];
+};
+
+#define QR(a, b, c, d)                 \
+  a += b; d = rotl(d ^ a, 16);         \
+  c += d; b = rotl(b ^ c, 12);         \
+  a += b; d = rotl(d ^ a, 8);          \
+  c += d; b = rotl(b ^ c, 7);
+
+__device__ __forceinline__ void chacha_block(const uint32_t key[8], uint32_t ctr,
+                                             const uint32_t nonce[3], uint32_t out[16]) {
+  uint32_t x0 = 0x61707865, x1 = 0x3320646e, x2 = 0x79622d32, x3 = 0x6b206574;
+  uint32_t x4 = key[0], x5 = key[1], x6 = key[2], x7 = key[3];
+  uint32_t x8 = key[4], x9 = key[5], x10 = key[6], x11 = key[7];
+  uint32_t x12 = ctr, x13 = nonce[0], x14 = nonce[1], x15 = nonce[2];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    QR(x0, x4, x8, x12) QR(x1, x5, x9, x13) QR(x2, x6, x10, x14) QR(x3, x7, x11, x15)
+    QR(x0, x5, x10, x15) QR(x1, x6, x11, x12) QR(x2, x7, x8, x13) QR(x3, x4, x9, x14)
+  }
+  out[0] = x0 + 0x61707865;
+  out[1] = x1 + 0x3320646e;
+  out[2] = x2 + 0x79622d32;
+  out[3] = x3 + 0x6b206574;
+  out[4] = x4 + key[0];
+  out[5] = x5 + key[1];
+  out[6] = x6 + key[2];
+  out[7] = x7 + key[3];
+  out[8] = x8 + key[4];
+  out[9] = x9 + key[5];
+  out[10] = x10 + key[6];
+  out[11] = x11 + key[7];
+  out[12] = x12 + ctr;
+  out[13] = x13 + nonce[0];
+  out[14] = x14 + nonce[1];
+  out[15] = x15 + nonce[2];
+}
+
+// ---------------------------------------------------------------------------
+// Poly1305 arithmetic modulo 2^130 - 5, radix 2^26.
+struct P {
+  uint32_t h[5];
+};
+
+__device__ __forceinline__ P pzero() { return P{{0, 0, 0, 0, 0}}; }
+
+__device__ __forceinline__ P padd(P a, const P &b) {
+#pragma unroll
+  for (int i = 0; i < 5; i++) a.h[i] += b.h[i];
+  return a;
+}
+
+// Block (16 bytes as 4 LE words) plus 2^128.
+__device__ __forceinline__ P pblock(uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3) {
+  P m;
+  m.h[0] = t0 & kM26;
+  m.h[1] = ((t0 >> 26) | (t1 << 6)) & kM26;
+  m.h[2] = ((t1 >> 20) | (t2 << 12)) & kM26;
+  m.h[3] = ((t2 >> 14) | (t3 << 18)) & kM26;
+  m.h[4] = (t3 >> 8) | (1u << 24);
+  return m;
+}
+
+__device__ __forceinline__ uint64_t mul64(uint32_t a, uint32_t b) { return (uint64_t)a * b; }
+
+// a * r mod p (partially reduced; limbs < 2^26 except h1 < 2^26 + 2^7).
+__device__ __forceinline__ P pmul(const P &a, const P &r) {
+  const uint32_t s1 = r.h[1] * 5, s2 = r.h[2] * 5, s3 = r.h[3] * 5, s4 = r.h[4] * 5;
+  uint64_t d0 = mul64(a.h[0], r.h[0]) + mul64(a.h[1], s4) + mul64(a.h[2], s3) +
+                mul64(a.h[3], s2) + mul64(a.h[4], s1);
+  uint64_t d1 = mul64(a.h[0], r.h[1]) + mul64(a.h[1], r.h[0]) + mul64(a.h[2], s4) +
+                mul64(a.h[3], s3) + mul64(a.h[4], s2);
+  uint64_t d2 = mul64(a.h[0], r.h[2]) + mul64(a.h[1], r.h[1]) + mul64(a.h[2], r.h[0]) +
+                mul64(a.h[3], s4) + mul64(a.h[4], s3);
+  uint64_t d3 = mul64(a.h[0], r.h[3]) + mul64(a.h[1], r.h[2]) + mul64(a.h[2], r.h[1]) +
+                mul64(a.h[3], r.h[0]) + mul64(a.h[4], s4);
+  uint64_t d4 = mul64(a.h[0], r.h[4]) + mul64(a.h[1], r.h[3]) + mul64(a.h[2], r.h[2]) +
+                mul64(a.h[3], r.h[1]) + mul64(a.h[4], r.h[0]);
+  P o;
+  uint64_t c;
+  o.h[0] = (uint32_t)d0 & kM26;
+  c = d0 >> 26;
+  d1 += c;
+  o.h[1] = (uint32_t)d1 & kM26;
+  c = d1 >> 26;
+  d2 += c;
+  o.h[2] = (uint32_t)d2 & kM26;
+  c = d2 >> 26;
+  d3 += c;
+  o.h[3] = (uint32_t)d3 & kM26;
+  c = d3 >> 26;
+  d4 += c;
+  o.h[4] = (uint32_t)d4 & kM26;
+  c = d4 >> 26;
+  uint64_t h0 = (uint64_t)o.h[0] + c * 5;
+  o.h[0] = (uint32_t)h0 & kM26;
+  o.h[1] += (uint32_t)(h0 >> 26);
+  return o;
+}
+
+__device__ __forceinline__ P pshfl(const P &v, int src, int width) {
+  P o;
+#pragma unroll
+  for (int i = 0; i < 5; i++) o.h[i] = __shfl(v.h[i], src, width);
+  return o;
+}
+
+__device__ __forceinline__ P pshfl_down(const P &v, int d, int width) {
+  P o;
+#pragma unroll
+  for (int i = 0; i < 5; i++) o.h[i] = __shfl_down(v.h[i], d, width);
+  return o;
+}
+
+// Tree-combine the 16 lane accumulators of a group (see gcm.hip
+// group_combine); pw[t] = base^(2^t).  All 64 lanes must call it.
+__device__ __forceinline__ P group_combine(const P &acc, int q, int src, const P pw[4]) {
+  P a = pshfl(acc, src, 16);
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    const int s = 1 << t;
+    P m = pmul(a, pw[t]);
+    P o = pshfl_down(a, s, 16);
+    if ((q & (2 * s - 1)) == 0) a = padd(m, o);
+  }
+  return pshfl(a, 0, 16);
+}
+
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ uint32_t load_le32_bytes(const uint8_t *p, uint64_t avail) {
+  uint32_t v = 0;
+  for (int i = 0; i < 4; i++)
+    if ((uint64_t)i < avail) v |= (uint32_t)p[i] << (8 * i);
+  return v;
+}
+
+// Final reduction and tag: (h mod p + s) mod 2^128 (poly1305.cc:255-313).
+__device__ void poly_finish(P h, const uint32_t s[4], uint32_t tag[4]) {
+  uint32_t c;
+  c = h.h[1] >> 26; h.h[1] &= kM26; h.h[2] += c;
+  c = h.h[2] >> 26; h.h[2] &= kM26; h.h[3] += c;
+  c = h.h[3] >> 26; h.h[3] &= kM26; h.h[4] += c;
+  c = h.h[4] >> 26; h.h[4] &= kM26; h.h[0] += c * 5;
+  c = h.h[0] >> 26; h.h[0] &= kM26; h.h[1] += c;
+  c = h.h[1] >> 26; h.h[1] &= kM26; h.h[2] += c;
+  c = h.h[2] >> 26; h.h[2] &= kM26; h.h[3] += c;
+  c = h.h[3] >> 26; h.h[3] &= kM26; h.h[4] += c;
+  c = h.h[4] >> 26; h.h[4] &= kM26; h.h[0] += c * 5;
+  c = h.h[0] >> 26; h.h[0] &= kM26; h.h[1] += c;
+  // g = h + 5 - 2^130
+  uint32_t g0 = h.h[0] + 5; c = g0 >> 26; g0 &= kM26;
+  uint32_t g1 = h.h[1] + c; c = g1 >> 26; g1 &= kM26;
+  uint32_t g2 = h.h[2] + c; c = g2 >> 26; g2 &= kM26;
+  uint32_t g3 = h.h[3] + c; c = g3 >> 26; g3 &= kM26;
+  uint32_t g4 = h.h[4] + c - (1u << 26);
+  uint32_t mask = (g4 >> 31) - 1;  // all ones if h >= p
+  h.h[0] = (h.h[0] & ~mask) | (g0 & mask);
+  h.h[1] = (h.h[1] & ~mask) | (g1 & mask);
+  h.h[2] = (h.h[2] & ~mask) | (g2 & mask);
+  h.h[3] = (h.h[3] & ~mask) | (g3 & mask);
+  h.h[4] = (h.h[4] & ~mask) | (g4 & mask);
+  uint32_t w0 = h.h[0] | (h.h[1] << 26);
+  uint32_t w1 = (h.h[1] >> 6) | (h.h[2] << 20);
+  uint32_t w2 = (h.h[2] >> 12) | (h.h[3] << 14);
+  uint32_t w3 = (h.h[3] >> 18) | (h.h[4] << 8);
+  uint64_t f = (uint64_t)w0 + s[0];
+  tag[0] = (uint32_t)f;
+  f = (uint64_t)w1 + s[1] + (f >> 32);
+  tag[1] = (uint32_t)f;
+  f = (uint64_t)w2 + s[2] + (f >> 32);
+  tag[2] = (uint32_t)f;
+  f = (uint64_t)w3 + s[3] + (f >> 32);
+  tag[3] = (uint32_t)f;
+}
+
+struct RecordMeta {
+  uint64_t off, len, ad_off, ad_len;
+};
+
+template <bool OPEN>
+__global__ __launch_bounds__(kThreads) void chacha_poly_kernel(
+    const ChaChaKeyDev *__restrict__ keys, BatchDesc b) {
+  const int lane = threadIdx.x & 63;
+  const int q = lane & 15;
+  const uint64_t rec = (uint64_t)blockIdx.x * kRecPerBlock + (threadIdx.x >> 4);
+  const bool active = rec < b.num_records;
+  RecordMeta m = {0, 0, 0, 0};
+  uint32_t kidx = 0;
+  if (active) {
+    m.off = b.offsets ? b.offsets[rec] : rec * b.record_stride;
+    m.len = b.lengths ? b.lengths[rec] : b.record_len;
+    m.ad_off = b.ad_offsets ? b.ad_offsets[rec] : rec * b.ad_stride;
+    m.ad_len = b.ad_lengths ? b.ad_lengths[rec] : b.ad_len;
+    kidx = b.key_index ? b.key_index[rec] : 0u;
+  }
+  // e_chacha20poly1305.cc:127-142: 12-byte nonce, < 2^32 - 1 blocks.
+  const bool bad = active && (kidx >= b.num_keys || b.nonce_len != 12 ||
+                              m.len >= (uint64_t(1) << 32) * 64 - 64);
+  const bool live = active && !bad;
+  uint32_t key[8], nonce[3];
+  {
+    const ChaChaKeyDev *kp = keys + (live ? kidx : 0u);
+#pragma unroll
+    for (int i = 0; i < 8; i++) key[i] = kp->k[i];
+    const uint8_t *np = b.nonces + (live ? rec * 12 : 0);
+#pragma unroll
+    for (int i = 0; i < 3; i++) nonce[i] = load_le32_bytes(np + 4 * i, live ? 4 : 0);
+  }
+
+  // Poly1305 key = ChaCha20(counter 0)[0:32] (e_chacha20poly1305.cc:89-93).
+  P r, pw_r[4], pw_R[4], r64;
+  uint32_t s[4];
+  {
+    uint32_t ks[16];
+    chacha_block(key, 0, nonce, ks);
+    const uint32_t t0 = ks[0] & 0x0fffffff, t1 = ks[1] & 0x0ffffffc, t2 = ks[2] & 0x0ffffffc,
+                   t3 = ks[3] & 0x0ffffffc;  // clamp (RFC 8439 2.5)
+    r.h[0] = t0 & kM26;
+    r.h[1] = ((t0 >> 26) | (t1 << 6)) & kM26;
+    r.h[2] = ((t1 >> 20) | (t2 << 12)) & kM26;
+    r.h[3] = ((t2 >> 14) | (t3 << 18)) & kM26;
+    r.h[4] = t3 >> 8;
+    s[0] = ks[4];
+    s[1] = ks[5];
+    s[2] = ks[6];
+    s[3] = ks[7];
+    pw_r[0] = r;
+    pw_r[1] = pmul(r, r);                // r^2
+    pw_r[2] = pmul(pw_r[1], pw_r[1]);    // r^4
+    pw_r[3] = pmul(pw_r[2], pw_r[2]);    // r^8
+    pw_R[0] = pw_r[2];                   // R = r^4
+    pw_R[1] = pw_r[3];                   // R^2 = r^8
+    pw_R[2] = pmul(pw_R[1], pw_R[1]);    // R^4 = r^16
+    pw_R[3] = pmul(pw_R[2], pw_R[2]);    // R^8 = r^32
+    r64 = pmul(pw_R[3], pw_R[3]);        // R^16 = r^64
+  }
+
+  // AD: exclusive Horner in r over the zero-padded 16-byte blocks.
+  P ya = pzero();
+  {
+    const uint8_t *ad = b.ad + (live ? m.ad_off : 0);
+    const uint64_t nab = live ? (m.ad_len + 15) / 16 : 0;
+    const int wmax = wave_max((int)min<uint64_t>(nab, 0x7fffffff));
+    auto ad_block = [&](uint64_t k) {
+      const uint8_t *p = ad + 16 * k;
+      const uint64_t avail = m.ad_len - 16 * k;
+      return pblock(load_le32_bytes(p, avail), load_le32_bytes(p + 4, avail > 4 ? avail - 4 : 0),
+                    load_le32_bytes(p + 8, avail > 8 ? avail - 8 : 0),
+                    load_le32_bytes(p + 12, avail > 12 ? avail - 12 : 0));
+    };
+    if (wmax <= 1) {
+      if (nab == 1) ya = ad_block(0);
+    } else {
+      P acc = pzero();
+      for (uint64_t k = q; k < nab; k += 16) acc = padd(pmul(acc, pw_R[2]), ad_block(k));
+      const int rr = (int)(nab & 15);
+      ya = group_combine(acc, q, (q + rr) & 15, pw_r);
+    }
+  }
+
+  // Bulk: ChaCha20 blocks 1.. and Poly1305 units.
+  const uint64_t nblk = live ? (m.len + 63) / 64 : 0;  // ChaCha data blocks
+  const uint64_t npoly = live ? (m.len + 15) / 16 : 0;
+  const uint64_t nunits = npoly / 4;                   // full 4-block units
+  const uint32_t tail_blocks = (uint32_t)(npoly & 3);
+  const uint8_t *src = b.in + m.off;
+  uint8_t *dst = b.out + m.off;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(src) |
+                         reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+  P acc = (q == 15 && live) ? ya : pzero();
+  P tail = pzero();
+  const int iters = wave_max((int)((nblk + 15) / 16));
+  for (int it = 0; it < iters; it++) {
+    const uint64_t u = (uint64_t)it * 16 + q;
+    uint32_t ks[16];
+    chacha_block(key, (uint32_t)(1 + u), nonce, ks);
+    if (u < nblk) {
+      const uint64_t rem = m.len - 64 * u;
+      uint32_t x[16], y[16];
+      if (rem >= 64 && aligned) {
+        const uint4 *sp = reinterpret_cast<const uint4 *>(src + 64 * u);
+        uint4 *dp = reinterpret_cast<uint4 *>(dst + 64 * u);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          uint4 v = sp[i];
+          x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) y[i] = x[i] ^ ks[i];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          dp[i] = make_uint4(y[4 * i], y[4 * i + 1], y[4 * i + 2], y[4 * i + 3]);
+      } else {
+        const uint8_t *sp = src + 64 * u;
+        uint8_t *dp = dst + 64 * u;
+        const uint32_t n = (uint32_t)min<uint64_t>(rem, 64);
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+          x[i] = load_le32_bytes(sp + 4 * i, n > 4u * i ? n - 4u * i : 0);
+          uint32_t mask = n >= 4u * i + 4 ? 0xffffffffu
+                          : n <= 4u * i   ? 0u
+                                          : ((1u << (8 * (n - 4 * i))) - 1u);
+          y[i] = (x[i] ^ ks[i]) & mask;
+        }
+        for (uint32_t i = 0; i < n; i++) dp[i] = (uint8_t)(y[i >> 2] >> (8 * (i & 3)));
+      }
+      const uint32_t *c = OPEN ? x : y;
+      if (u < nunits) {
+        P unit = pblock(c[0], c[1], c[2], c[3]);
+        unit = padd(pmul(unit, r), pblock(c[4], c[5], c[6], c[7]));
+        unit = padd(pmul(unit, r), pblock(c[8], c[9], c[10], c[11]));
+        unit = padd(pmul(unit, r), pblock(c[12], c[13], c[14], c[15]));
+        acc = padd(pmul(acc, r64), unit);
+      } else {
+        // Trailing partial unit: tail_blocks (1..3) Poly blocks.
+        P tt = pblock(c[0], c[1], c[2], c[3]);
+        for (uint32_t k = 1; k < tail_blocks; k++)
+          tt = padd(pmul(tt, r), pblock(c[4 * k], c[4 * k + 1], c[4 * k + 2], c[4 * k + 3]));
+        tail = tt;
+      }
+    }
+  }
+  const int rw = (int)((nunits + 1) & 15);
+  P z = group_combine(acc, q, (q + rw + 15) & 15, pw_R);
+  // Z = X * r^t + tail, the tail from the lane that owns unit `nunits`.
+  tail = pshfl(tail, (int)(nunits & 15), 16);
+  const int tmax = wave_max((int)tail_blocks);
+  for (int k = 0; k < tmax; k++)
+    if ((uint32_t)k < tail_blocks) z = pmul(z, r);
+  if (tail_blocks) z = padd(z, tail);
+  // h = ((Z r) + L) r with L = le64(ad_len) || le64(ct_len) (+2^128).
+  const P lb = pblock((uint32_t)m.ad_len, (uint32_t)(m.ad_len >> 32), (uint32_t)m.len,
+                      (uint32_t)(m.len >> 32));
+  const P h = pmul(padd(pmul(z, r), lb), r);
+  uint32_t tag[4];
+  poly_finish(h, s, tag);
+
+  uint8_t *tagp = b.tags + rec * b.tag_len;
+  bool ok = live;
+  if (OPEN && live) {
+    uint32_t diff = 0;
+    for (uint32_t i = 0; i < b.tag_len; i++)
+      diff |= ((tag[i >> 2] >> (8 * (i & 3))) & 0xff) ^ tagp[i];
+    ok = diff == 0;  // CRYPTO_memcmp, e_chacha20poly1305.cc:322-326
+  }
+  if (active && q == 0) {
+    if (!OPEN)
+      for (uint32_t i = 0; i < b.tag_len; i++)
+        tagp[i] = ok ? (uint8_t)(tag[i >> 2] >> (8 * (i & 3))) : 0;
+    if (b.status) b.status[rec] = ok ? 1 : 0;
+  }
+  if (active && !ok) {
+    for (uint64_t j = q; j * 16 < m.len; j += 16) {
+      const uint64_t n = min<uint64_t>(m.len - j * 16, 16);
+      for (uint64_t i = 0; i < n; i++) dst[j * 16 + i] = 0;
+    }
+  }
+}
+
+}  // namespace
+
+int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, void *stream,
+                  float *timing_ms) {
+  if (b.num_records == 0) return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (timing_ms) {
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipEventRecord(e0, s);
+  }
+  const uint64_t blocks = (b.num_records + kRecPerBlock - 1) / kRecPerBlock;
+  if (blocks > 0x7fffffffu) return 1;
+  if (open)
+    hipLaunchKernelGGL(chacha_poly_kernel<true>, dim3((unsigned)blocks), dim3(kThreads), 0, s,
+                       keys, b);
+  else
+    hipLaunchKernelGGL(chacha_poly_kernel<false>, dim3((unsigned)blocks), dim3(kThreads), 0, s,
+                       keys, b);
+  int rc = (int)hipGetLastError();
+  if (timing_ms) {
+    hipEventRecord(e1, s);
+    hipEventSynchronize(e1);
+    hipEventElapsedTime(timing_ms, e0, e1);
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+  }
+  return rc;
+}
+
+}  // namespace bssl_amd

@@ -1,0 +1,85 @@
+// internal.h -- definitions shared by the host C-ABI layer and the HIP kernels.
+//
+// Device data layout (all resident in HBM, 16-byte aligned):
+//
+//   GcmKeyDev   one per AES-GCM key (41,216 bytes): the AES round keys and
+//               the GHASH multiplication tables for H, H^2, H^4, H^8, H^16.
+//               Equivalent of the reference's GCM128_KEY
+//               (crypto/fipsmodule/aes/internal.h:325-334), re-laid-out for the
+//               LDS-table GHASH of gcm.hip.
+//   ChaChaKeyDev one per ChaCha20-Poly1305 key (32 bytes).
+//   BatchDesc   the record-batch descriptor passed by value to the kernels.
+#ifndef BSSL_AMD_INTERNAL_H
+#define BSSL_AMD_INTERNAL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+namespace bssl_amd {
+
+// GHASH table powers held per key: kGhashPow[i] = H^(2^i).
+constexpr int kGhashPowers = 5;           // H, H^2, H^4, H^8, H^16
+constexpr int kGhashTableWords = 32 * 16 * 4;  // 32 nibble positions x 16 values x 16 B
+
+struct alignas(16) GcmKeyDev {
+  // Round keys as little-endian words of the FIPS-197 schedule bytes; the
+  // middle rounds (1..nr-1) are stored rotated left by 16 bits, which is how
+  // the T-table round of gcm.hip consumes them.
+  uint32_t rk[15][4];
+  uint32_t nr;
+  uint32_t key_bytes;
+  uint32_t pad[2];
+  // htab[p][pos][v] = (element with nibble `pos` equal to v) * H^(2^p), as 4
+  // little-endian words of the 16 GCM-order bytes.  Nibble position
+  // pos = 2*k + 0 is the high nibble of byte k, 2*k + 1 the low nibble.
+  uint32_t htab[kGhashPowers][32][16][4];
+};
+static_assert(sizeof(GcmKeyDev) == 240 + 16 + kGhashPowers * 8192, "layout");
+
+struct alignas(16) ChaChaKeyDev {
+  uint32_t k[8];
+};
+
+enum AeadKind : int { kAeadAesGcm = 0, kAeadChaChaPoly = 1 };
+
+// Record-batch descriptor (device pointers), see BSSL_AMD_BATCH.
+struct BatchDesc {
+  const uint8_t *in;
+  uint8_t *out;
+  const uint64_t *offsets;
+  const uint64_t *lengths;
+  uint64_t record_stride;
+  uint64_t record_len;
+  const uint8_t *nonces;
+  uint64_t nonce_len;
+  const uint8_t *ad;
+  const uint64_t *ad_offsets;
+  const uint64_t *ad_lengths;
+  uint64_t ad_stride;
+  uint64_t ad_len;
+  uint8_t *tags;
+  uint8_t *status;
+  const uint32_t *key_index;
+  uint64_t num_records;
+  uint32_t tag_len;
+  uint32_t num_keys;
+};
+
+// Kernel launchers (gcm.hip / chacha.hip).  Return 0 on success or a HIP
+// error code.  `timing_ms` (optional) receives the kernel's device time
+// measured with HIP events on `stream`.
+int launch_gcm(const GcmKeyDev *keys, const BatchDesc &b, bool open,
+               int nr, void *stream, float *timing_ms);
+int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open,
+                  void *stream, float *timing_ms);
+int launch_synth(uint64_t first, size_t n, const uint64_t *offsets,
+                 const uint64_t *lengths, uint8_t *pt, uint8_t *nonces,
+                 uint8_t *ads, void *stream);
+
+// Host-side key setup (key_setup.cc).
+bool gcm_key_setup(const uint8_t *key, size_t key_len, GcmKeyDev *out);
+void chacha_key_setup(const uint8_t *key, ChaChaKeyDev *out);
+
+}  // namespace bssl_amd
+
+#endif

@@ -1,0 +1,94 @@
+"""CPU tests of the drop-in boundary: the C-ABI library loads, exports every
+symbol include/bssl_amd/aead.h declares, and the host-side (no-GPU) parts of
+the EVP_AEAD surface behave like the reference (aead.cc.inc:82-106 key-length
+check, e_aes.cc.inc:742-749 tag length, err.h packing, aead.h:204-217 sizes)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "bssl_amd", "aead.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = "\n".join(l for l in text.splitlines() if not l.lstrip().startswith("#"))
+    names = re.findall(r"BSSL_AMD_EXPORT[^;(]*?\b(\w+)\s*\(", text, flags=re.S)
+    return sorted(set(names))
+
+
+def test_header_declares_expected_surface():
+    names = header_functions()
+    for must in ("EVP_AEAD_CTX_seal", "EVP_AEAD_CTX_open", "EVP_AEAD_CTX_seal_scatter",
+                 "EVP_AEAD_CTX_sealv", "EVP_AEAD_CTX_openv_detached",
+                 "EVP_AEAD_CTX_seal_batch_device", "BSSL_AMD_KEYSET_seal_batch_device"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    import boringssl_amd as ba
+    names = header_functions()
+    assert sorted(ba.EXPORTED_SYMBOLS) == names
+    out = subprocess.check_output(["nm", "-D", "--defined-only", ba.LIB_PATH], text=True)
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    # nothing else leaks out of the library except the declared ABI
+    extra = sorted(n for n in exported if not n.startswith("_") and n not in names)
+    assert not extra, extra
+
+
+def test_aead_parameters():
+    import boringssl_amd as ba
+    L = ba.lib
+    for name, key_len in [("aes-128-gcm", 16), ("aes-192-gcm", 24), ("aes-256-gcm", 32),
+                          ("chacha20-poly1305", 32), ("aes-128-gcm-tls13", 16)]:
+        a = ba.EVP_aead(name)
+        assert L.EVP_AEAD_key_length(a) == key_len
+        assert L.EVP_AEAD_nonce_length(a) == 12
+        assert L.EVP_AEAD_max_overhead(a) == 16
+        assert L.EVP_AEAD_max_tag_len(a) == 16
+
+
+def test_init_rejects_bad_key_and_tag_length_without_gpu():
+    import boringssl_amd as ba
+    with pytest.raises(ba.AEADError) as e:
+        ba.AEADCtx("aes-128-gcm", bytes(15))
+    assert e.value.lib == ba.ERR_LIB_CIPHER and e.value.reason == ba.CIPHER_R_UNSUPPORTED_KEY_SIZE
+    with pytest.raises(ba.AEADError) as e:
+        ba.AEADCtx("aes-256-gcm", bytes(32), tag_len=17)
+    assert e.value.reason == ba.CIPHER_R_TAG_TOO_LARGE
+    with pytest.raises(ba.AEADError) as e:
+        ba.AEADCtx("chacha20-poly1305", bytes(32), tag_len=17)
+    assert e.value.reason == ba.CIPHER_R_TOO_LARGE
+    assert ba.lib.ERR_get_error() == 0
+
+
+def test_error_queue_is_bounded_fifo():
+    import boringssl_amd as ba
+    L = ba.lib
+    L.ERR_clear_error()
+    ctx = ba.EVP_AEAD_CTX()
+    for _ in range(20):
+        assert not L.EVP_AEAD_CTX_init(ctypes.byref(ctx), ba.EVP_aead("aes-128-gcm"), bytes(3), 3,
+                                       0, None)
+    n = 0
+    while True:
+        e = L.ERR_get_error()
+        if not e:
+            break
+        assert (e >> 24) == 30 and (e & 0xfff) == ba.CIPHER_R_UNSUPPORTED_KEY_SIZE
+        n += 1
+    assert n == 15  # ERR_NUM_ERRORS - 1 entries retained, as the reference queue
+
+
+def test_zeroed_ctx_cleanup_is_safe():
+    import boringssl_amd as ba
+    ctx = ba.EVP_AEAD_CTX()
+    ba.lib.EVP_AEAD_CTX_zero(ctypes.byref(ctx))
+    ba.lib.EVP_AEAD_CTX_cleanup(ctypes.byref(ctx))
+    ba.lib.EVP_AEAD_CTX_cleanup(ctypes.byref(ctx))

@@ -1,0 +1,348 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the reference's
+own vectors, the reference library's outputs (tests/golden/ref_*.json) and
+the CPU oracle, bit for bit.
+
+Mirrors the reference's test strategy (crypto/cipher/aead_test.cc):
+TestVector (188-281), truncated tags (963-1066), in-place / unaligned
+(1068-1185), Wycheproof (1493-1564); plus batch-level checks at BASELINE
+sizes through digests of the reference outputs (checksum of checksums) and
+open(seal(x)) round trips.
+"""
+import hashlib
+import os
+import random
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import boringssl_amd as ba  # noqa: E402
+import oracle_lib as o  # noqa: E402
+from golden_util import AEAD_KEYLEN, batch_digests, load  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+ORACLE_ID = {"aes-128-gcm": o.AES_GCM, "aes-192-gcm": o.AES_GCM, "aes-256-gcm": o.AES_GCM,
+             "chacha20-poly1305": o.CHACHA20_POLY1305}
+
+
+def _h(s):
+    return bytes.fromhex(s)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+    ba.lib.ERR_clear_error()
+    yield
+    torch.cuda.synchronize()
+
+
+# ---------------------------------------------------------------------------
+# helpers
+
+def _pack(chunks, align=16, odd=0):
+    """Concatenate byte strings into one uint8 array; returns (array, offsets)."""
+    offs, pos = [], odd
+    for c in chunks:
+        offs.append(pos)
+        pos += len(c)
+        pos = (pos + align - 1) // align * align + odd
+    buf = np.zeros(max(pos, 1) + 16, dtype=np.uint8)
+    for off, c in zip(offs, chunks):
+        if c:
+            buf[off:off + len(c)] = np.frombuffer(c, dtype=np.uint8)
+    return buf, np.array(offs, dtype=np.uint64)
+
+
+def _t(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.to(DEV)
+
+
+def run_batch(aead, keys, key_index, ins, nonces, ads, tag_len, open_=False, tags=None,
+              align=16, odd=0, inplace=False):
+    """Seal (or open) records given as Python bytes through the device batch
+    API.  `keys` is a list; records select keys with key_index (None = ctx of
+    keys[0]).  Returns (outs, tags, status)."""
+    n = len(ins)
+    nonce_len = len(nonces[0])
+    assert all(len(x) == nonce_len for x in nonces)
+    inbuf, offs = _pack(ins, align, odd)
+    adbuf, ad_offs = _pack(ads, 1)
+    d_in = _t(inbuf)
+    d_out = d_in if inplace else torch.zeros_like(d_in)
+    d_nonce = _t(np.frombuffer(b"".join(nonces), dtype=np.uint8).copy() if nonce_len else
+                 np.zeros(1, np.uint8))
+    d_ad = _t(adbuf)
+    lens = np.array([len(x) for x in ins], dtype=np.int64)
+    ad_lens = np.array([len(x) for x in ads], dtype=np.int64)
+    d_tags = torch.zeros(max(1, n * tag_len), dtype=torch.uint8, device=DEV)
+    if tags is not None:
+        d_tags = _t(np.frombuffer(b"".join(tags), dtype=np.uint8).copy())
+    d_status = torch.full((max(n, 1),), 7, dtype=torch.uint8, device=DEV)
+    d_ki = _t(np.array(key_index, dtype=np.int32)) if key_index is not None else None
+    b = ba.make_batch(n, d_in, d_out, d_tags, d_nonce, nonce_len, d_ad,
+                      offsets=_t(offs.astype(np.int64)), lengths=_t(lens),
+                      ad_offsets=_t(ad_offs.astype(np.int64)), ad_lengths=_t(ad_lens),
+                      status=d_status, key_index=d_ki)
+    if key_index is None:
+        ctx = ba.AEADCtx(aead, keys[0], tag_len)
+        (ctx.open_batch_device if open_ else ctx.seal_batch_device)(b)
+    else:
+        ks = ba.Keyset(aead, b"".join(keys), len(keys), tag_len)
+        (ks.open_batch_device if open_ else ks.seal_batch_device)(b)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    tg = d_tags.cpu().numpy().tobytes()
+    st = d_status.cpu().numpy()[:n]
+    outs = [out[int(offs[i]):int(offs[i]) + len(ins[i])].tobytes() for i in range(n)]
+    return outs, [tg[i * tag_len:(i + 1) * tag_len] for i in range(n)], st
+
+
+# ---------------------------------------------------------------------------
+# reference known-answer files through the single-record host API
+
+@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-192-gcm", "aes-256-gcm", "chacha20-poly1305"])
+def test_kat_single_record(aead):
+    cases = [c for c in load("kat_aead.json") if c["aead"] == aead]
+    ctxs = {}
+    for c in cases:
+        key, nonce, ad, pt, ct, tag = (_h(c[k]) for k in ("key", "nonce", "ad", "pt", "ct", "tag"))
+        tag_len = c.get("tag_len", len(tag))
+        k = (key, tag_len)
+        if k not in ctxs:
+            ctxs[k] = ba.AEADCtx(aead, key, tag_len)
+        ctx = ctxs[k]
+        if c["valid"]:
+            assert ctx.seal(nonce, pt, ad) == ct + tag, c["source"]
+            assert ctx.open(nonce, ct + tag, ad) == pt, c["source"]
+            if tag:
+                bad = bytearray(ct + tag)
+                bad[-1] ^= 0x80
+                with pytest.raises(ba.AEADError) as e:
+                    ctx.open(nonce, bytes(bad), ad)
+                assert e.value.lib == ba.ERR_LIB_CIPHER
+        else:
+            with pytest.raises(ba.AEADError) as e:
+                ctx.open(nonce, ct + tag, ad)
+            assert e.value.lib == ba.ERR_LIB_CIPHER, c["source"]
+
+
+def test_ref_edge_single_record():
+    for c in load("ref_edge.json")[::3]:
+        key, nonce, ad, pt, ct, tag = (_h(c[k]) for k in ("key", "nonce", "ad", "pt", "ct", "tag"))
+        ctx = ba.AEADCtx(c["aead"], key, len(tag))
+        assert ctx.seal(nonce, pt, ad) == ct + tag, (c["aead"], len(pt), len(nonce), len(ad))
+
+
+# ---------------------------------------------------------------------------
+# batches
+
+def _groups(cases):
+    g = {}
+    for c in cases:
+        tag_len = c.get("tag_len", len(_h(c["tag"])))
+        g.setdefault((c["aead"], len(_h(c["nonce"])), tag_len), []).append(c)
+    return g
+
+
+@pytest.mark.parametrize("source", ["ref_edge.json", "kat_aead.json"])
+def test_batch_multikey_vectors(source):
+    """Every record with its own key (keyset + key_index), seal then open."""
+    cases = [c for c in load(source) if c.get("valid", True)]
+    for (aead, nl, tag_len), grp in _groups(cases).items():
+        if aead == "chacha20-poly1305" and nl != 12:
+            continue
+        if nl == 0:
+            continue
+        keys = [_h(c["key"]) for c in grp]
+        ins = [_h(c["pt"]) for c in grp]
+        nonces = [_h(c["nonce"]) for c in grp]
+        ads = [_h(c["ad"]) for c in grp]
+        outs, tags, st = run_batch(aead, keys, list(range(len(grp))), ins, nonces, ads, tag_len)
+        assert st.tolist() == [1] * len(grp)
+        for c, out, tag in zip(grp, outs, tags):
+            assert out == _h(c["ct"]) and tag == _h(c["tag"]), (aead, c.get("source"), len(ins))
+        back, _, st = run_batch(aead, keys, list(range(len(grp))), outs, nonces, ads, tag_len,
+                                open_=True, tags=tags)
+        assert st.tolist() == [1] * len(grp)
+        assert back == ins
+
+
+@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm", "chacha20-poly1305"])
+@pytest.mark.parametrize("layout", ["aligned", "unaligned", "inplace"])
+def test_batch_ragged_vs_oracle(aead, layout):
+    rng = random.Random(hash((aead, layout)) & 0xffff)
+    key = bytes(rng.getrandbits(8) for _ in range(AEAD_KEYLEN[aead]))
+    n = 300
+    lens = [rng.choice([0, 1, 15, 16, 17, 63, 64, 65, 255, 256, 1000, 1350, 4097, 16384])
+            for _ in range(n)]
+    ins = [bytes(rng.getrandbits(8) for _ in range(l)) for l in lens]
+    nonces = [bytes(rng.getrandbits(8) for _ in range(12)) for _ in range(n)]
+    ads = [bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 5, 13, 16, 40, 300])))
+           for _ in range(n)]
+    outs, tags, st = run_batch(aead, [key], None, ins, nonces, ads, 16,
+                               odd=3 if layout == "unaligned" else 0,
+                               inplace=layout == "inplace")
+    assert st.all()
+    for i in range(n):
+        ok, ct, tag = o.seal(ORACLE_ID[aead], key, nonces[i], ins[i], ads[i])
+        assert ok and outs[i] == ct and tags[i] == tag, (i, lens[i], len(ads[i]))
+
+
+def test_batch_gcm_nonce_lengths_and_truncated_tags():
+    rng = random.Random(7)
+    for nl in (1, 8, 12, 16, 17, 60, 128):
+        for tag_len in (16, 12, 4, 1):
+            key = bytes(rng.getrandbits(8) for _ in range(16))
+            n = 40
+            ins = [bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 700))) for _ in range(n)]
+            nonces = [bytes(rng.getrandbits(8) for _ in range(nl)) for _ in range(n)]
+            ads = [bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 40))) for _ in range(n)]
+            outs, tags, st = run_batch("aes-128-gcm", [key], None, ins, nonces, ads, tag_len)
+            assert st.all()
+            for i in range(n):
+                ok, ct, tag = o.seal(o.AES_GCM, key, nonces[i], ins[i], ads[i], tag_len)
+                assert outs[i] == ct and tags[i] == tag, (nl, tag_len, i)
+
+
+@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm", "chacha20-poly1305"])
+def test_open_rejects_tampering_and_zeroes_output(aead):
+    rng = random.Random(11)
+    key = bytes(rng.getrandbits(8) for _ in range(AEAD_KEYLEN[aead]))
+    n = 64
+    ins = [bytes(rng.getrandbits(8) for _ in range(rng.randrange(1, 3000))) for _ in range(n)]
+    nonces = [bytes(rng.getrandbits(8) for _ in range(12)) for _ in range(n)]
+    ads = [bytes(rng.getrandbits(8) for _ in range(13)) for _ in range(n)]
+    cts, tags, st = run_batch(aead, [key], None, ins, nonces, ads, 16)
+    assert st.all()
+    bad = set(range(0, n, 3))
+    cts2, tags2, ads2 = list(cts), list(tags), list(ads)
+    for i in bad:
+        what = i % 4
+        if what == 0:
+            b = bytearray(cts2[i]); b[rng.randrange(len(b))] ^= 1 << rng.randrange(8); cts2[i] = bytes(b)
+        elif what == 1:
+            b = bytearray(tags2[i]); b[rng.randrange(16)] ^= 0x40; tags2[i] = bytes(b)
+        elif what == 2:
+            b = bytearray(ads2[i]); b[0] ^= 0x01; ads2[i] = bytes(b)
+        else:
+            tags2[i] = bytes(16)
+    pts, _, st = run_batch(aead, [key], None, cts2, nonces, ads2, 16, open_=True, tags=tags2)
+    for i in range(n):
+        if i in bad:
+            assert st[i] == 0 and pts[i] == bytes(len(ins[i])), i
+        else:
+            assert st[i] == 1 and pts[i] == ins[i], i
+
+
+def test_device_synth_matches_host_definition():
+    lens = np.array([16384, 1350, 1, 0, 77, 4096], dtype=np.uint64)
+    pt, offs, nonces, ads = o.synth_batch(1000, lens)
+    d_pt = torch.zeros(len(pt), dtype=torch.uint8, device=DEV)
+    d_n = torch.zeros(12 * len(lens), dtype=torch.uint8, device=DEV)
+    d_a = torch.zeros(13 * len(lens), dtype=torch.uint8, device=DEV)
+    ba.synth_fill_device(1000, len(lens), _t(offs.astype(np.int64)), _t(lens.astype(np.int64)),
+                         d_pt, d_n, d_a)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_pt.cpu().numpy(), pt)
+    assert np.array_equal(d_n.cpu().numpy(), nonces)
+    assert np.array_equal(d_a.cpu().numpy(), ads)
+
+
+# ---------------------------------------------------------------------------
+# synthetic workloads vs the reference library's digests
+
+def synth_device_batch(aead, nkeys, rpk, length, first=0):
+    n = nkeys * rpk
+    if length == "mixed":
+        lens = np.array([o.synth_mixed_len(first + i) for i in range(n)], dtype=np.uint64)
+    else:
+        lens = np.full(n, int(length), dtype=np.uint64)
+    padded = (lens + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(padded[:-1])
+    total = int(padded.sum())
+    d_offs, d_lens = _t(offs.astype(np.int64)), _t(lens.astype(np.int64))
+    d_pt = torch.empty(total, dtype=torch.uint8, device=DEV)
+    d_n = torch.empty(12 * n, dtype=torch.uint8, device=DEV)
+    d_a = torch.empty(13 * n, dtype=torch.uint8, device=DEV)
+    ba.synth_fill_device(first, n, d_offs, d_lens, d_pt, d_n, d_a)
+    return lens, offs, d_offs, d_lens, d_pt, d_n, d_a
+
+
+def _device_digests(d_out, offs, lens, d_tags, chunk=1024):
+    """tags_sha256 and the checksum-of-checksums ct digest, streamed from the
+    device chunk by chunk."""
+    n = len(lens)
+    parts = []
+    for c in range(0, n, chunk):
+        hi = min(n, c + chunk)
+        lo_b, hi_b = int(offs[c]), int(offs[hi - 1] + lens[hi - 1])
+        host = d_out[lo_b:hi_b].cpu().numpy()
+        h = hashlib.sha256()
+        for i in range(c, hi):
+            s = int(offs[i]) - lo_b
+            h.update(host[s:s + int(lens[i])].data)
+        parts.append(h.digest())
+    tags = d_tags.cpu().numpy().tobytes()
+    return hashlib.sha256(tags).hexdigest(), hashlib.sha256(b"".join(parts)).hexdigest()
+
+
+def _run_synth_digest(name):
+    g = load("ref_digests.json")[name]
+    aead, nkeys, rpk, length = g["aead"], g["nkeys"], g["records_per_key"], g["len"]
+    n = nkeys * rpk
+    lens, offs, d_offs, d_lens, d_pt, d_n, d_a = synth_device_batch(aead, nkeys, rpk, length)
+    d_out = torch.empty_like(d_pt)
+    d_tags = torch.zeros(16 * n, dtype=torch.uint8, device=DEV)
+    d_st = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    keys = [o.synth_key(k, AEAD_KEYLEN[aead]) for k in range(nkeys)]
+    b = ba.make_batch(n, d_pt, d_out, d_tags, d_n, 12, d_a, offsets=d_offs, lengths=d_lens,
+                      ad_stride=13, ad_len=13, status=d_st,
+                      key_index=_t((np.arange(n) // rpk).astype(np.int32)) if nkeys > 1 else None)
+    if nkeys > 1:
+        obj = ba.Keyset(aead, b"".join(keys), nkeys, 16)
+    else:
+        obj = ba.AEADCtx(aead, keys[0], 16)
+    obj.seal_batch_device(b)
+    torch.cuda.synchronize()
+    assert bool(d_st.all())
+    tags_d, ct_d = _device_digests(d_out, offs, lens, d_tags)
+    assert tags_d == g["tags_sha256"], name
+    assert ct_d == g["ct_sha256"], name
+    # open(seal(x)) == x, in place, all tags verify
+    d_st.zero_()
+    b2 = ba.make_batch(n, d_out, d_out, d_tags, d_n, 12, d_a, offsets=d_offs, lengths=d_lens,
+                       ad_stride=13, ad_len=13, status=d_st, key_index=b._refs[-1])
+    obj.open_batch_device(b2)
+    torch.cuda.synchronize()
+    assert bool(d_st.all())
+    assert torch.equal(d_out, d_pt)
+
+
+@pytest.mark.parametrize("name", ["parity_aes128_16k", "parity_aes256_mixed", "parity_chacha_1350",
+                                  "parity_multikey_aes128"])
+def test_synth_parity_digest(name):
+    _run_synth_digest(name)
+
+
+@pytest.mark.parametrize("name", ["config2_aes128_16k", "config3_chacha_1350"])
+def test_baseline_config_digest(name):
+    """BASELINE.json configs 2 and 3 at full size (16 GiB / 1.3 GiB)."""
+    _run_synth_digest(name)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", ["config4_aes256_mixed", "config5_multikey_aes128"])
+def test_baseline_config_digest_large(name):
+    """BASELINE.json configs 4 (32 GiB, mixed lengths) and 5 (64K keys)."""
+    if os.environ.get("BSSL_AMD_RUN_LARGE") != "1":
+        pytest.skip("set BSSL_AMD_RUN_LARGE=1")
+    _run_synth_digest(name)

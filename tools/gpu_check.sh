@@ -1,0 +1,30 @@
+#!/bin/bash
+# One gpurun session: smoke -> GPU parity tests -> bench -> rocprofv3 stats.
+# Each GPU step has its own time limit; a fault, abort or timeout ends the
+# session (exit codes other than 0/1 stop the chain).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STEPS="${STEPS:-smoke pytest bench prof}"
+run() {
+  local name=$1 t=$2; shift 2
+  echo "[$(date +%T)] start $name" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc" | tee -a gpurun_out/steps.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+  return 0
+}
+for s in $STEPS; do
+  case $s in
+    smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    pytest) run pytest 1500 python -m pytest tests/test_gpu_parity.py -q -m gpu -rf ${PYTEST_ARGS:-} ;;
+    bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} ;;
+    pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc1 -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} &&
+         run pmc2 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc2 -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
