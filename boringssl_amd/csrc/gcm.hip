@@ -35,10 +35,10 @@
 namespace bssl_amd {
 namespace {
 
-constexpr int kWaves = 8;
+constexpr int kWaves = 16;
 constexpr int kThreads = kWaves * 64;
 constexpr int kRecPerWave = 4;
-constexpr int kRecPerTile = kWaves * kRecPerWave;  // 32
+constexpr int kRecPerTile = kWaves * kRecPerWave;  // 64
 
 // ---------------------------------------------------------------------------
 // Compile-time AES tables.
@@ -82,106 +82,167 @@ constexpr Tables make_tables() {
 __constant__ Tables kTables = make_tables();
 
 // ---------------------------------------------------------------------------
-// LDS.
-constexpr int kGhashLdsBytes = kGhashPowers * 8192;  // 40 KiB
-constexpr int kAesLdsBytes = 256 * 256;              // 64 KiB
+// LDS layout of the main kernel (one static array, so offsets are link-time
+// constants that fold into the 16-bit ds_read offset field):
+//   [0, 40960)       GHASH nibble tables, power p at p*8192, position k at
+//                    k*256, value v at v*16
+//   [40960, 106496)  AES T0/T1, replicated per bank (see header comment)
+constexpr uint32_t kLdsGhash = 0;
+constexpr uint32_t kGhashLdsBytes = kGhashPowers * 8192;
+constexpr uint32_t kLdsAes = kGhashLdsBytes;
+constexpr uint32_t kAesLdsBytes = 256 * 256;
+constexpr uint32_t kLdsBytes = kLdsAes + kAesLdsBytes;
 
 __device__ __forceinline__ uint32_t rotl(uint32_t v, int n) {
   return __builtin_amdgcn_alignbit(v, v, 32 - n);
 }
 
-__device__ __forceinline__ uint32_t lds_u32(const uint8_t *base, uint32_t off) {
-  return *reinterpret_cast<const uint32_t *>(base + off);
-}
-
-__device__ __forceinline__ uint4 lds_u128(const uint8_t *base, uint32_t off) {
-  return *reinterpret_cast<const uint4 *>(base + off);
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32, gfx950
 }
 
 __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
   return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
 }
 
+__device__ __forceinline__ uint4 xor4_3(uint4 a, uint4 b, uint4 c) {
+  return make_uint4(xor3(a.x, b.x, c.x), xor3(a.y, b.y, c.y), xor3(a.z, b.z, c.z),
+                    xor3(a.w, b.w, c.w));
+}
+
+// (byte B of v) & 0xf0 in one VALU op (SDWA byte select).
+#define DEFINE_NIB(B)                                                          \
+  __device__ __forceinline__ uint32_t nib_b##B(uint32_t v, uint32_t mf0) {     \
+    uint32_t r;                                                                \
+    asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD "       \
+        "src0_sel:BYTE_" #B " src1_sel:DWORD"                                  \
+        : "=v"(r)                                                              \
+        : "v"(v), "v"(mf0));                                                   \
+    return r;                                                                  \
+  }
+DEFINE_NIB(1)
+DEFINE_NIB(2)
+DEFINE_NIB(3)
+#undef DEFINE_NIB
+
+template <int B>
+__device__ __forceinline__ uint32_t nib(uint32_t v, uint32_t mf0) {
+  if constexpr (B == 0) return v & 0xf0u;
+  if constexpr (B == 1) return nib_b1(v, mf0);
+  if constexpr (B == 2) return nib_b2(v, mf0);
+  return nib_b3(v, mf0);
+}
+
 // ---------------------------------------------------------------------------
 // AES.  State: 4 little-endian column words (byte r of word c = row r).
-// Lookup address of T(slot) entry for state byte k: v_perm puts byte k at
-// bits 8..15 and the lane/slot constant `lc` (bits 0..7) below it.
+// Lookup address of the T(slot) entry for state byte k: v_perm puts byte k at
+// bits 8..15 below which the lane/slot constant `lc` (bits 0..7) sits.
 template <int K>
 __device__ __forceinline__ uint32_t taddr(uint32_t lc, uint32_t s) {
   return __builtin_amdgcn_perm(lc, s, 0x0c0c0004u | (K << 8));
 }
 
-// One full round column: rows come from columns (a, b, c, d); rkx is the round
-// key word pre-rotated by 16.
-__device__ __forceinline__ uint32_t round_col(const uint8_t *T, uint32_t lc0,
-                                              uint32_t lc1, uint32_t a,
-                                              uint32_t b, uint32_t c,
-                                              uint32_t d, uint32_t rkx) {
-  uint32_t x0 = lds_u32(T, taddr<0>(lc0, a));
-  uint32_t x1 = lds_u32(T, taddr<1>(lc1, b));
-  uint32_t x2 = lds_u32(T, taddr<2>(lc0, c));
-  uint32_t x3 = lds_u32(T, taddr<3>(lc1, d));
-  return x0 ^ x1 ^ rotl(x2 ^ x3 ^ rkx, 16);
+template <uint32_t TB>
+__device__ __forceinline__ uint32_t tload(const uint8_t *smem, uint32_t a) {
+  return *reinterpret_cast<const uint32_t *>(smem + TB + a);
 }
 
-__device__ __forceinline__ uint32_t last_col(const uint8_t *T, uint32_t lc0,
-                                             uint32_t a, uint32_t b,
-                                             uint32_t c, uint32_t d,
-                                             uint32_t rk) {
-  uint32_t x0 = lds_u32(T, taddr<0>(lc0, a));
-  uint32_t x1 = lds_u32(T, taddr<1>(lc0, b));
-  uint32_t x2 = lds_u32(T, taddr<2>(lc0, c));
-  uint32_t x3 = lds_u32(T, taddr<3>(lc0, d));
+// One full round column: rows come from columns (a, b, c, d); rkx is the round
+// key word pre-rotated by 16:  T0[a0] ^ T1[b1] ^ rotl16(T0[c2] ^ T1[d3] ^ rkx).
+template <uint32_t TB>
+__device__ __forceinline__ uint32_t round_col(const uint8_t *smem, uint32_t lc0, uint32_t lc1,
+                                              uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                                              uint32_t rkx) {
+  const uint32_t x0 = tload<TB>(smem, taddr<0>(lc0, a));
+  const uint32_t x1 = tload<TB>(smem, taddr<1>(lc1, b));
+  const uint32_t x2 = tload<TB>(smem, taddr<2>(lc0, c));
+  const uint32_t x3 = tload<TB>(smem, taddr<3>(lc1, d));
+  return xor3(x0, x1, rotl(xor3(x2, x3, rkx), 16));
+}
+
+template <uint32_t TB>
+__device__ __forceinline__ uint32_t last_col(const uint8_t *smem, uint32_t lc0, uint32_t a,
+                                             uint32_t b, uint32_t c, uint32_t d, uint32_t rk) {
+  const uint32_t x0 = tload<TB>(smem, taddr<0>(lc0, a));
+  const uint32_t x1 = tload<TB>(smem, taddr<1>(lc0, b));
+  const uint32_t x2 = tload<TB>(smem, taddr<2>(lc0, c));
+  const uint32_t x3 = tload<TB>(smem, taddr<3>(lc0, d));
   // S[x] is byte 1 (and byte 2) of Te0[x].
-  uint32_t lo = __builtin_amdgcn_perm(x1, x0, 0x0c0c0501u);
-  uint32_t hi = __builtin_amdgcn_perm(x3, x2, 0x06020c0cu);
-  return lo ^ hi ^ rk;
+  const uint32_t lo = __builtin_amdgcn_perm(x1, x0, 0x0c0c0501u);
+  const uint32_t hi = __builtin_amdgcn_perm(x3, x2, 0x06020c0cu);
+  return xor3(lo, hi, rk);
 }
 
 struct RoundKeys {
   uint32_t w[15][4];
 };
 
-template <int NR>
-__device__ __forceinline__ uint4 aes_encrypt(uint4 in, const RoundKeys &rk,
-                                             const uint8_t *T, uint32_t lc0,
-                                             uint32_t lc1) {
-  uint32_t s0 = in.x ^ rk.w[0][0], s1 = in.y ^ rk.w[0][1];
-  uint32_t s2 = in.z ^ rk.w[0][2], s3 = in.w ^ rk.w[0][3];
+// AES rounds 1..NR on a state that already includes round key 0.
+template <int NR, uint32_t TB>
+__device__ __forceinline__ uint4 aes_rounds(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+                                            const RoundKeys &rk, const uint8_t *smem,
+                                            uint32_t lc0, uint32_t lc1) {
 #pragma unroll
   for (int r = 1; r < NR; r++) {
-    uint32_t t0 = round_col(T, lc0, lc1, s0, s1, s2, s3, rk.w[r][0]);
-    uint32_t t1 = round_col(T, lc0, lc1, s1, s2, s3, s0, rk.w[r][1]);
-    uint32_t t2 = round_col(T, lc0, lc1, s2, s3, s0, s1, rk.w[r][2]);
-    uint32_t t3 = round_col(T, lc0, lc1, s3, s0, s1, s2, rk.w[r][3]);
+    const uint32_t t0 = round_col<TB>(smem, lc0, lc1, s0, s1, s2, s3, rk.w[r][0]);
+    const uint32_t t1 = round_col<TB>(smem, lc0, lc1, s1, s2, s3, s0, rk.w[r][1]);
+    const uint32_t t2 = round_col<TB>(smem, lc0, lc1, s2, s3, s0, s1, rk.w[r][2]);
+    const uint32_t t3 = round_col<TB>(smem, lc0, lc1, s3, s0, s1, s2, rk.w[r][3]);
     s0 = t0;
     s1 = t1;
     s2 = t2;
     s3 = t3;
   }
   uint4 o;
-  o.x = last_col(T, lc0, s0, s1, s2, s3, rk.w[NR][0]);
-  o.y = last_col(T, lc0, s1, s2, s3, s0, rk.w[NR][1]);
-  o.z = last_col(T, lc0, s2, s3, s0, s1, rk.w[NR][2]);
-  o.w = last_col(T, lc0, s3, s0, s1, s2, rk.w[NR][3]);
+  o.x = last_col<TB>(smem, lc0, s0, s1, s2, s3, rk.w[NR][0]);
+  o.y = last_col<TB>(smem, lc0, s1, s2, s3, s0, rk.w[NR][1]);
+  o.z = last_col<TB>(smem, lc0, s2, s3, s0, s1, rk.w[NR][2]);
+  o.w = last_col<TB>(smem, lc0, s3, s0, s1, s2, rk.w[NR][3]);
   return o;
 }
 
 // ---------------------------------------------------------------------------
-// GHASH: x * H^(2^p) with the nibble tables of power p at `tab` (LDS).
-__device__ __forceinline__ uint4 gmul(uint4 x, const uint8_t *tab) {
-  uint4 r = make_uint4(0, 0, 0, 0);
-  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const uint32_t v = w[k >> 2];
-    const int sh = 8 * (k & 3);
-    const uint32_t hi = (v >> sh) & 0xf0u;
-    const uint32_t lo = (sh >= 4 ? (v >> (sh - 4)) : (v << 4)) & 0xf0u;
-    r = xor4(r, lds_u128(tab, (2 * k) * 256 + hi));
-    r = xor4(r, lds_u128(tab, (2 * k + 1) * 256 + lo));
-  }
+// GHASH: x * H^(2^p); the tables of power p start at byte TB of `tab`
+// (LDS in the main kernel, global memory in the prologue).
+template <uint32_t TB>
+__device__ __forceinline__ uint4 tab128(const uint8_t *tab, uint32_t a) {
+  return *reinterpret_cast<const uint4 *>(tab + TB + a);
+}
+
+template <uint32_t TB, int W>
+__device__ __forceinline__ uint4 gmul_word(uint4 r, uint32_t v, const uint8_t *tab,
+                                           uint32_t mf0) {
+  const uint32_t l = v << 4;  // low nibble of byte k -> high nibble of byte k of l
+  r = xor4_3(r, tab128<TB + (8 * W + 0) * 256>(tab, nib<0>(v, mf0)),
+             tab128<TB + (8 * W + 1) * 256>(tab, nib<0>(l, mf0)));
+  r = xor4_3(r, tab128<TB + (8 * W + 2) * 256>(tab, nib<1>(v, mf0)),
+             tab128<TB + (8 * W + 3) * 256>(tab, nib<1>(l, mf0)));
+  r = xor4_3(r, tab128<TB + (8 * W + 4) * 256>(tab, nib<2>(v, mf0)),
+             tab128<TB + (8 * W + 5) * 256>(tab, nib<2>(l, mf0)));
+  r = xor4_3(r, tab128<TB + (8 * W + 6) * 256>(tab, nib<3>(v, mf0)),
+             tab128<TB + (8 * W + 7) * 256>(tab, nib<3>(l, mf0)));
   return r;
+}
+
+template <uint32_t TB>
+__device__ __forceinline__ uint4 gmul(uint4 x, const uint8_t *tab, uint32_t mf0) {
+  // The scheduling barriers keep at most one word's lookups (8 x 16 B) in
+  // flight; without them hipcc hoists all 32 loads and needs 128 VGPRs.
+  uint4 r = make_uint4(0, 0, 0, 0);
+  r = gmul_word<TB, 0>(r, x.x, tab, mf0);
+  __builtin_amdgcn_sched_barrier(0);
+  r = gmul_word<TB, 1>(r, x.y, tab, mf0);
+  __builtin_amdgcn_sched_barrier(0);
+  r = gmul_word<TB, 2>(r, x.z, tab, mf0);
+  __builtin_amdgcn_sched_barrier(0);
+  r = gmul_word<TB, 3>(r, x.w, tab, mf0);
+  __builtin_amdgcn_sched_barrier(0);
+  return r;
+}
+
+// Runtime power index (prologue, tree).
+__device__ __forceinline__ uint4 gmul_pow(uint4 x, const uint8_t *tab, int p, uint32_t mf0) {
+  return gmul<0>(x, tab + p * 8192, mf0);
 }
 
 __device__ __forceinline__ uint4 shfl4(uint4 v, int src, int width) {
@@ -192,24 +253,6 @@ __device__ __forceinline__ uint4 shfl4(uint4 v, int src, int width) {
 __device__ __forceinline__ uint4 shfl_down4(uint4 v, int d, int width) {
   return make_uint4(__shfl_down(v.x, d, width), __shfl_down(v.y, d, width),
                     __shfl_down(v.z, d, width), __shfl_down(v.w, d, width));
-}
-
-// Combine the 16 per-lane Horner accumulators of a group.  Lane q's
-// accumulator must be weighted by H^e with e = (r - 1 - v) mod 16 where v is
-// the lane's virtual index (see DESIGN.md "GHASH lane algebra").  `src` is the
-// lane whose accumulator goes to position q.  Result valid in every lane.
-// Must be called with all 64 lanes active.
-__device__ __forceinline__ uint4 group_combine(uint4 acc, int q, int src,
-                                               const uint8_t *gtab) {
-  uint4 a = shfl4(acc, src, 16);
-#pragma unroll
-  for (int t = 0; t < 4; t++) {
-    const int s = 1 << t;
-    uint4 m = gmul(a, gtab + t * 8192);
-    uint4 o = shfl_down4(a, s, 16);
-    if ((q & (2 * s - 1)) == 0) a = xor4(m, o);
-  }
-  return shfl4(a, 0, 16);
 }
 
 // ---------------------------------------------------------------------------
@@ -230,10 +273,8 @@ __device__ __forceinline__ uint4 mask_block(uint4 v, uint32_t n) {
   uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    const int lo = 4 * i;
-    uint32_t m = (n >= (uint32_t)lo + 4) ? 0xffffffffu
-                 : (n <= (uint32_t)lo) ? 0u
-                                       : ((1u << (8 * (n - lo))) - 1u);
+    const uint32_t lo = 4 * i;
+    const uint32_t m = (n >= lo + 4) ? 0xffffffffu : (n <= lo) ? 0u : ((1u << (8 * (n - lo))) - 1u);
     w[i] &= m;
   }
   return make_uint4(w[0], w[1], w[2], w[3]);
@@ -249,35 +290,6 @@ __device__ __forceinline__ int wave_max(int v) {
   return v;
 }
 
-// Exclusive Horner (sum_k B_k H^(m-1-k)) of the zero-padded 16-byte blocks of
-// `len` bytes at p, optionally followed by one extra block; all lanes of the
-// group return the value.  All 64 lanes must call it.
-__device__ uint4 group_ghash(const uint8_t *p, uint64_t len, bool has_extra,
-                             uint4 extra, bool active, int q,
-                             const uint8_t *gtab) {
-  const uint64_t nb = active ? (len + 15) / 16 + (has_extra ? 1 : 0) : 0;
-  const int wmax = wave_max((int)min<uint64_t>(nb, 0x7fffffff));
-  if (wmax <= 1) {
-    // Single block: no multiplication needed.
-    uint4 b0 = make_uint4(0, 0, 0, 0);
-    if (nb == 1) b0 = len ? load_partial(p, (uint32_t)min<uint64_t>(len, 16)) : extra;
-    return b0;
-  }
-  uint4 acc = make_uint4(0, 0, 0, 0);
-  for (uint64_t k = q; k < nb; k += 16) {
-    uint4 blk;
-    if (k * 16 < len) {
-      const uint64_t rem = len - k * 16;
-      blk = load_partial(p + k * 16, (uint32_t)min<uint64_t>(rem, 16));
-    } else {
-      blk = extra;
-    }
-    acc = xor4(gmul(acc, gtab + 4 * 8192), blk);
-  }
-  const int r = (int)(nb & 15);
-  return group_combine(acc, q, (q + r) & 15, gtab);
-}
-
 struct RecordMeta {
   uint64_t off, len, ad_off, ad_len;
 };
@@ -291,60 +303,110 @@ __device__ __forceinline__ RecordMeta record_meta(const BatchDesc &b, uint64_t i
   return m;
 }
 
-// ---------------------------------------------------------------------------
-// Process the (up to) 4 records of this wave.  `active` is per group.
-template <int NR, bool OPEN>
-__device__ void process_records(const RoundKeys &rk, const BatchDesc &b,
-                                uint64_t rec, bool active, bool bad_key,
-                                const uint8_t *gtab, const uint8_t *T,
-                                uint32_t lc0, uint32_t lc1) {
-  const int lane = threadIdx.x & 63;
-  const int q = lane & 15;
-  RecordMeta m = {0, 0, 0, 0};
-  if (active) m = record_meta(b, rec);
-  // gcm.cc.inc:409 message limit 2^36-32; e_aes.cc.inc:790 empty nonce.
-  const bool bad = active && (bad_key || b.nonce_len == 0 ||
-                              m.len > ((uint64_t(1) << 36) - 32) ||
-                              m.ad_len > (uint64_t(1) << 61));
-  const bool live = active && !bad;
-  const uint8_t *nonce = b.nonces + (live ? rec * b.nonce_len : 0);
+// Per-record state handed from the prologue to the bulk kernel (64 bytes).
+struct alignas(16) RecState {
+  uint4 j0;   // pre-counter block J0 (gcm.cc.inc:316-338)
+  uint4 ek0;  // E_K(J0)
+  uint4 ya;   // exclusive GHASH of the AD: sum A_k H^(m-1-k)
+  uint32_t live, pad[3];
+};
 
-  // J0 (gcm.cc.inc:316-338).
-  uint4 j0;
-  {
-    const bool std_iv = b.nonce_len == 12;
-    uint4 lenblk = make_uint4(0, 0, 0, bswap32((uint32_t)(b.nonce_len << 3)));
-    lenblk.z = bswap32((uint32_t)(b.nonce_len >> 29));
-    uint4 y = group_ghash(nonce, std_iv ? 0 : b.nonce_len, true, lenblk,
-                          live && !std_iv, q, gtab);
-    if (std_iv) {
-      j0 = live ? load_partial(nonce, 12) : make_uint4(0, 0, 0, 0);
+// ---------------------------------------------------------------------------
+// Prologue: one thread per record.  J0 (incl. the GHASH-derived J0 of a
+// non-96-bit nonce), E_K(J0) and the AD hash -- the per-record constant work
+// of CRYPTO_gcm128_init_ctx / _aad (gcm.cc.inc:298-398).
+template <int NR>
+__global__ __launch_bounds__(256) void gcm_prologue(const GcmKeyDev *__restrict__ keys,
+                                                    BatchDesc b, RecState *__restrict__ st) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kAesLdsBytes];
+  // Only replica 0 of T0/T1 (lane constant 0 / 128): conflicts do not matter here.
+  for (int e = threadIdx.x; e < 512; e += blockDim.x) {
+    const int idx = e >> 1;
+    const uint32_t v = kTables.te0[idx];
+    reinterpret_cast<uint32_t *>(smem)[idx * 64 + (e & 1) * 32] = (e & 1) ? rotl(v, 8) : v;
+  }
+  __syncthreads();
+  const uint64_t rec = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (rec >= b.num_records) return;
+  const RecordMeta m = record_meta(b, rec);
+  const uint32_t k = b.key_index ? b.key_index[rec] : 0u;
+  // e_aes.cc.inc:790 (empty nonce), gcm.cc.inc:368,409 (length limits).
+  const bool live = k < b.num_keys && b.nonce_len != 0 &&
+                    m.len <= ((uint64_t(1) << 36) - 32) && m.ad_len <= (uint64_t(1) << 61);
+  RecState s;
+  s.live = live;
+  s.pad[0] = s.pad[1] = s.pad[2] = 0;
+  s.j0 = s.ek0 = s.ya = make_uint4(0, 0, 0, 0);
+  if (live) {
+    const GcmKeyDev *kp = keys + k;
+    const uint8_t *htab = reinterpret_cast<const uint8_t *>(kp->htab);
+    const uint32_t mf0 = 0xf0;
+    RoundKeys rk;
+#pragma unroll
+    for (int r = 0; r <= NR; r++)
+#pragma unroll
+      for (int c = 0; c < 4; c++) rk.w[r][c] = kp->rk[r][c];
+    const uint8_t *nonce = b.nonces + rec * b.nonce_len;
+    uint4 j0;
+    if (b.nonce_len == 12) {
+      j0 = load_partial(nonce, 12);
       j0.w = 0x01000000u;  // be32(1)
     } else {
-      j0 = gmul(y, gtab);  // GHASH = H * (exclusive Horner)
+      j0 = make_uint4(0, 0, 0, 0);
+      for (uint64_t o = 0; o < b.nonce_len; o += 16)
+        j0 = gmul_pow(xor4(j0, load_partial(nonce + o, (uint32_t)min<uint64_t>(b.nonce_len - o, 16))),
+                      htab, 0, mf0);
+      const uint64_t bits = b.nonce_len << 3;
+      j0 = gmul_pow(xor4(j0, make_uint4(0, 0, bswap32((uint32_t)(bits >> 32)), bswap32((uint32_t)bits))),
+                    htab, 0, mf0);
     }
+    s.j0 = j0;
+    s.ek0 = aes_rounds<NR, 0>(j0.x ^ rk.w[0][0], j0.y ^ rk.w[0][1], j0.z ^ rk.w[0][2],
+                              j0.w ^ rk.w[0][3], rk, smem, 0u, 128u);
+    const uint8_t *ad = b.ad + m.ad_off;
+    uint4 ya = make_uint4(0, 0, 0, 0);
+    for (uint64_t o = 0; o < m.ad_len; o += 16) {
+      const uint4 blk = load_partial(ad + o, (uint32_t)min<uint64_t>(m.ad_len - o, 16));
+      ya = o ? xor4(gmul_pow(ya, htab, 0, mf0), blk) : blk;
+    }
+    s.ya = ya;
   }
-  const uint32_t ctr0 = bswap32(j0.w);
-  const uint4 ek0 = aes_encrypt<NR>(j0, rk, T, lc0, lc1);
+  st[rec] = s;
+}
 
-  // AAD (gcm.cc.inc:346-398).
-  const uint4 ya = group_ghash(b.ad + (live ? m.ad_off : 0), live ? m.ad_len : 0, false,
-                               make_uint4(0, 0, 0, 0), live, q, gtab);
-
-  // Bulk CTR + GHASH (gcm.cc.inc:400-574).
+// ---------------------------------------------------------------------------
+// Bulk kernel: CTR keystream + GHASH + tag for the (up to) 4 records of a
+// wave, 16 lanes per record.  `active` is per group (record in this key pass).
+template <int NR, bool OPEN>
+__device__ __forceinline__ void process_records(const RoundKeys &rk, const BatchDesc &b,
+                                                const RecState *__restrict__ st, uint64_t rec,
+                                                bool active, const uint8_t *smem,
+                                                uint32_t lc0, uint32_t lc1, uint32_t mf0) {
+  const int q = threadIdx.x & 15;
+  RecordMeta m = {0, 0, 0, 0};
+  RecState s;
+  s.j0 = s.ek0 = s.ya = make_uint4(0, 0, 0, 0);
+  s.live = 0;
+  if (active) {
+    m = record_meta(b, rec);
+    s = st[rec];
+  }
+  const bool live = active && s.live;
   const uint64_t nb = live ? (m.len + 15) / 16 : 0;
+  const uint32_t ctr0 = bswap32(s.j0.w);
+  // Round 0 of the counter blocks: words 0..2 are constant per record.
+  const uint32_t c0 = s.j0.x ^ rk.w[0][0], c1 = s.j0.y ^ rk.w[0][1], c2 = s.j0.z ^ rk.w[0][2];
   const uint8_t *src = b.in + m.off;
   uint8_t *dst = b.out + m.off;
   const bool aligned = ((reinterpret_cast<uintptr_t>(src) |
                          reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
-  uint4 acc = (q == 15 && live) ? ya : make_uint4(0, 0, 0, 0);
-  const uint8_t *h16 = gtab + 4 * 8192;
+  uint4 acc = (q == 15 && live) ? s.ya : make_uint4(0, 0, 0, 0);
   const int iters = wave_max((int)((nb + 15) / 16));
   for (int it = 0; it < iters; it++) {
     const uint64_t j = (uint64_t)it * 16 + q;
     const uint32_t ctr = ctr0 + 1u + (uint32_t)j;  // inc32 wraps mod 2^32
-    const uint4 ks = aes_encrypt<NR>(make_uint4(j0.x, j0.y, j0.z, bswap32(ctr)), rk, T,
-                                     lc0, lc1);
+    const uint4 ks = aes_rounds<NR, kLdsAes>(c0, c1, c2, bswap32(ctr) ^ rk.w[0][3], rk, smem,
+                                             lc0, lc1);
     if (j < nb) {
       const uint64_t rem = m.len - j * 16;
       uint4 x, y;
@@ -358,36 +420,55 @@ __device__ void process_records(const RoundKeys &rk, const BatchDesc &b,
         y = mask_block(xor4(x, ks), n);
         store_partial(dst + j * 16, y, n);
       }
-      acc = xor4(gmul(acc, h16), OPEN ? x : y);
+      acc = xor4(gmul<kLdsGhash + 4 * 8192>(acc, smem, mf0), OPEN ? x : y);
     }
   }
+  // Lane algebra: lane q holds the virtual elements v = q+1+16i of
+  // [Y_A, C_0, ..., C_{nb-1}]; rotate so position p holds the lane whose
+  // weight is H^(15-p), then tree-combine with H, H^2, H^4, H^8.
   const int r = (int)((nb + 1) & 15);
-  const uint4 z = group_combine(acc, q, (q + r + 15) & 15, gtab);
-
-  // Tag (gcm.cc.inc:576-604): ((Z*H) ^ len block) * H ^ E_K(J0).
+  uint4 a = shfl4(acc, (q + r + 15) & 15, 16);
+  // Kept as a rolled loop so hipcc does not interleave the six dependent
+  // multiplications (which costs ~120 VGPRs when unrolled).
+#pragma unroll 1
+  for (int t = 0; t < 4; t++) {
+    const int sh = 1 << t;
+    const uint4 o = shfl_down4(a, sh, 16);
+    const uint4 mlt = gmul<0>(a, smem + kLdsGhash + t * 8192, mf0);
+    if ((q & (2 * sh - 1)) == 0) a = xor4(mlt, o);
+  }
+  // Tag (gcm.cc.inc:576-604): ((Z*H) ^ len block) * H ^ E_K(J0), in lane 0.
   const uint64_t abits = m.ad_len << 3, cbits = m.len << 3;
-  const uint4 lb = make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
-                              bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits));
-  const uint4 tag = xor4(gmul(xor4(gmul(z, gtab), lb), gtab), ek0);
+  uint4 add = make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
+                         bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits));
+#pragma unroll 1
+  for (int t = 0; t < 2; t++) {
+    a = xor4(gmul<0>(a, smem + kLdsGhash, mf0), add);
+    add = s.ek0;
+  }
+  const uint4 tag = a;
 
   uint8_t *tagp = b.tags + rec * b.tag_len;
-  bool ok = live;
-  if (OPEN && live) {
-    const uint32_t tw[4] = {tag.x, tag.y, tag.z, tag.w};
-    uint32_t diff = 0;
-    for (uint32_t i = 0; i < b.tag_len; i++)
-      diff |= ((tw[i >> 2] >> (8 * (i & 3))) & 0xff) ^ tagp[i];
-    ok = diff == 0;  // CRYPTO_memcmp, e_aes.cc.inc:860-864
-  }
-  if (active && q == 0) {
-    if (!OPEN) {
-      if (ok)
-        store_partial(tagp, tag, b.tag_len);
-      else
-        for (uint32_t i = 0; i < b.tag_len; i++) tagp[i] = 0;
+  int ok = live;
+  if (q == 0) {
+    if (OPEN && live) {
+      const uint32_t tw[4] = {tag.x, tag.y, tag.z, tag.w};
+      uint32_t diff = 0;
+      for (uint32_t i = 0; i < b.tag_len; i++)
+        diff |= ((tw[i >> 2] >> (8 * (i & 3))) & 0xff) ^ tagp[i];
+      ok = diff == 0;  // CRYPTO_memcmp, e_aes.cc.inc:860-864
     }
-    if (b.status) b.status[rec] = ok ? 1 : 0;
+    if (active) {
+      if (!OPEN) {
+        if (ok)
+          store_partial(tagp, tag, b.tag_len);
+        else
+          for (uint32_t i = 0; i < b.tag_len; i++) tagp[i] = 0;
+      }
+      if (b.status) b.status[rec] = ok ? 1 : 0;
+    }
   }
+  ok = __shfl(ok, 0, 16);
   // Zero the output of a failed record (aead.cc.inc:132-139, 539-547).
   if (active && !ok) {
     for (uint64_t j = q; j * 16 < m.len; j += 16) {
@@ -399,11 +480,14 @@ __device__ void process_records(const RoundKeys &rk, const BatchDesc &b,
 
 template <int NR, bool OPEN>
 __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restrict__ keys,
-                                                      BatchDesc b) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_ghash[kGhashLdsBytes];
-  __shared__ __attribute__((aligned(16))) uint8_t s_aes[kAesLdsBytes];
-  __shared__ uint32_t s_keys[kRecPerTile];
-
+                                                      BatchDesc b,
+                                                      const RecState *__restrict__ st) {
+  static_assert(kRecPerTile == 64, "one wave plans a tile with ballots");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
+  // Pass list of the current tile: key and 64-bit record mask per pass.
+  __shared__ uint32_t s_pass_key[kRecPerTile];
+  __shared__ uint64_t s_pass_mask[kRecPerTile];
+  __shared__ int s_npass;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -414,49 +498,57 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
   for (int e = tid; e < 256 * 64; e += kThreads) {
     const int idx = e >> 6, slot = (e >> 5) & 1;
     const uint32_t v = kTables.te0[idx];
-    reinterpret_cast<uint32_t *>(s_aes)[e] = slot ? rotl(v, 8) : v;
+    reinterpret_cast<uint32_t *>(smem + kLdsAes)[e] = slot ? rotl(v, 8) : v;
   }
   const uint32_t lc0 = (uint32_t)(lane & 31) * 4u;
   const uint32_t lc1 = lc0 + 128u;
+  const uint32_t mf0 = 0xf0u;
 
   uint32_t loaded = 0xffffffffu;
-  RoundKeys rk;
   const uint64_t n = b.num_records;
   for (uint64_t base = (uint64_t)blockIdx.x * kRecPerTile; base < n;
        base += (uint64_t)gridDim.x * kRecPerTile) {
     __syncthreads();
-    if (tid < kRecPerTile) {
-      const uint64_t i = base + tid;
-      s_keys[tid] = i < n ? (b.key_index ? b.key_index[i] : 0u) : 0xffffffffu;
+    if (wave == 0) {
+      // Plan the tile: one pass per distinct key, in record order.
+      const uint64_t i = base + lane;
+      uint32_t k = i < n ? (b.key_index ? b.key_index[i] : 0u) : 0xffffffffu;
+      if (k != 0xffffffffu && k >= b.num_keys) k = 0;  // flagged dead by the prologue
+      uint64_t pending = __ballot(k != 0xffffffffu);
+      int np = 0;
+      while (pending) {
+        const uint32_t kk = __shfl(k, __builtin_ctzll(pending), 64);
+        const uint64_t mask = __ballot(k == kk) & pending;
+        if (lane == 0) {
+          s_pass_key[np] = kk;
+          s_pass_mask[np] = mask;
+        }
+        pending &= ~mask;
+        np++;
+      }
+      if (lane == 0) s_npass = np;
     }
     __syncthreads();
-    uint64_t pending = 0;
-    for (int t = 0; t < kRecPerTile; t++)
-      if (s_keys[t] != 0xffffffffu) pending |= uint64_t(1) << t;
-    while (pending) {
-      const int first = __builtin_ctzll(pending);
-      const uint32_t k = __builtin_amdgcn_readfirstlane(s_keys[first]);
-      uint64_t mask = 0;
-      for (int t = 0; t < kRecPerTile; t++)
-        if (((pending >> t) & 1) && s_keys[t] == k) mask |= uint64_t(1) << t;
-      pending &= ~mask;
-      const bool bad_key = k >= b.num_keys;
-      const uint32_t kk = bad_key ? 0u : k;
-      if (kk != loaded) {
+    const int npass = s_npass;
+    for (int pi = 0; pi < npass; pi++) {
+      const uint32_t k = __builtin_amdgcn_readfirstlane(s_pass_key[pi]);
+      const uint64_t mask = s_pass_mask[pi];
+      if (k != loaded) {
         __syncthreads();
-        const uint4 *srcp = reinterpret_cast<const uint4 *>(keys[kk].htab);
-        for (int e = tid; e < kGhashLdsBytes / 16; e += kThreads)
-          reinterpret_cast<uint4 *>(s_ghash)[e] = srcp[e];
+        const uint4 *srcp = reinterpret_cast<const uint4 *>(keys[k].htab);
+        for (uint32_t e = tid; e < kGhashLdsBytes / 16; e += kThreads)
+          reinterpret_cast<uint4 *>(smem + kLdsGhash)[e] = srcp[e];
         __syncthreads();
-        loaded = kk;
-#pragma unroll
-        for (int r = 0; r <= NR; r++)
-#pragma unroll
-          for (int c = 0; c < 4; c++) rk.w[r][c] = keys[kk].rk[r][c];
+        loaded = k;
       }
+      RoundKeys rk;
+#pragma unroll
+      for (int r = 0; r <= NR; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) rk.w[r][c] = keys[k].rk[r][c];
       const int t = wave * kRecPerWave + g;
       const bool active = (mask >> t) & 1;
-      process_records<NR, OPEN>(rk, b, base + t, active, bad_key, s_ghash, s_aes, lc0, lc1);
+      process_records<NR, OPEN>(rk, b, st, base + t, active, smem, lc0, lc1, mf0);
     }
   }
 }
@@ -472,10 +564,19 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s) {
         hipSuccess)
       return 1;
   }
+  RecState *st = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void **>(&st), b.num_records * sizeof(RecState), s) !=
+      hipSuccess)
+    return 2;
+  const uint64_t pblocks = (b.num_records + 255) / 256;
+  hipLaunchKernelGGL((gcm_prologue<NR>), dim3((unsigned)pblocks), dim3(256), 0, s, keys, b, st);
   const uint64_t tiles = (b.num_records + kRecPerTile - 1) / kRecPerTile;
   const unsigned grid = (unsigned)(tiles < (uint64_t)g_num_cus ? tiles : (uint64_t)g_num_cus);
-  hipLaunchKernelGGL((gcm_kernel<NR, OPEN>), dim3(grid), dim3(kThreads), 0, s, keys, b);
-  return (int)hipGetLastError();
+  hipLaunchKernelGGL((gcm_kernel<NR, OPEN>), dim3(grid), dim3(kThreads), 0, s, keys, b,
+                     (const RecState *)st);
+  int rc = (int)hipGetLastError();
+  hipFreeAsync(st, s);
+  return rc;
 }
 
 }  // namespace
