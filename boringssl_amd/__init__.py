@@ -67,7 +67,8 @@ EXPORTED_SYMBOLS = [
     "BSSL_AMD_KEYSET_new", "BSSL_AMD_KEYSET_free", "BSSL_AMD_KEYSET_num_keys",
     "BSSL_AMD_KEYSET_seal_batch_device", "BSSL_AMD_KEYSET_open_batch_device",
     "BSSL_AMD_set_device", "BSSL_AMD_device_count", "BSSL_AMD_synth_fill_device",
-    "BSSL_AMD_set_kernel_timing", "BSSL_AMD_last_kernel_ms", "BSSL_AMD_last_kernel_name",
+    "BSSL_AMD_set_kernel_timing", "BSSL_AMD_collect_kernel_times", "BSSL_AMD_last_kernel_ms",
+    "BSSL_AMD_last_kernel_name",
 ]
 
 
@@ -131,6 +132,7 @@ _SIGS = {
     "BSSL_AMD_device_count": (_I, []),
     "BSSL_AMD_synth_fill_device": (_I, [ctypes.c_uint64, _S, _P, _P, _P, _P, _P, _P]),
     "BSSL_AMD_set_kernel_timing": (None, [_I]),
+    "BSSL_AMD_collect_kernel_times": (_S, [ctypes.POINTER(ctypes.c_double), _S]),
     "BSSL_AMD_last_kernel_ms": (ctypes.c_double, []),
     "BSSL_AMD_last_kernel_name": (ctypes.c_char_p, []),
 }
@@ -332,6 +334,22 @@ def synth_fill_device(first_record, n, offsets, lengths, pt, nonces, ads, stream
                                            _dptr(pt), _dptr(nonces), _dptr(ads),
                                            _stream_ptr(stream)):
         raise RuntimeError("BSSL_AMD_synth_fill_device failed")
+
+
+def set_kernel_timing(enable):
+    """Record HIP events around every batch's bulk kernel (see aead.h)."""
+    _lib.BSSL_AMD_set_kernel_timing(1 if enable else 0)
+
+
+def collect_kernel_times(max_n=4096):
+    """Durations (ms) of the bulk kernels launched since the last call."""
+    buf = (ctypes.c_double * max_n)()
+    n = _lib.BSSL_AMD_collect_kernel_times(buf, max_n)
+    return [buf[i] for i in range(min(n, max_n))]
+
+
+def last_kernel_name():
+    return _lib.BSSL_AMD_last_kernel_name().decode()
 
 
 def set_device(dev):

@@ -145,9 +145,41 @@ void free_keys(KeyMaterial *km) {
   delete km;
 }
 
-thread_local bool t_timing = false;
-thread_local double t_last_ms = 0;
-thread_local const char *t_last_name = "";
+// Kernel timing: when enabled, every batch launch records a pair of HIP
+// events around its bulk kernel (no host synchronisation);
+// BSSL_AMD_collect_kernel_times() waits for them and reports the durations.
+struct TimingState {
+  bool enabled = false;
+  std::vector<KernelEvents> free_pairs, pending;
+  double last_ms = 0;
+  const char *last_name = "";
+  ~TimingState() {
+    for (auto &e : free_pairs) {
+      hipEventDestroy(reinterpret_cast<hipEvent_t>(e.start));
+      hipEventDestroy(reinterpret_cast<hipEvent_t>(e.stop));
+    }
+  }
+};
+thread_local TimingState t_timing;
+
+const KernelEvents *timing_pair() {
+  if (!t_timing.enabled) return nullptr;
+  KernelEvents e;
+  if (!t_timing.free_pairs.empty()) {
+    e = t_timing.free_pairs.back();
+    t_timing.free_pairs.pop_back();
+  } else {
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess) return nullptr;
+    if (hipEventCreate(&b) != hipSuccess) {
+      hipEventDestroy(a);
+      return nullptr;
+    }
+    e = KernelEvents{a, b};
+  }
+  t_timing.pending.push_back(e);
+  return &t_timing.pending.back();
+}
 
 // Launch a batch over device buffers.  Returns 1 on success.
 int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch, bool open,
@@ -172,18 +204,15 @@ int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch
   d.num_records = batch->num_records;
   d.tag_len = (uint32_t)tag_len;
   d.num_keys = (uint32_t)km->num_keys;
-  float ms = 0;
   int rc;
+  const KernelEvents *ev = timing_pair();
   if (km->aead->kind == kAeadAesGcm) {
-    rc = launch_gcm(static_cast<const GcmKeyDev *>(km->dev), d, open, km->nr, stream,
-                    t_timing ? &ms : nullptr);
-    t_last_name = "gcm_kernel";
+    rc = launch_gcm(static_cast<const GcmKeyDev *>(km->dev), d, open, km->nr, stream, ev);
+    t_timing.last_name = "gcm_kernel";
   } else {
-    rc = launch_chacha(static_cast<const ChaChaKeyDev *>(km->dev), d, open, stream,
-                       t_timing ? &ms : nullptr);
-    t_last_name = "chacha_poly_kernel";
+    rc = launch_chacha(static_cast<const ChaChaKeyDev *>(km->dev), d, open, stream, ev);
+    t_timing.last_name = "chacha_poly_kernel";
   }
-  t_last_ms = ms;
   if (rc != 0) {
     PUT_ERROR(ERR_R_INTERNAL_ERROR);
     return 0;
@@ -936,8 +965,26 @@ int BSSL_AMD_synth_fill_device(uint64_t first_record, size_t n, const uint64_t *
   return launch_synth(first_record, n, offsets, lengths, pt, nonces, ads, hip_stream) == 0;
 }
 
-void BSSL_AMD_set_kernel_timing(int enable) { t_timing = enable != 0; }
-double BSSL_AMD_last_kernel_ms(void) { return t_last_ms; }
-const char *BSSL_AMD_last_kernel_name(void) { return t_last_name; }
+void BSSL_AMD_set_kernel_timing(int enable) { t_timing.enabled = enable != 0; }
+
+size_t BSSL_AMD_collect_kernel_times(double *out_ms, size_t max) {
+  size_t n = 0;
+  for (auto &e : t_timing.pending) {
+    float ms = 0;
+    if (hipEventSynchronize(reinterpret_cast<hipEvent_t>(e.stop)) == hipSuccess &&
+        hipEventElapsedTime(&ms, reinterpret_cast<hipEvent_t>(e.start),
+                            reinterpret_cast<hipEvent_t>(e.stop)) == hipSuccess) {
+      if (out_ms && n < max) out_ms[n] = ms;
+      n++;
+      t_timing.last_ms = ms;
+    }
+    t_timing.free_pairs.push_back(e);
+  }
+  t_timing.pending.clear();
+  return n;
+}
+
+double BSSL_AMD_last_kernel_ms(void) { return t_timing.last_ms; }
+const char *BSSL_AMD_last_kernel_name(void) { return t_timing.last_name; }
 
 }  // extern "C"

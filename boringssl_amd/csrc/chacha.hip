@@ -400,31 +400,20 @@ __global__ __launch_bounds__(kThreads) void chacha_poly_kernel(
 }  // namespace
 
 int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, void *stream,
-                  float *timing_ms) {
+                  const KernelEvents *ev) {
   if (b.num_records == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (timing_ms) {
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
-    hipEventRecord(e0, s);
-  }
   const uint64_t blocks = (b.num_records + kRecPerBlock - 1) / kRecPerBlock;
   if (blocks > 0x7fffffffu) return 1;
+  if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
   if (open)
     hipLaunchKernelGGL(chacha_poly_kernel<true>, dim3((unsigned)blocks), dim3(kThreads), 0, s,
                        keys, b);
   else
     hipLaunchKernelGGL(chacha_poly_kernel<false>, dim3((unsigned)blocks), dim3(kThreads), 0, s,
                        keys, b);
-  int rc = (int)hipGetLastError();
-  if (timing_ms) {
-    hipEventRecord(e1, s);
-    hipEventSynchronize(e1);
-    hipEventElapsedTime(timing_ms, e0, e1);
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-  }
+  const int rc = (int)hipGetLastError();
+  if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
   return rc;
 }
 

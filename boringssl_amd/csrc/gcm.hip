@@ -177,13 +177,13 @@ struct RoundKeys {
   uint32_t w[15][4];
 };
 
-// AES rounds 1..NR on a state that already includes round key 0.
-template <int NR, uint32_t TB>
+// AES rounds R0..NR on a state that already includes rounds < R0.
+template <int NR, uint32_t TB, int R0 = 1>
 __device__ __forceinline__ uint4 aes_rounds(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
                                             const RoundKeys &rk, const uint8_t *smem,
                                             uint32_t lc0, uint32_t lc1) {
 #pragma unroll
-  for (int r = 1; r < NR; r++) {
+  for (int r = R0; r < NR; r++) {
     const uint32_t t0 = round_col<TB>(smem, lc0, lc1, s0, s1, s2, s3, rk.w[r][0]);
     const uint32_t t1 = round_col<TB>(smem, lc0, lc1, s1, s2, s3, s0, rk.w[r][1]);
     const uint32_t t2 = round_col<TB>(smem, lc0, lc1, s2, s3, s0, s1, rk.w[r][2]);
@@ -401,12 +401,43 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   const bool aligned = ((reinterpret_cast<uintptr_t>(src) |
                          reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
   uint4 acc = (q == 15 && live) ? s.ya : make_uint4(0, 0, 0, 0);
+  // Counter-mode caching (Bernstein-Schwabe): within a 256-counter window only
+  // byte 15 of the counter block changes, so round 1 needs one lookup (column
+  // 0, row 3) and round 2 four; K0..K3 / L0..L3 hold the constant parts and
+  // are recomputed when a lane's counter enters a new window.
+  constexpr uint32_t T = kLdsAes;
+  const uint32_t k0 = tload<T>(smem, taddr<0>(lc0, c0)) ^ tload<T>(smem, taddr<1>(lc1, c1)) ^
+                      rotl(tload<T>(smem, taddr<2>(lc0, c2)) ^ rk.w[1][0], 16);
+  uint32_t win = 0xffffffffu, k1 = 0, k2 = 0, k3 = 0, l0 = 0, l1 = 0, l2 = 0, l3 = 0;
   const int iters = wave_max((int)((nb + 15) / 16));
   for (int it = 0; it < iters; it++) {
     const uint64_t j = (uint64_t)it * 16 + q;
     const uint32_t ctr = ctr0 + 1u + (uint32_t)j;  // inc32 wraps mod 2^32
-    const uint4 ks = aes_rounds<NR, kLdsAes>(c0, c1, c2, bswap32(ctr) ^ rk.w[0][3], rk, smem,
-                                             lc0, lc1);
+    const uint32_t s3 = bswap32(ctr) ^ rk.w[0][3];
+    if ((ctr >> 8) != win) {
+      win = ctr >> 8;
+      k1 = round_col<T>(smem, lc0, lc1, c1, c2, s3, c0, rk.w[1][1]);
+      k2 = round_col<T>(smem, lc0, lc1, c2, s3, c0, c1, rk.w[1][2]);
+      k3 = round_col<T>(smem, lc0, lc1, s3, c0, c1, c2, rk.w[1][3]);
+      l0 = tload<T>(smem, taddr<1>(lc1, k1)) ^
+           rotl(tload<T>(smem, taddr<2>(lc0, k2)) ^ tload<T>(smem, taddr<3>(lc1, k3)) ^
+                    rk.w[2][0], 16);
+      l1 = tload<T>(smem, taddr<0>(lc0, k1)) ^ tload<T>(smem, taddr<1>(lc1, k2)) ^
+           rotl(tload<T>(smem, taddr<2>(lc0, k3)) ^ rk.w[2][1], 16);
+      l2 = tload<T>(smem, taddr<0>(lc0, k2)) ^ tload<T>(smem, taddr<1>(lc1, k3)) ^
+           rotl(tload<T>(smem, taddr<3>(lc1, k1)) ^ rk.w[2][2], 16);
+      l3 = tload<T>(smem, taddr<0>(lc0, k3)) ^
+           rotl(tload<T>(smem, taddr<2>(lc0, k1)) ^ tload<T>(smem, taddr<3>(lc1, k2)) ^
+                    rk.w[2][3], 16);
+    }
+    // Round 1: t = (K0 ^ T3[s3 row 3], K1, K2, K3).
+    const uint32_t t0 = k0 ^ rotl(tload<T>(smem, taddr<3>(lc1, s3)), 16);
+    // Round 2.
+    const uint32_t u0 = tload<T>(smem, taddr<0>(lc0, t0)) ^ l0;
+    const uint32_t u1 = rotl(tload<T>(smem, taddr<3>(lc1, t0)), 16) ^ l1;
+    const uint32_t u2 = rotl(tload<T>(smem, taddr<2>(lc0, t0)), 16) ^ l2;
+    const uint32_t u3 = tload<T>(smem, taddr<1>(lc1, t0)) ^ l3;
+    const uint4 ks = aes_rounds<NR, T, 3>(u0, u1, u2, u3, rk, smem, lc0, lc1);
     if (j < nb) {
       const uint64_t rem = m.len - j * 16;
       uint4 x, y;
@@ -556,7 +587,7 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
 int g_num_cus = 0;
 
 template <int NR, bool OPEN>
-int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s) {
+int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const KernelEvents *ev) {
   if (!g_num_cus) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 1;
@@ -572,9 +603,11 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s) {
   hipLaunchKernelGGL((gcm_prologue<NR>), dim3((unsigned)pblocks), dim3(256), 0, s, keys, b, st);
   const uint64_t tiles = (b.num_records + kRecPerTile - 1) / kRecPerTile;
   const unsigned grid = (unsigned)(tiles < (uint64_t)g_num_cus ? tiles : (uint64_t)g_num_cus);
+  if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
   hipLaunchKernelGGL((gcm_kernel<NR, OPEN>), dim3(grid), dim3(kThreads), 0, s, keys, b,
                      (const RecState *)st);
   int rc = (int)hipGetLastError();
+  if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
   hipFreeAsync(st, s);
   return rc;
 }
@@ -582,30 +615,15 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s) {
 }  // namespace
 
 int launch_gcm(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, void *stream,
-               float *timing_ms) {
+               const KernelEvents *ev) {
   if (b.num_records == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (timing_ms) {
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
-    hipEventRecord(e0, s);
-  }
-  int rc;
   switch (nr) {
-    case 10: rc = open ? launch_nr<10, true>(keys, b, s) : launch_nr<10, false>(keys, b, s); break;
-    case 12: rc = open ? launch_nr<12, true>(keys, b, s) : launch_nr<12, false>(keys, b, s); break;
-    case 14: rc = open ? launch_nr<14, true>(keys, b, s) : launch_nr<14, false>(keys, b, s); break;
-    default: rc = 1;
+    case 10: return open ? launch_nr<10, true>(keys, b, s, ev) : launch_nr<10, false>(keys, b, s, ev);
+    case 12: return open ? launch_nr<12, true>(keys, b, s, ev) : launch_nr<12, false>(keys, b, s, ev);
+    case 14: return open ? launch_nr<14, true>(keys, b, s, ev) : launch_nr<14, false>(keys, b, s, ev);
+    default: return 1;
   }
-  if (timing_ms) {
-    hipEventRecord(e1, s);
-    hipEventSynchronize(e1);
-    hipEventElapsedTime(timing_ms, e0, e1);
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-  }
-  return rc;
 }
 
 }  // namespace bssl_amd

@@ -65,13 +65,19 @@ struct BatchDesc {
   uint32_t num_keys;
 };
 
+// HIP events recorded on the launch stream immediately before and after the
+// dominant (bulk) kernel of a batch, for kernel-level timing.
+struct KernelEvents {
+  void *start;
+  void *stop;
+};
+
 // Kernel launchers (gcm.hip / chacha.hip).  Return 0 on success or a HIP
-// error code.  `timing_ms` (optional) receives the kernel's device time
-// measured with HIP events on `stream`.
+// error code.  `ev` (optional) brackets the bulk kernel.
 int launch_gcm(const GcmKeyDev *keys, const BatchDesc &b, bool open,
-               int nr, void *stream, float *timing_ms);
+               int nr, void *stream, const KernelEvents *ev);
 int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open,
-                  void *stream, float *timing_ms);
+                  void *stream, const KernelEvents *ev);
 int launch_synth(uint64_t first, size_t n, const uint64_t *offsets,
                  const uint64_t *lengths, uint8_t *pt, uint8_t *nonces,
                  uint8_t *ads, void *stream);

@@ -254,10 +254,14 @@ BSSL_AMD_EXPORT int BSSL_AMD_synth_fill_device(uint64_t first_record, size_t n,
                                                uint8_t *pt, uint8_t *nonces,
                                                uint8_t *ads, void *hip_stream);
 
-/* Kernel-level statistics of the last batch launched by this thread: the
- * dominant kernel's name and its device time in ms, measured with HIP events
- * on the launch stream when timing is enabled (BSSL_AMD_set_kernel_timing). */
+/* Kernel-level timing for this host thread.  While enabled, every batch
+ * launch records HIP events on its stream around its bulk kernel (no host
+ * synchronisation).  BSSL_AMD_collect_kernel_times waits for the recorded
+ * launches, writes up to `max` durations (ms) in launch order and returns how
+ * many launches were pending.  last_kernel_ms / _name describe the most
+ * recent one. */
 BSSL_AMD_EXPORT void BSSL_AMD_set_kernel_timing(int enable);
+BSSL_AMD_EXPORT size_t BSSL_AMD_collect_kernel_times(double *out_ms, size_t max);
 BSSL_AMD_EXPORT double BSSL_AMD_last_kernel_ms(void);
 BSSL_AMD_EXPORT const char *BSSL_AMD_last_kernel_name(void);
 

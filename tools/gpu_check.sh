@@ -23,8 +23,13 @@ for s in $STEPS; do
     pytest) run pytest 1500 python -m pytest tests/test_gpu_parity.py -q -m gpu -rf ${PYTEST_ARGS:-} ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} ;;
-    pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc1 -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} &&
-         run pmc2 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc2 -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} ;;
+    pmc)
+      PB="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --records ${PMC_RECORDS:-262144} ${BENCH_ARGS:-}"
+      run pmc_a 600 rocprofv3 --kernel-include-regex "${PMC_KERNEL:-gcm_kernel}" --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmc_a -o run --output-format csv -- $PB
+      run pmc_b 600 rocprofv3 --kernel-include-regex "${PMC_KERNEL:-gcm_kernel}" --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY -d gpurun_out/pmc_b -o run --output-format csv -- $PB
+      run pmc_c 600 rocprofv3 --kernel-include-regex "${PMC_KERNEL:-gcm_kernel}" --pmc FETCH_SIZE -d gpurun_out/pmc_c -o run --output-format csv -- $PB
+      run pmc_d 600 rocprofv3 --kernel-include-regex "${PMC_KERNEL:-gcm_kernel}" --pmc WRITE_SIZE -d gpurun_out/pmc_d -o run --output-format csv -- $PB
+      ;;
     *) echo "unknown step $s" ;;
   esac
 done
