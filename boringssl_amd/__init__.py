@@ -19,7 +19,8 @@ except ImportError:  # pragma: no cover
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libbssl_amd.so")
+# BSSL_AMD_LIB may point at a diagnostic build (csrc/Makefile `ablate`).
+LIB_PATH = os.environ.get("BSSL_AMD_LIB", os.path.join(_HERE, "libbssl_amd.so"))
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

@@ -32,13 +32,26 @@
 
 #include "internal.h"
 
+#ifndef BSSL_AMD_ABLATE
+#define BSSL_AMD_ABLATE 0
+#endif
+
 namespace bssl_amd {
 namespace {
 
-constexpr int kWaves = 16;
+// Waves per workgroup (one workgroup per CU: the LDS tables take 104 KiB) and
+// AES streams per lane; build-time knobs for tuning (-DBSSL_AMD_GCM_WAVES=..).
+#ifndef BSSL_AMD_GCM_WAVES
+#define BSSL_AMD_GCM_WAVES 12
+#endif
+#ifndef BSSL_AMD_GCM_STREAMS
+#define BSSL_AMD_GCM_STREAMS 1
+#endif
+constexpr int kWaves = BSSL_AMD_GCM_WAVES;
+constexpr int kStreams = BSSL_AMD_GCM_STREAMS;
 constexpr int kThreads = kWaves * 64;
 constexpr int kRecPerWave = 4;
-constexpr int kRecPerTile = kWaves * kRecPerWave;  // 64
+constexpr int kRecPerTile = kWaves * kRecPerWave;  // <= 64 (one planning wave)
 
 // ---------------------------------------------------------------------------
 // Compile-time AES tables.
@@ -177,27 +190,68 @@ struct RoundKeys {
   uint32_t w[15][4];
 };
 
+// One full AES round on all four columns.  All 16 lookups are issued before
+// any is consumed so a wave keeps 16 LDS reads in flight (the per-column form
+// lets hipcc wait after every 4).
+template <uint32_t TB>
+__device__ __forceinline__ void aes_round(uint32_t &s0, uint32_t &s1, uint32_t &s2,
+                                          uint32_t &s3, const uint32_t *rkx,
+                                          const uint8_t *smem, uint32_t lc0, uint32_t lc1) {
+  const uint32_t a00 = taddr<0>(lc0, s0), a01 = taddr<1>(lc1, s1), a02 = taddr<2>(lc0, s2),
+                 a03 = taddr<3>(lc1, s3);
+  const uint32_t a10 = taddr<0>(lc0, s1), a11 = taddr<1>(lc1, s2), a12 = taddr<2>(lc0, s3),
+                 a13 = taddr<3>(lc1, s0);
+  const uint32_t a20 = taddr<0>(lc0, s2), a21 = taddr<1>(lc1, s3), a22 = taddr<2>(lc0, s0),
+                 a23 = taddr<3>(lc1, s1);
+  const uint32_t a30 = taddr<0>(lc0, s3), a31 = taddr<1>(lc1, s0), a32 = taddr<2>(lc0, s1),
+                 a33 = taddr<3>(lc1, s2);
+  const uint32_t x00 = tload<TB>(smem, a00), x01 = tload<TB>(smem, a01),
+                 x02 = tload<TB>(smem, a02), x03 = tload<TB>(smem, a03);
+  const uint32_t x10 = tload<TB>(smem, a10), x11 = tload<TB>(smem, a11),
+                 x12 = tload<TB>(smem, a12), x13 = tload<TB>(smem, a13);
+  const uint32_t x20 = tload<TB>(smem, a20), x21 = tload<TB>(smem, a21),
+                 x22 = tload<TB>(smem, a22), x23 = tload<TB>(smem, a23);
+  const uint32_t x30 = tload<TB>(smem, a30), x31 = tload<TB>(smem, a31),
+                 x32 = tload<TB>(smem, a32), x33 = tload<TB>(smem, a33);
+  s0 = xor3(x00, x01, rotl(xor3(x02, x03, rkx[0]), 16));
+  s1 = xor3(x10, x11, rotl(xor3(x12, x13, rkx[1]), 16));
+  s2 = xor3(x20, x21, rotl(xor3(x22, x23, rkx[2]), 16));
+  s3 = xor3(x30, x31, rotl(xor3(x32, x33, rkx[3]), 16));
+}
+
 // AES rounds R0..NR on a state that already includes rounds < R0.
 template <int NR, uint32_t TB, int R0 = 1>
 __device__ __forceinline__ uint4 aes_rounds(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
                                             const RoundKeys &rk, const uint8_t *smem,
                                             uint32_t lc0, uint32_t lc1) {
 #pragma unroll
-  for (int r = R0; r < NR; r++) {
-    const uint32_t t0 = round_col<TB>(smem, lc0, lc1, s0, s1, s2, s3, rk.w[r][0]);
-    const uint32_t t1 = round_col<TB>(smem, lc0, lc1, s1, s2, s3, s0, rk.w[r][1]);
-    const uint32_t t2 = round_col<TB>(smem, lc0, lc1, s2, s3, s0, s1, rk.w[r][2]);
-    const uint32_t t3 = round_col<TB>(smem, lc0, lc1, s3, s0, s1, s2, rk.w[r][3]);
-    s0 = t0;
-    s1 = t1;
-    s2 = t2;
-    s3 = t3;
-  }
+  for (int r = R0; r < NR; r++) aes_round<TB>(s0, s1, s2, s3, rk.w[r], smem, lc0, lc1);
+  const uint32_t a00 = taddr<0>(lc0, s0), a01 = taddr<1>(lc0, s1), a02 = taddr<2>(lc0, s2),
+                 a03 = taddr<3>(lc0, s3);
+  const uint32_t a10 = taddr<0>(lc0, s1), a11 = taddr<1>(lc0, s2), a12 = taddr<2>(lc0, s3),
+                 a13 = taddr<3>(lc0, s0);
+  const uint32_t a20 = taddr<0>(lc0, s2), a21 = taddr<1>(lc0, s3), a22 = taddr<2>(lc0, s0),
+                 a23 = taddr<3>(lc0, s1);
+  const uint32_t a30 = taddr<0>(lc0, s3), a31 = taddr<1>(lc0, s0), a32 = taddr<2>(lc0, s1),
+                 a33 = taddr<3>(lc0, s2);
+  const uint32_t x00 = tload<TB>(smem, a00), x01 = tload<TB>(smem, a01),
+                 x02 = tload<TB>(smem, a02), x03 = tload<TB>(smem, a03);
+  const uint32_t x10 = tload<TB>(smem, a10), x11 = tload<TB>(smem, a11),
+                 x12 = tload<TB>(smem, a12), x13 = tload<TB>(smem, a13);
+  const uint32_t x20 = tload<TB>(smem, a20), x21 = tload<TB>(smem, a21),
+                 x22 = tload<TB>(smem, a22), x23 = tload<TB>(smem, a23);
+  const uint32_t x30 = tload<TB>(smem, a30), x31 = tload<TB>(smem, a31),
+                 x32 = tload<TB>(smem, a32), x33 = tload<TB>(smem, a33);
+  // Last round: S[x] is byte 1 (and byte 2) of Te0[x].
   uint4 o;
-  o.x = last_col<TB>(smem, lc0, s0, s1, s2, s3, rk.w[NR][0]);
-  o.y = last_col<TB>(smem, lc0, s1, s2, s3, s0, rk.w[NR][1]);
-  o.z = last_col<TB>(smem, lc0, s2, s3, s0, s1, rk.w[NR][2]);
-  o.w = last_col<TB>(smem, lc0, s3, s0, s1, s2, rk.w[NR][3]);
+  o.x = xor3(__builtin_amdgcn_perm(x01, x00, 0x0c0c0501u),
+             __builtin_amdgcn_perm(x03, x02, 0x06020c0cu), rk.w[NR][0]);
+  o.y = xor3(__builtin_amdgcn_perm(x11, x10, 0x0c0c0501u),
+             __builtin_amdgcn_perm(x13, x12, 0x06020c0cu), rk.w[NR][1]);
+  o.z = xor3(__builtin_amdgcn_perm(x21, x20, 0x0c0c0501u),
+             __builtin_amdgcn_perm(x23, x22, 0x06020c0cu), rk.w[NR][2]);
+  o.w = xor3(__builtin_amdgcn_perm(x31, x30, 0x0c0c0501u),
+             __builtin_amdgcn_perm(x33, x32, 0x06020c0cu), rk.w[NR][3]);
   return o;
 }
 
@@ -301,6 +355,59 @@ __device__ __forceinline__ RecordMeta record_meta(const BatchDesc &b, uint64_t i
   m.ad_off = b.ad_offsets ? b.ad_offsets[i] : i * b.ad_stride;
   m.ad_len = b.ad_lengths ? b.ad_lengths[i] : b.ad_len;
   return m;
+}
+
+// Counter-mode cache of one AES stream (see process_records).
+struct WindowCache {
+  uint32_t win = 0xffffffffu, k1 = 0, k2 = 0, k3 = 0, l0 = 0, l1 = 0, l2 = 0, l3 = 0;
+
+  template <uint32_t T>
+  __device__ __forceinline__ void update(uint32_t ctr, uint32_t s3, uint32_t c0, uint32_t c1,
+                                         uint32_t c2, const RoundKeys &rk,
+                                         const uint8_t *smem, uint32_t lc0, uint32_t lc1) {
+    if ((ctr >> 8) == win) return;
+    win = ctr >> 8;
+    k1 = round_col<T>(smem, lc0, lc1, c1, c2, s3, c0, rk.w[1][1]);
+    k2 = round_col<T>(smem, lc0, lc1, c2, s3, c0, c1, rk.w[1][2]);
+    k3 = round_col<T>(smem, lc0, lc1, s3, c0, c1, c2, rk.w[1][3]);
+    l0 = tload<T>(smem, taddr<1>(lc1, k1)) ^
+         rotl(tload<T>(smem, taddr<2>(lc0, k2)) ^ tload<T>(smem, taddr<3>(lc1, k3)) ^
+                  rk.w[2][0], 16);
+    l1 = tload<T>(smem, taddr<0>(lc0, k1)) ^ tload<T>(smem, taddr<1>(lc1, k2)) ^
+         rotl(tload<T>(smem, taddr<2>(lc0, k3)) ^ rk.w[2][1], 16);
+    l2 = tload<T>(smem, taddr<0>(lc0, k2)) ^ tload<T>(smem, taddr<1>(lc1, k3)) ^
+         rotl(tload<T>(smem, taddr<3>(lc1, k1)) ^ rk.w[2][2], 16);
+    l3 = tload<T>(smem, taddr<0>(lc0, k3)) ^
+         rotl(tload<T>(smem, taddr<2>(lc0, k1)) ^ tload<T>(smem, taddr<3>(lc1, k2)) ^
+                  rk.w[2][3], 16);
+  }
+
+  // Rounds 1 and 2 of a counter block whose round-0 word 3 is s3.
+  template <uint32_t T>
+  __device__ __forceinline__ void rounds12(uint32_t k0, uint32_t s3, uint32_t &u0, uint32_t &u1,
+                                           uint32_t &u2, uint32_t &u3, const uint8_t *smem,
+                                           uint32_t lc0, uint32_t lc1) const {
+    const uint32_t t0 = k0 ^ rotl(tload<T>(smem, taddr<3>(lc1, s3)), 16);
+    u0 = tload<T>(smem, taddr<0>(lc0, t0)) ^ l0;
+    u1 = rotl(tload<T>(smem, taddr<3>(lc1, t0)), 16) ^ l1;
+    u2 = rotl(tload<T>(smem, taddr<2>(lc0, t0)), 16) ^ l2;
+    u3 = tload<T>(smem, taddr<1>(lc1, t0)) ^ l3;
+  }
+};
+
+// Two interleaved AES streams, rounds R0..NR.
+template <int NR, uint32_t TB, int R0>
+__device__ __forceinline__ void aes_rounds2(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
+                                            uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3,
+                                            const RoundKeys &rk, const uint8_t *smem,
+                                            uint32_t lc0, uint32_t lc1, uint4 &oa, uint4 &ob) {
+#pragma unroll
+  for (int r = R0; r < NR; r++) {
+    aes_round<TB>(a0, a1, a2, a3, rk.w[r], smem, lc0, lc1);
+    aes_round<TB>(b0, b1, b2, b3, rk.w[r], smem, lc0, lc1);
+  }
+  oa = aes_rounds<NR, TB, NR>(a0, a1, a2, a3, rk, smem, lc0, lc1);
+  ob = aes_rounds<NR, TB, NR>(b0, b1, b2, b3, rk, smem, lc0, lc1);
 }
 
 // Per-record state handed from the prologue to the bulk kernel (64 bytes).
@@ -408,50 +515,66 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   constexpr uint32_t T = kLdsAes;
   const uint32_t k0 = tload<T>(smem, taddr<0>(lc0, c0)) ^ tload<T>(smem, taddr<1>(lc1, c1)) ^
                       rotl(tload<T>(smem, taddr<2>(lc0, c2)) ^ rk.w[1][0], 16);
-  uint32_t win = 0xffffffffu, k1 = 0, k2 = 0, k3 = 0, l0 = 0, l1 = 0, l2 = 0, l3 = 0;
-  const int iters = wave_max((int)((nb + 15) / 16));
+  WindowCache wa, wb;
+  // kStreams independent counter blocks per lane per iteration (j, j+16)
+  // give each wave that many AES dependency chains to interleave.
+  constexpr int S = kStreams;
+  const int iters = wave_max((int)((nb + 16 * S - 1) / (16 * S)));
   for (int it = 0; it < iters; it++) {
-    const uint64_t j = (uint64_t)it * 16 + q;
-    const uint32_t ctr = ctr0 + 1u + (uint32_t)j;  // inc32 wraps mod 2^32
-    const uint32_t s3 = bswap32(ctr) ^ rk.w[0][3];
-    if ((ctr >> 8) != win) {
-      win = ctr >> 8;
-      k1 = round_col<T>(smem, lc0, lc1, c1, c2, s3, c0, rk.w[1][1]);
-      k2 = round_col<T>(smem, lc0, lc1, c2, s3, c0, c1, rk.w[1][2]);
-      k3 = round_col<T>(smem, lc0, lc1, s3, c0, c1, c2, rk.w[1][3]);
-      l0 = tload<T>(smem, taddr<1>(lc1, k1)) ^
-           rotl(tload<T>(smem, taddr<2>(lc0, k2)) ^ tload<T>(smem, taddr<3>(lc1, k3)) ^
-                    rk.w[2][0], 16);
-      l1 = tload<T>(smem, taddr<0>(lc0, k1)) ^ tload<T>(smem, taddr<1>(lc1, k2)) ^
-           rotl(tload<T>(smem, taddr<2>(lc0, k3)) ^ rk.w[2][1], 16);
-      l2 = tload<T>(smem, taddr<0>(lc0, k2)) ^ tload<T>(smem, taddr<1>(lc1, k3)) ^
-           rotl(tload<T>(smem, taddr<3>(lc1, k1)) ^ rk.w[2][2], 16);
-      l3 = tload<T>(smem, taddr<0>(lc0, k3)) ^
-           rotl(tload<T>(smem, taddr<2>(lc0, k1)) ^ tload<T>(smem, taddr<3>(lc1, k2)) ^
-                    rk.w[2][3], 16);
+    const uint64_t ja = (uint64_t)it * 16 * S + q, jb = ja + 16;
+    const bool fa = ja < nb && aligned && m.len - ja * 16 >= 16;
+    const bool fb = S == 2 && jb < nb && aligned && m.len - jb * 16 >= 16;
+    uint4 xa = make_uint4(0, 0, 0, 0), xb = make_uint4(0, 0, 0, 0);
+    if (fa) xa = *reinterpret_cast<const uint4 *>(src + ja * 16);
+    if (fb) xb = *reinterpret_cast<const uint4 *>(src + jb * 16);
+    const uint32_t ctra = ctr0 + 1u + (uint32_t)ja;  // inc32 wraps mod 2^32
+    const uint32_t sa = bswap32(ctra) ^ rk.w[0][3];
+    wa.update<T>(ctra, sa, c0, c1, c2, rk, smem, lc0, lc1);
+    uint32_t a0, a1, a2, a3;
+    wa.rounds12<T>(k0, sa, a0, a1, a2, a3, smem, lc0, lc1);
+    uint4 ksa, ksb = make_uint4(0, 0, 0, 0);
+    if constexpr (S == 2) {
+      const uint32_t ctrb = ctr0 + 1u + (uint32_t)jb;
+      const uint32_t sb = bswap32(ctrb) ^ rk.w[0][3];
+      wb.update<T>(ctrb, sb, c0, c1, c2, rk, smem, lc0, lc1);
+      uint32_t b0, b1, b2, b3;
+      wb.rounds12<T>(k0, sb, b0, b1, b2, b3, smem, lc0, lc1);
+#if BSSL_AMD_ABLATE == 2  // diagnostic build: no AES rounds 3..NR (wrong output)
+      ksa = make_uint4(a0, a1, a2, a3);
+      ksb = make_uint4(b0, b1, b2, b3);
+#else
+      aes_rounds2<NR, T, 3>(a0, a1, a2, a3, b0, b1, b2, b3, rk, smem, lc0, lc1, ksa, ksb);
+#endif
+    } else {
+#if BSSL_AMD_ABLATE == 2
+      ksa = make_uint4(a0, a1, a2, a3);
+#else
+      ksa = aes_rounds<NR, T, 3>(a0, a1, a2, a3, rk, smem, lc0, lc1);
+#endif
     }
-    // Round 1: t = (K0 ^ T3[s3 row 3], K1, K2, K3).
-    const uint32_t t0 = k0 ^ rotl(tload<T>(smem, taddr<3>(lc1, s3)), 16);
-    // Round 2.
-    const uint32_t u0 = tload<T>(smem, taddr<0>(lc0, t0)) ^ l0;
-    const uint32_t u1 = rotl(tload<T>(smem, taddr<3>(lc1, t0)), 16) ^ l1;
-    const uint32_t u2 = rotl(tload<T>(smem, taddr<2>(lc0, t0)), 16) ^ l2;
-    const uint32_t u3 = tload<T>(smem, taddr<1>(lc1, t0)) ^ l3;
-    const uint4 ks = aes_rounds<NR, T, 3>(u0, u1, u2, u3, rk, smem, lc0, lc1);
-    if (j < nb) {
-      const uint64_t rem = m.len - j * 16;
-      uint4 x, y;
-      if (rem >= 16 && aligned) {
-        x = *reinterpret_cast<const uint4 *>(src + j * 16);
-        y = xor4(x, ks);
-        *reinterpret_cast<uint4 *>(dst + j * 16) = y;
-      } else {
-        const uint32_t n = (uint32_t)min<uint64_t>(rem, 16);
-        x = load_partial(src + j * 16, n);
-        y = mask_block(xor4(x, ks), n);
-        store_partial(dst + j * 16, y, n);
+#pragma unroll
+    for (int h = 0; h < S; h++) {
+      const uint64_t j = h ? jb : ja;
+      if (j < nb) {
+        const uint4 ks = h ? ksb : ksa;
+        const bool full = h ? fb : fa;
+        uint4 x, y;
+        if (full) {
+          x = h ? xb : xa;
+          y = xor4(x, ks);
+          *reinterpret_cast<uint4 *>(dst + j * 16) = y;
+        } else {
+          const uint32_t n = (uint32_t)min<uint64_t>(m.len - j * 16, 16);
+          x = load_partial(src + j * 16, n);
+          y = mask_block(xor4(x, ks), n);
+          store_partial(dst + j * 16, y, n);
+        }
+#if BSSL_AMD_ABLATE == 1  // diagnostic build: no GHASH multiply (wrong tags)
+        acc = xor4(acc, OPEN ? x : y);
+#else
+        acc = xor4(gmul<kLdsGhash + 4 * 8192>(acc, smem, mf0), OPEN ? x : y);
+#endif
       }
-      acc = xor4(gmul<kLdsGhash + 4 * 8192>(acc, smem, mf0), OPEN ? x : y);
     }
   }
   // Lane algebra: lane q holds the virtual elements v = q+1+16i of
@@ -513,7 +636,7 @@ template <int NR, bool OPEN>
 __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restrict__ keys,
                                                       BatchDesc b,
                                                       const RecState *__restrict__ st) {
-  static_assert(kRecPerTile == 64, "one wave plans a tile with ballots");
+  static_assert(kRecPerTile <= 64, "one wave plans a tile with ballots");
   __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
   // Pass list of the current tile: key and 64-bit record mask per pass.
   __shared__ uint32_t s_pass_key[kRecPerTile];
@@ -543,7 +666,7 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
     if (wave == 0) {
       // Plan the tile: one pass per distinct key, in record order.
       const uint64_t i = base + lane;
-      uint32_t k = i < n ? (b.key_index ? b.key_index[i] : 0u) : 0xffffffffu;
+      uint32_t k = (lane < kRecPerTile && i < n) ? (b.key_index ? b.key_index[i] : 0u) : 0xffffffffu;
       if (k != 0xffffffffu && k >= b.num_keys) k = 0;  // flagged dead by the prologue
       uint64_t pending = __ballot(k != 0xffffffffu);
       int np = 0;
