@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""End-to-end seal rate when records start and end in HOST memory (TLS socket
+buffers): pinned host buffers -> hipMemcpyAsync H2D -> batch seal ->
+hipMemcpyAsync D2H, pipelined over NSTREAMS streams in chunks.  Reported in
+DESIGN.md; never the bench `value` (which is device-resident).
+
+Usage: python tools/e2e_bench.py [--records 262144] [--chunk 16384] [--streams 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import boringssl_amd as ba  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="config2")
+    ap.add_argument("--records", type=int, default=262144)
+    ap.add_argument("--chunk", type=int, default=16384)
+    ap.add_argument("--streams", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    aead, key_len, _, length, _ = bench.CONFIGS[args.config]
+    assert length != "mixed"
+    n, c = args.records, args.chunk
+    stride = (length + 15) // 16 * 16
+    # Host inputs: synthetic records generated on the device once, copied to
+    # pinned host memory (the "socket buffers").
+    h_pt = torch.empty(n * stride, dtype=torch.uint8).pin_memory()
+    h_ct = torch.empty(n * stride, dtype=torch.uint8).pin_memory()
+    h_tags = torch.empty(n * 16, dtype=torch.uint8).pin_memory()
+    h_nonce = torch.empty(n * 12, dtype=torch.uint8).pin_memory()
+    h_ad = torch.empty(n * 13, dtype=torch.uint8).pin_memory()
+    for s0 in range(0, n, c):
+        m = min(c, n - s0)
+        lens = torch.full((m,), length, dtype=torch.int64, device=dev)
+        offs = torch.arange(m, dtype=torch.int64, device=dev) * stride
+        d = torch.empty(m * stride, dtype=torch.uint8, device=dev)
+        dn = torch.empty(m * 12, dtype=torch.uint8, device=dev)
+        da = torch.empty(m * 13, dtype=torch.uint8, device=dev)
+        ba.synth_fill_device(s0, m, offs, lens, d, dn, da)
+        h_pt[s0 * stride:(s0 + m) * stride].copy_(d)
+        h_nonce[s0 * 12:(s0 + m) * 12].copy_(dn)
+        h_ad[s0 * 13:(s0 + m) * 13].copy_(da)
+    torch.cuda.synchronize()
+    ctx = ba.AEADCtx(aead, bench.synth_key(0, key_len), 16)
+    streams = [torch.cuda.Stream() for _ in range(args.streams)]
+    slots = []
+    for _ in range(args.streams):
+        slots.append(dict(pt=torch.empty(c * stride, dtype=torch.uint8, device=dev),
+                          ct=torch.empty(c * stride, dtype=torch.uint8, device=dev),
+                          tags=torch.empty(c * 16, dtype=torch.uint8, device=dev),
+                          nonce=torch.empty(c * 12, dtype=torch.uint8, device=dev),
+                          ad=torch.empty(c * 13, dtype=torch.uint8, device=dev)))
+
+    def run():
+        for i, s0 in enumerate(range(0, n, c)):
+            m = min(c, n - s0)
+            st, sl = streams[i % len(streams)], slots[i % len(streams)]
+            with torch.cuda.stream(st):
+                sl["pt"][:m * stride].copy_(h_pt[s0 * stride:(s0 + m) * stride], non_blocking=True)
+                sl["nonce"][:m * 12].copy_(h_nonce[s0 * 12:(s0 + m) * 12], non_blocking=True)
+                sl["ad"][:m * 13].copy_(h_ad[s0 * 13:(s0 + m) * 13], non_blocking=True)
+                b = ba.make_batch(m, sl["pt"], sl["ct"], sl["tags"], sl["nonce"], 12, sl["ad"],
+                                  record_stride=stride, record_len=length, ad_stride=13, ad_len=13)
+                ctx.seal_batch_device(b, st)
+                h_ct[s0 * stride:(s0 + m) * stride].copy_(sl["ct"][:m * stride], non_blocking=True)
+                h_tags[s0 * 16:(s0 + m) * 16].copy_(sl["tags"][:m * 16], non_blocking=True)
+        torch.cuda.synchronize()
+
+    run()
+    times = []
+    for _ in range(args.reps):
+        t0 = time.perf_counter()
+        run()
+        times.append(time.perf_counter() - t0)
+    # copy-only rates for context
+    d_big = torch.empty(n * stride, dtype=torch.uint8, device=dev)
+    t0 = time.perf_counter(); d_big.copy_(h_pt, non_blocking=True); torch.cuda.synchronize()
+    h2d = n * stride / (time.perf_counter() - t0) / 2**30
+    t0 = time.perf_counter(); h_ct.copy_(d_big, non_blocking=True); torch.cuda.synchronize()
+    d2h = n * stride / (time.perf_counter() - t0) / 2**30
+    best = min(times)
+    print(json.dumps({"e2e_gib_per_s": round(n * length / best / 2**30, 2),
+                      "records": n, "record_bytes": length, "chunk_records": c,
+                      "streams": args.streams, "h2d_gib_per_s": round(h2d, 2),
+                      "d2h_gib_per_s": round(d2h, 2), "times_s": [round(t, 4) for t in times]}))
+
+
+if __name__ == "__main__":
+    main()
