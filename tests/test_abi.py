@@ -92,3 +92,14 @@ def test_zeroed_ctx_cleanup_is_safe():
     ba.lib.EVP_AEAD_CTX_zero(ctypes.byref(ctx))
     ba.lib.EVP_AEAD_CTX_cleanup(ctypes.byref(ctx))
     ba.lib.EVP_AEAD_CTX_cleanup(ctypes.byref(ctx))
+
+
+def test_plain_c_caller_compiles_and_links(tmp_path):
+    """A C program written against the reference API links to the library."""
+    import boringssl_amd as ba
+    exe = tmp_path / "seal_one"
+    subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "examples", "seal_one.c"),
+                           "-L", os.path.dirname(ba.LIB_PATH), "-lbssl_amd",
+                           f"-Wl,-rpath,{os.path.dirname(ba.LIB_PATH)}", "-o", str(exe)])
+    assert exe.exists()
