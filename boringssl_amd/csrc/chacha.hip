@@ -7,16 +7,19 @@
 // poly1305.cc) / the fused chacha20_poly1305_seal_avx2 (chacha20_poly1305_
 // x86_64.pl:861).  Design:
 //
-// * 16 lanes per record, 4 records per wave.  Lane q owns the record's 64-byte
-//   ChaCha blocks u = q, q+16, ... (block counter 1+u, RFC 8439): one lane per
-//   64-byte block, keystream XORed with the input in registers.
-// * Poly1305: the four 16-byte Poly blocks of ChaCha block u form one unit
-//   U_u = ((M0 r + M1) r + M2) r + M3.  A lane folds its units with Horner's
-//   rule in R = r^4 at stride 16 (multiplier R^16 = r^64); the 16 lane
-//   accumulators are rotated into exponent order and tree-combined with R,
-//   R^2, R^4, R^8 -- the same lane algebra as the GHASH of gcm.hip, here in
-//   GF(2^130-5) with 26-bit limbs.  A trailing partial unit and the AD are
-//   folded in afterwards; the tag is (((Z r) + L) r mod p + s) mod 2^128.
+// * L = 8 lanes per record, 8 records per wave.  The record's ChaCha blocks
+//   u = 0..n (u = 0: the Poly1305 key block, counter 0; u >= 1: data block u-1,
+//   counter u, RFC 8439) are dealt round-robin to the lanes: one lane per
+//   64-byte block, keystream XORed with the input in registers.  Folding the
+//   key block into slot 0 keeps a 1350-byte record at 23 blocks in 24 slots.
+// * Poly1305: the four 16-byte Poly blocks of data block d form one unit
+//   U = M0 r^3 + M1 r^2 + M2 r + M3.  A lane folds its units with Horner's
+//   rule in R = r^4 at stride L (multiplier R^L), one lazily reduced sum of
+//   four products per unit; the L lane accumulators are rotated into exponent
+//   order and tree-combined with R, R^2, R^4 -- the same lane algebra as the
+//   GHASH of gcm.hip, here in GF(2^130-5) with 26-bit limbs.  A trailing
+//   partial unit and the AD are folded in afterwards; the tag is
+//   (((Z r) + L) r mod p + s) mod 2^128.
 #include <hip/hip_runtime.h>
 
 #include "internal.h"
@@ -25,7 +28,6 @@ namespace bssl_amd {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kRecPerBlock = kThreads / 16;
 constexpr uint32_t kM26 = 0x3ffffff;
 
 __device__ __forceinline__ uint32_t rotl(uint32_t v, int n) {
@@ -147,20 +149,6 @@ __device__ __forceinline__ P pshfl_down(const P &v, int d, int width) {
   return o;
 }
 
-// Tree-combine the 16 lane accumulators of a group (see gcm.hip
-// group_combine); pw[t] = base^(2^t).  All 64 lanes must call it.
-__device__ __forceinline__ P group_combine(const P &acc, int q, int src, const P pw[4]) {
-  P a = pshfl(acc, src, 16);
-#pragma unroll
-  for (int t = 0; t < 4; t++) {
-    const int s = 1 << t;
-    P m = pmul(a, pw[t]);
-    P o = pshfl_down(a, s, 16);
-    if ((q & (2 * s - 1)) == 0) a = padd(m, o);
-  }
-  return pshfl(a, 0, 16);
-}
-
 __device__ __forceinline__ int wave_max(int v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
@@ -217,12 +205,67 @@ struct RecordMeta {
   uint64_t off, len, ad_off, ad_len;
 };
 
-template <bool OPEN>
+// Lazily reduced sum of products: d_i += a * r (no carry propagation).
+struct PAcc {
+  uint64_t d[5];
+};
+
+__device__ __forceinline__ PAcc pacc_zero() { return PAcc{{0, 0, 0, 0, 0}}; }
+
+__device__ __forceinline__ void pmac(PAcc &acc, const P &a, const P &r) {
+  const uint32_t s1 = r.h[1] * 5, s2 = r.h[2] * 5, s3 = r.h[3] * 5, s4 = r.h[4] * 5;
+  acc.d[0] += mul64(a.h[0], r.h[0]) + mul64(a.h[1], s4) + mul64(a.h[2], s3) +
+              mul64(a.h[3], s2) + mul64(a.h[4], s1);
+  acc.d[1] += mul64(a.h[0], r.h[1]) + mul64(a.h[1], r.h[0]) + mul64(a.h[2], s4) +
+              mul64(a.h[3], s3) + mul64(a.h[4], s2);
+  acc.d[2] += mul64(a.h[0], r.h[2]) + mul64(a.h[1], r.h[1]) + mul64(a.h[2], r.h[0]) +
+              mul64(a.h[3], s4) + mul64(a.h[4], s3);
+  acc.d[3] += mul64(a.h[0], r.h[3]) + mul64(a.h[1], r.h[2]) + mul64(a.h[2], r.h[1]) +
+              mul64(a.h[3], r.h[0]) + mul64(a.h[4], s4);
+  acc.d[4] += mul64(a.h[0], r.h[4]) + mul64(a.h[1], r.h[3]) + mul64(a.h[2], r.h[2]) +
+              mul64(a.h[3], r.h[1]) + mul64(a.h[4], r.h[0]);
+}
+
+// Carry-propagate a lazy sum (at most 4 products of limbs < 2^27.1 and
+// powers < 2^26.01: every d_i < 2^60).
+__device__ __forceinline__ P preduce(PAcc a) {
+  P o;
+  uint64_t c;
+  o.h[0] = (uint32_t)a.d[0] & kM26;
+  c = a.d[0] >> 26;
+  a.d[1] += c;
+  o.h[1] = (uint32_t)a.d[1] & kM26;
+  c = a.d[1] >> 26;
+  a.d[2] += c;
+  o.h[2] = (uint32_t)a.d[2] & kM26;
+  c = a.d[2] >> 26;
+  a.d[3] += c;
+  o.h[3] = (uint32_t)a.d[3] & kM26;
+  c = a.d[3] >> 26;
+  a.d[4] += c;
+  o.h[4] = (uint32_t)a.d[4] & kM26;
+  c = a.d[4] >> 26;
+  const uint64_t h0 = (uint64_t)o.h[0] + c * 5;
+  o.h[0] = (uint32_t)h0 & kM26;
+  o.h[1] += (uint32_t)(h0 >> 26);
+  return o;
+}
+
+// ChaCha20-Poly1305 over L lanes per record (64/L records per wave).
+// ChaCha blocks u = 0..nblk of a record are dealt round-robin to the lanes
+// (u = it*L + q): u = 0 is the Poly1305 key block (counter 0), u >= 1 the data
+// block u-1 (counter u).  Poly1305 runs on the virtual sequence
+// [Y_A, U_0, U_1, ...] of 4-block units, element v = u in lane u mod L, with
+// Horner's rule in R = r^4 at stride L (multiplier R^L), then the rotation +
+// log2(L)-level tree of gcm.hip's lane algebra.
+template <bool OPEN, int L>
 __global__ __launch_bounds__(kThreads) void chacha_poly_kernel(
     const ChaChaKeyDev *__restrict__ keys, BatchDesc b) {
+  static_assert(L == 4 || L == 8 || L == 16, "lanes per record");
+  constexpr int kLog = L == 4 ? 2 : L == 8 ? 3 : 4;
   const int lane = threadIdx.x & 63;
-  const int q = lane & 15;
-  const uint64_t rec = (uint64_t)blockIdx.x * kRecPerBlock + (threadIdx.x >> 4);
+  const int q = lane & (L - 1);
+  const uint64_t rec = ((uint64_t)blockIdx.x * kThreads + threadIdx.x) / L;
   const bool active = rec < b.num_records;
   RecordMeta m = {0, 0, 0, 0};
   uint32_t kidx = 0;
@@ -246,36 +289,85 @@ __global__ __launch_bounds__(kThreads) void chacha_poly_kernel(
 #pragma unroll
     for (int i = 0; i < 3; i++) nonce[i] = load_le32_bytes(np + 4 * i, live ? 4 : 0);
   }
+  const uint64_t nblk = live ? (m.len + 63) / 64 : 0;  // ChaCha data blocks
+  const uint64_t npoly = live ? (m.len + 15) / 16 : 0;
+  const uint64_t nunits = npoly / 4;                   // full 4-block units
+  const uint32_t tail_blocks = (uint32_t)(npoly & 3);
+  const uint8_t *src = b.in + m.off;
+  uint8_t *dst = b.out + m.off;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(src) |
+                         reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
 
-  // Poly1305 key = ChaCha20(counter 0)[0:32] (e_chacha20poly1305.cc:89-93).
-  P r, pw_r[4], pw_R[4], r64;
+  // Encrypt (or decrypt) the data block of ChaCha block u held in ks; returns
+  // the ciphertext words (masked past the end) in c[].
+  auto crypt_block = [&](uint64_t u, const uint32_t ks[16], uint32_t c[16]) {
+    const uint64_t d = u - 1;
+    const uint64_t rem = m.len - 64 * d;
+    uint32_t x[16], y[16];
+    if (rem >= 64 && aligned) {
+      const uint4 *sp = reinterpret_cast<const uint4 *>(src + 64 * d);
+      uint4 *dp = reinterpret_cast<uint4 *>(dst + 64 * d);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint4 v = sp[i];
+        x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
+      }
+#pragma unroll
+      for (int i = 0; i < 16; i++) y[i] = x[i] ^ ks[i];
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        dp[i] = make_uint4(y[4 * i], y[4 * i + 1], y[4 * i + 2], y[4 * i + 3]);
+    } else {
+      const uint8_t *sp = src + 64 * d;
+      uint8_t *dp = dst + 64 * d;
+      const uint32_t n = (uint32_t)min<uint64_t>(rem, 64);
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        x[i] = load_le32_bytes(sp + 4 * i, n > 4u * i ? n - 4u * i : 0);
+        const uint32_t mask = n >= 4u * i + 4 ? 0xffffffffu
+                              : n <= 4u * i   ? 0u
+                                              : ((1u << (8 * (n - 4 * i))) - 1u);
+        y[i] = (x[i] ^ ks[i]) & mask;
+      }
+      for (uint32_t i = 0; i < n; i++) dp[i] = (uint8_t)(y[i >> 2] >> (8 * (i & 3)));
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) c[i] = OPEN ? x[i] : y[i];
+  };
+
+  // Iteration 0: lane 0 computes the Poly1305 key block (counter 0,
+  // e_chacha20poly1305.cc:89-93), lanes 1..L-1 the data blocks 0..L-2.
+  const int iters = wave_max((int)((nblk + 1 + L - 1) / L));
+  uint32_t ks[16], c0[16];
+  chacha_block(key, (uint32_t)q, nonce, ks);
+  const bool have0 = q >= 1 && (uint64_t)q <= nblk;
+  if (have0) crypt_block((uint64_t)q, ks, c0);
+  uint32_t kw[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) kw[i] = __shfl(ks[i], 0, L);
+  P pw[kLog + 4];  // pw[k] = r^(2^k), k = 0 .. kLog + 2  (r^(4L))
   uint32_t s[4];
   {
-    uint32_t ks[16];
-    chacha_block(key, 0, nonce, ks);
-    const uint32_t t0 = ks[0] & 0x0fffffff, t1 = ks[1] & 0x0ffffffc, t2 = ks[2] & 0x0ffffffc,
-                   t3 = ks[3] & 0x0ffffffc;  // clamp (RFC 8439 2.5)
-    r.h[0] = t0 & kM26;
-    r.h[1] = ((t0 >> 26) | (t1 << 6)) & kM26;
-    r.h[2] = ((t1 >> 20) | (t2 << 12)) & kM26;
-    r.h[3] = ((t2 >> 14) | (t3 << 18)) & kM26;
-    r.h[4] = t3 >> 8;
-    s[0] = ks[4];
-    s[1] = ks[5];
-    s[2] = ks[6];
-    s[3] = ks[7];
-    pw_r[0] = r;
-    pw_r[1] = pmul(r, r);                // r^2
-    pw_r[2] = pmul(pw_r[1], pw_r[1]);    // r^4
-    pw_r[3] = pmul(pw_r[2], pw_r[2]);    // r^8
-    pw_R[0] = pw_r[2];                   // R = r^4
-    pw_R[1] = pw_r[3];                   // R^2 = r^8
-    pw_R[2] = pmul(pw_R[1], pw_R[1]);    // R^4 = r^16
-    pw_R[3] = pmul(pw_R[2], pw_R[2]);    // R^8 = r^32
-    r64 = pmul(pw_R[3], pw_R[3]);        // R^16 = r^64
+    const uint32_t t0 = kw[0] & 0x0fffffff, t1 = kw[1] & 0x0ffffffc, t2 = kw[2] & 0x0ffffffc,
+                   t3 = kw[3] & 0x0ffffffc;  // clamp (RFC 8439 2.5)
+    pw[0].h[0] = t0 & kM26;
+    pw[0].h[1] = ((t0 >> 26) | (t1 << 6)) & kM26;
+    pw[0].h[2] = ((t1 >> 20) | (t2 << 12)) & kM26;
+    pw[0].h[3] = ((t2 >> 14) | (t3 << 18)) & kM26;
+    pw[0].h[4] = t3 >> 8;
+    s[0] = kw[4];
+    s[1] = kw[5];
+    s[2] = kw[6];
+    s[3] = kw[7];
+#pragma unroll
+    for (int k = 1; k <= kLog + 2; k++) pw[k] = pmul(pw[k - 1], pw[k - 1]);
   }
+  const P &r = pw[0];
+  const P r2 = pw[1];
+  const P r3 = pmul(r2, r);
+  const P &rstride = pw[kLog + 2];  // R^L = r^(4L)
 
-  // AD: exclusive Horner in r over the zero-padded 16-byte blocks.
+  // AD: exclusive Horner in r over the zero-padded 16-byte blocks, stride L.
   P ya = pzero();
   {
     const uint8_t *ad = b.ad + (live ? m.ad_off : 0);
@@ -292,78 +384,63 @@ __global__ __launch_bounds__(kThreads) void chacha_poly_kernel(
       if (nab == 1) ya = ad_block(0);
     } else {
       P acc = pzero();
-      for (uint64_t k = q; k < nab; k += 16) acc = padd(pmul(acc, pw_R[2]), ad_block(k));
-      const int rr = (int)(nab & 15);
-      ya = group_combine(acc, q, (q + rr) & 15, pw_r);
+      for (uint64_t k = q; k < nab; k += L) acc = padd(pmul(acc, pw[kLog]), ad_block(k));
+      P a = pshfl(acc, (q + (int)(nab % L)) & (L - 1), L);
+#pragma unroll
+      for (int t = 0; t < kLog; t++) {
+        const int sh = 1 << t;
+        const P mm = pmul(a, pw[t]);
+        const P o = pshfl_down(a, sh, L);
+        if ((q & (2 * sh - 1)) == 0) a = padd(mm, o);
+      }
+      ya = pshfl(a, 0, L);
     }
   }
 
-  // Bulk: ChaCha20 blocks 1.. and Poly1305 units.
-  const uint64_t nblk = live ? (m.len + 63) / 64 : 0;  // ChaCha data blocks
-  const uint64_t npoly = live ? (m.len + 15) / 16 : 0;
-  const uint64_t nunits = npoly / 4;                   // full 4-block units
-  const uint32_t tail_blocks = (uint32_t)(npoly & 3);
-  const uint8_t *src = b.in + m.off;
-  uint8_t *dst = b.out + m.off;
-  const bool aligned = ((reinterpret_cast<uintptr_t>(src) |
-                         reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
-  P acc = (q == 15 && live) ? ya : pzero();
+  // Absorb data block d = u-1: a full unit folds into acc (acc*R^L + U with
+  // lazy reduction), the trailing partial unit is kept in `tail`.
+  P acc = (q == 0 && live) ? ya : pzero();
   P tail = pzero();
-  const int iters = wave_max((int)((nblk + 15) / 16));
-  for (int it = 0; it < iters; it++) {
-    const uint64_t u = (uint64_t)it * 16 + q;
-    uint32_t ks[16];
-    chacha_block(key, (uint32_t)(1 + u), nonce, ks);
-    if (u < nblk) {
-      const uint64_t rem = m.len - 64 * u;
-      uint32_t x[16], y[16];
-      if (rem >= 64 && aligned) {
-        const uint4 *sp = reinterpret_cast<const uint4 *>(src + 64 * u);
-        uint4 *dp = reinterpret_cast<uint4 *>(dst + 64 * u);
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          uint4 v = sp[i];
-          x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
-        }
-#pragma unroll
-        for (int i = 0; i < 16; i++) y[i] = x[i] ^ ks[i];
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-          dp[i] = make_uint4(y[4 * i], y[4 * i + 1], y[4 * i + 2], y[4 * i + 3]);
-      } else {
-        const uint8_t *sp = src + 64 * u;
-        uint8_t *dp = dst + 64 * u;
-        const uint32_t n = (uint32_t)min<uint64_t>(rem, 64);
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-          x[i] = load_le32_bytes(sp + 4 * i, n > 4u * i ? n - 4u * i : 0);
-          uint32_t mask = n >= 4u * i + 4 ? 0xffffffffu
-                          : n <= 4u * i   ? 0u
-                                          : ((1u << (8 * (n - 4 * i))) - 1u);
-          y[i] = (x[i] ^ ks[i]) & mask;
-        }
-        for (uint32_t i = 0; i < n; i++) dp[i] = (uint8_t)(y[i >> 2] >> (8 * (i & 3)));
-      }
-      const uint32_t *c = OPEN ? x : y;
-      if (u < nunits) {
-        P unit = pblock(c[0], c[1], c[2], c[3]);
-        unit = padd(pmul(unit, r), pblock(c[4], c[5], c[6], c[7]));
-        unit = padd(pmul(unit, r), pblock(c[8], c[9], c[10], c[11]));
-        unit = padd(pmul(unit, r), pblock(c[12], c[13], c[14], c[15]));
-        acc = padd(pmul(acc, r64), unit);
-      } else {
-        // Trailing partial unit: tail_blocks (1..3) Poly blocks.
-        P tt = pblock(c[0], c[1], c[2], c[3]);
-        for (uint32_t k = 1; k < tail_blocks; k++)
-          tt = padd(pmul(tt, r), pblock(c[4 * k], c[4 * k + 1], c[4 * k + 2], c[4 * k + 3]));
-        tail = tt;
-      }
+  auto absorb = [&](uint64_t u, const uint32_t c[16]) {
+    const uint64_t d = u - 1;
+    if (d < nunits) {
+      PAcc t = pacc_zero();
+      pmac(t, acc, rstride);
+      pmac(t, pblock(c[0], c[1], c[2], c[3]), r3);
+      pmac(t, pblock(c[4], c[5], c[6], c[7]), r2);
+      pmac(t, pblock(c[8], c[9], c[10], c[11]), r);
+      acc = padd(preduce(t), pblock(c[12], c[13], c[14], c[15]));
+    } else {
+      P tt = pblock(c[0], c[1], c[2], c[3]);
+      for (uint32_t k = 1; k < tail_blocks; k++)
+        tt = padd(pmul(tt, r), pblock(c[4 * k], c[4 * k + 1], c[4 * k + 2], c[4 * k + 3]));
+      tail = tt;
+    }
+  };
+  if (have0) absorb((uint64_t)q, c0);
+  for (int it = 1; it < iters; it++) {
+    const uint64_t u = (uint64_t)it * L + q;
+    chacha_block(key, (uint32_t)u, nonce, ks);
+    if (u <= nblk) {
+      uint32_t c[16];
+      crypt_block(u, ks, c);
+      absorb(u, c);
     }
   }
-  const int rw = (int)((nunits + 1) & 15);
-  P z = group_combine(acc, q, (q + rw + 15) & 15, pw_R);
-  // Z = X * r^t + tail, the tail from the lane that owns unit `nunits`.
-  tail = pshfl(tail, (int)(nunits & 15), 16);
+
+  // Combine the lanes: M = nunits + 1 virtual elements; lane p takes the
+  // accumulator of lane (p + M mod L) and the tree weights position p by
+  // R^(L-1-p).
+  P z = pshfl(acc, (q + (int)((nunits + 1) % L)) & (L - 1), L);
+#pragma unroll
+  for (int t = 0; t < kLog; t++) {
+    const int sh = 1 << t;
+    const P mm = pmul(z, pw[t + 2]);
+    const P o = pshfl_down(z, sh, L);
+    if ((q & (2 * sh - 1)) == 0) z = padd(mm, o);
+  }
+  // Z = X * r^t + tail (tail held by the lane of unit `nunits`).
+  tail = pshfl(tail, (int)((nunits + 1) % L), L);
   const int tmax = wave_max((int)tail_blocks);
   for (int k = 0; k < tmax; k++)
     if ((uint32_t)k < tail_blocks) z = pmul(z, r);
@@ -376,21 +453,24 @@ __global__ __launch_bounds__(kThreads) void chacha_poly_kernel(
   poly_finish(h, s, tag);
 
   uint8_t *tagp = b.tags + rec * b.tag_len;
-  bool ok = live;
-  if (OPEN && live) {
-    uint32_t diff = 0;
-    for (uint32_t i = 0; i < b.tag_len; i++)
-      diff |= ((tag[i >> 2] >> (8 * (i & 3))) & 0xff) ^ tagp[i];
-    ok = diff == 0;  // CRYPTO_memcmp, e_chacha20poly1305.cc:322-326
-  }
-  if (active && q == 0) {
-    if (!OPEN)
+  int ok = live;
+  if (q == 0) {
+    if (OPEN && live) {
+      uint32_t diff = 0;
       for (uint32_t i = 0; i < b.tag_len; i++)
-        tagp[i] = ok ? (uint8_t)(tag[i >> 2] >> (8 * (i & 3))) : 0;
-    if (b.status) b.status[rec] = ok ? 1 : 0;
+        diff |= ((tag[i >> 2] >> (8 * (i & 3))) & 0xff) ^ tagp[i];
+      ok = diff == 0;  // CRYPTO_memcmp, e_chacha20poly1305.cc:322-326
+    }
+    if (active) {
+      if (!OPEN)
+        for (uint32_t i = 0; i < b.tag_len; i++)
+          tagp[i] = ok ? (uint8_t)(tag[i >> 2] >> (8 * (i & 3))) : 0;
+      if (b.status) b.status[rec] = ok ? 1 : 0;
+    }
   }
+  ok = __shfl(ok, 0, L);
   if (active && !ok) {
-    for (uint64_t j = q; j * 16 < m.len; j += 16) {
+    for (uint64_t j = q; j * 16 < m.len; j += L) {
       const uint64_t n = min<uint64_t>(m.len - j * 16, 16);
       for (uint64_t i = 0; i < n; i++) dst[j * 16 + i] = 0;
     }
@@ -403,15 +483,16 @@ int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, void 
                   const KernelEvents *ev) {
   if (b.num_records == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const uint64_t blocks = (b.num_records + kRecPerBlock - 1) / kRecPerBlock;
+  constexpr int L = 8;  // lanes per record (see chacha_poly_kernel)
+  const uint64_t blocks = (b.num_records * L + kThreads - 1) / kThreads;
   if (blocks > 0x7fffffffu) return 1;
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
   if (open)
-    hipLaunchKernelGGL(chacha_poly_kernel<true>, dim3((unsigned)blocks), dim3(kThreads), 0, s,
+    hipLaunchKernelGGL((chacha_poly_kernel<true, L>), dim3((unsigned)blocks), dim3(kThreads), 0, s,
                        keys, b);
   else
-    hipLaunchKernelGGL(chacha_poly_kernel<false>, dim3((unsigned)blocks), dim3(kThreads), 0, s,
-                       keys, b);
+    hipLaunchKernelGGL((chacha_poly_kernel<false, L>), dim3((unsigned)blocks), dim3(kThreads), 0,
+                       s, keys, b);
   const int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
   return rc;

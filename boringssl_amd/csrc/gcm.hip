@@ -47,6 +47,9 @@ namespace {
 #ifndef BSSL_AMD_GCM_STREAMS
 #define BSSL_AMD_GCM_STREAMS 1
 #endif
+#ifndef BSSL_AMD_GCM_FUSED  // interleave the GHASH multiply with the AES rounds
+#define BSSL_AMD_GCM_FUSED 0
+#endif
 constexpr int kWaves = BSSL_AMD_GCM_WAVES;
 constexpr int kStreams = BSSL_AMD_GCM_STREAMS;
 constexpr int kThreads = kWaves * 64;
@@ -294,6 +297,32 @@ __device__ __forceinline__ uint4 gmul(uint4 x, const uint8_t *tab, uint32_t mf0)
   return r;
 }
 
+// AES rounds R0..NR of one counter block with the four word-phases of a
+// GHASH multiplication (g = x * H^(2^p), tables at TG) interleaved between the
+// rounds, so each dependent LDS phase of the wave carries both the AES
+// lookups and a GHASH word's lookups.
+template <int NR, uint32_t TA, int R0, uint32_t TG>
+__device__ __forceinline__ uint4 aes_rounds_ghash(uint32_t s0, uint32_t s1, uint32_t s2,
+                                                  uint32_t s3, const RoundKeys &rk,
+                                                  const uint8_t *smem, uint32_t lc0, uint32_t lc1,
+                                                  uint4 x, uint4 &g, uint32_t mf0) {
+  constexpr int kSpan = (NR - R0) / 4;  // rounds between GHASH word phases
+  uint4 r = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int rr = R0; rr < NR; rr++) {
+    aes_round<TA>(s0, s1, s2, s3, rk.w[rr], smem, lc0, lc1);
+    const int w = (rr - R0) / kSpan;
+    if ((rr - R0) % kSpan == 0 && w < 4) {
+      if (w == 0) r = gmul_word<TG, 0>(r, x.x, smem, mf0);
+      if (w == 1) r = gmul_word<TG, 1>(r, x.y, smem, mf0);
+      if (w == 2) r = gmul_word<TG, 2>(r, x.z, smem, mf0);
+      if (w == 3) r = gmul_word<TG, 3>(r, x.w, smem, mf0);
+    }
+  }
+  g = r;
+  return aes_rounds<NR, TA, NR>(s0, s1, s2, s3, rk, smem, lc0, lc1);
+}
+
 // Runtime power index (prologue, tree).
 __device__ __forceinline__ uint4 gmul_pow(uint4 x, const uint8_t *tab, int p, uint32_t mf0) {
   return gmul<0>(x, tab + p * 8192, mf0);
@@ -532,7 +561,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     wa.update<T>(ctra, sa, c0, c1, c2, rk, smem, lc0, lc1);
     uint32_t a0, a1, a2, a3;
     wa.rounds12<T>(k0, sa, a0, a1, a2, a3, smem, lc0, lc1);
-    uint4 ksa, ksb = make_uint4(0, 0, 0, 0);
+    uint4 ksa, ksb = make_uint4(0, 0, 0, 0), gacc = make_uint4(0, 0, 0, 0);
     if constexpr (S == 2) {
       const uint32_t ctrb = ctr0 + 1u + (uint32_t)jb;
       const uint32_t sb = bswap32(ctrb) ^ rk.w[0][3];
@@ -548,6 +577,9 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     } else {
 #if BSSL_AMD_ABLATE == 2
       ksa = make_uint4(a0, a1, a2, a3);
+#elif BSSL_AMD_ABLATE == 0 && BSSL_AMD_GCM_FUSED
+      ksa = aes_rounds_ghash<NR, T, 3, kLdsGhash + 4 * 8192>(a0, a1, a2, a3, rk, smem, lc0, lc1,
+                                                             acc, gacc, mf0);
 #else
       ksa = aes_rounds<NR, T, 3>(a0, a1, a2, a3, rk, smem, lc0, lc1);
 #endif
@@ -572,7 +604,10 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
 #if BSSL_AMD_ABLATE == 1  // diagnostic build: no GHASH multiply (wrong tags)
         acc = xor4(acc, OPEN ? x : y);
 #else
-        acc = xor4(gmul<kLdsGhash + 4 * 8192>(acc, smem, mf0), OPEN ? x : y);
+        if (S == 1 && BSSL_AMD_GCM_FUSED)
+          acc = xor4(gacc, OPEN ? x : y);  // gacc = acc * H^16, computed inside the rounds
+        else
+          acc = xor4(gmul<kLdsGhash + 4 * 8192>(acc, smem, mf0), OPEN ? x : y);
 #endif
       }
     }
