@@ -300,16 +300,25 @@ __global__ __launch_bounds__(kThreads) void chacha_poly_kernel(
 
   // Encrypt (or decrypt) the data block of ChaCha block u held in ks; returns
   // the ciphertext words (masked past the end) in c[].
-  auto crypt_block = [&](uint64_t u, const uint32_t ks[16], uint32_t c[16]) {
+  // Input of data block d = u-1 when it is a full aligned 64-byte block
+  // (issued before the ChaCha rounds so the HBM latency hides under them).
+  auto prefetch = [&](uint64_t u, uint4 pre[4]) {
+    const uint64_t d = u - 1;
+    if (u >= 1 && u <= nblk && aligned && m.len - 64 * d >= 64) {
+      const uint4 *sp = reinterpret_cast<const uint4 *>(src + 64 * d);
+#pragma unroll
+      for (int i = 0; i < 4; i++) pre[i] = sp[i];
+    }
+  };
+  auto crypt_block = [&](uint64_t u, const uint32_t ks[16], const uint4 pre[4], uint32_t c[16]) {
     const uint64_t d = u - 1;
     const uint64_t rem = m.len - 64 * d;
     uint32_t x[16], y[16];
     if (rem >= 64 && aligned) {
-      const uint4 *sp = reinterpret_cast<const uint4 *>(src + 64 * d);
       uint4 *dp = reinterpret_cast<uint4 *>(dst + 64 * d);
 #pragma unroll
       for (int i = 0; i < 4; i++) {
-        const uint4 v = sp[i];
+        const uint4 v = pre[i];
         x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
       }
 #pragma unroll
@@ -339,9 +348,11 @@ __global__ __launch_bounds__(kThreads) void chacha_poly_kernel(
   // e_chacha20poly1305.cc:89-93), lanes 1..L-1 the data blocks 0..L-2.
   const int iters = wave_max((int)((nblk + 1 + L - 1) / L));
   uint32_t ks[16], c0[16];
+  uint4 pre[4];
+  prefetch((uint64_t)q, pre);
   chacha_block(key, (uint32_t)q, nonce, ks);
   const bool have0 = q >= 1 && (uint64_t)q <= nblk;
-  if (have0) crypt_block((uint64_t)q, ks, c0);
+  if (have0) crypt_block((uint64_t)q, ks, pre, c0);
   uint32_t kw[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) kw[i] = __shfl(ks[i], 0, L);
@@ -420,10 +431,11 @@ __global__ __launch_bounds__(kThreads) void chacha_poly_kernel(
   if (have0) absorb((uint64_t)q, c0);
   for (int it = 1; it < iters; it++) {
     const uint64_t u = (uint64_t)it * L + q;
+    prefetch(u, pre);
     chacha_block(key, (uint32_t)u, nonce, ks);
     if (u <= nblk) {
       uint32_t c[16];
-      crypt_block(u, ks, c);
+      crypt_block(u, ks, pre, c);
       absorb(u, c);
     }
   }

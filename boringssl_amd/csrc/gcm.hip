@@ -39,19 +39,15 @@
 namespace bssl_amd {
 namespace {
 
-// Waves per workgroup (one workgroup per CU: the LDS tables take 104 KiB) and
-// AES streams per lane; build-time knobs for tuning (-DBSSL_AMD_GCM_WAVES=..).
+// Waves per workgroup (one workgroup per CU: the LDS tables take 104 KiB); a
+// build-time knob for tuning (-DBSSL_AMD_GCM_WAVES=..).
+#ifndef BSSL_AMD_GHASH_GROUP
+#define BSSL_AMD_GHASH_GROUP 1
+#endif
 #ifndef BSSL_AMD_GCM_WAVES
 #define BSSL_AMD_GCM_WAVES 12
 #endif
-#ifndef BSSL_AMD_GCM_STREAMS
-#define BSSL_AMD_GCM_STREAMS 1
-#endif
-#ifndef BSSL_AMD_GCM_FUSED  // interleave the GHASH multiply with the AES rounds
-#define BSSL_AMD_GCM_FUSED 0
-#endif
 constexpr int kWaves = BSSL_AMD_GCM_WAVES;
-constexpr int kStreams = BSSL_AMD_GCM_STREAMS;
 constexpr int kThreads = kWaves * 64;
 constexpr int kRecPerWave = 4;
 constexpr int kRecPerTile = kWaves * kRecPerWave;  // <= 64 (one planning wave)
@@ -278,6 +274,60 @@ __device__ __forceinline__ uint4 gmul_word(uint4 r, uint32_t v, const uint8_t *t
              tab128<TB + (8 * W + 5) * 256>(tab, nib<2>(l, mf0)));
   r = xor4_3(r, tab128<TB + (8 * W + 6) * 256>(tab, nib<3>(v, mf0)),
              tab128<TB + (8 * W + 7) * 256>(tab, nib<3>(l, mf0)));
+#if BSSL_AMD_GHASH_GROUP
+  // Keep the word's 8 lookups in flight together (hipcc otherwise issues
+  // them two at a time under register pressure).
+  __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+  __builtin_amdgcn_sched_group_barrier(0x2, 16, 0);
+#endif
+  return r;
+}
+
+// Hot-loop form: the word's 8 lookups are issued back to back by one asm
+// block (hipcc's scheduler otherwise issues them two at a time, one LDS round
+// trip per pair).  `base` is the LDS byte address of the power's tables.
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+template <uint32_t OFF>
+__device__ __forceinline__ void lds_read8(const uint32_t a[8], v4u d[8]) {
+  static_assert(OFF + 7 * 256 < 65536, "ds_read offset field");
+  asm volatile(
+      "ds_read_b128 %0, %8 offset:%16\n\t"
+      "ds_read_b128 %1, %9 offset:%17\n\t"
+      "ds_read_b128 %2, %10 offset:%18\n\t"
+      "ds_read_b128 %3, %11 offset:%19\n\t"
+      "ds_read_b128 %4, %12 offset:%20\n\t"
+      "ds_read_b128 %5, %13 offset:%21\n\t"
+      "ds_read_b128 %6, %14 offset:%22\n\t"
+      "ds_read_b128 %7, %15 offset:%23\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]), "=&v"(d[5]),
+        "=&v"(d[6]), "=&v"(d[7])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]),
+        "i"(OFF), "i"(OFF + 256), "i"(OFF + 512), "i"(OFF + 768), "i"(OFF + 1024),
+        "i"(OFF + 1280), "i"(OFF + 1536), "i"(OFF + 1792));
+}
+
+template <uint32_t TB, int W>
+__device__ __forceinline__ uint4 gmul_word_batched(uint4 r, uint32_t v, uint32_t base,
+                                                   uint32_t mf0) {
+  const uint32_t l = v << 4;
+  const uint32_t a[8] = {base + nib<0>(v, mf0), base + nib<0>(l, mf0), base + nib<1>(v, mf0),
+                         base + nib<1>(l, mf0), base + nib<2>(v, mf0), base + nib<2>(l, mf0),
+                         base + nib<3>(v, mf0), base + nib<3>(l, mf0)};
+  v4u d[8];
+  lds_read8<TB + 8 * W * 256>(a, d);
+  const v4u t = (d[0] ^ d[1] ^ d[2]) ^ (d[3] ^ d[4] ^ d[5]) ^ (d[6] ^ d[7]);
+  return make_uint4(r.x ^ t.x, r.y ^ t.y, r.z ^ t.z, r.w ^ t.w);
+}
+
+template <uint32_t TB>
+__device__ __forceinline__ uint4 gmul_batched(uint4 x, uint32_t base, uint32_t mf0) {
+  uint4 r = make_uint4(0, 0, 0, 0);
+  r = gmul_word_batched<TB, 0>(r, x.x, base, mf0);
+  r = gmul_word_batched<TB, 1>(r, x.y, base, mf0);
+  r = gmul_word_batched<TB, 2>(r, x.z, base, mf0);
+  r = gmul_word_batched<TB, 3>(r, x.w, base, mf0);
   return r;
 }
 
@@ -295,32 +345,6 @@ __device__ __forceinline__ uint4 gmul(uint4 x, const uint8_t *tab, uint32_t mf0)
   r = gmul_word<TB, 3>(r, x.w, tab, mf0);
   __builtin_amdgcn_sched_barrier(0);
   return r;
-}
-
-// AES rounds R0..NR of one counter block with the four word-phases of a
-// GHASH multiplication (g = x * H^(2^p), tables at TG) interleaved between the
-// rounds, so each dependent LDS phase of the wave carries both the AES
-// lookups and a GHASH word's lookups.
-template <int NR, uint32_t TA, int R0, uint32_t TG>
-__device__ __forceinline__ uint4 aes_rounds_ghash(uint32_t s0, uint32_t s1, uint32_t s2,
-                                                  uint32_t s3, const RoundKeys &rk,
-                                                  const uint8_t *smem, uint32_t lc0, uint32_t lc1,
-                                                  uint4 x, uint4 &g, uint32_t mf0) {
-  constexpr int kSpan = (NR - R0) / 4;  // rounds between GHASH word phases
-  uint4 r = make_uint4(0, 0, 0, 0);
-#pragma unroll
-  for (int rr = R0; rr < NR; rr++) {
-    aes_round<TA>(s0, s1, s2, s3, rk.w[rr], smem, lc0, lc1);
-    const int w = (rr - R0) / kSpan;
-    if ((rr - R0) % kSpan == 0 && w < 4) {
-      if (w == 0) r = gmul_word<TG, 0>(r, x.x, smem, mf0);
-      if (w == 1) r = gmul_word<TG, 1>(r, x.y, smem, mf0);
-      if (w == 2) r = gmul_word<TG, 2>(r, x.z, smem, mf0);
-      if (w == 3) r = gmul_word<TG, 3>(r, x.w, smem, mf0);
-    }
-  }
-  g = r;
-  return aes_rounds<NR, TA, NR>(s0, s1, s2, s3, rk, smem, lc0, lc1);
 }
 
 // Runtime power index (prologue, tree).
@@ -423,21 +447,6 @@ struct WindowCache {
     u3 = tload<T>(smem, taddr<1>(lc1, t0)) ^ l3;
   }
 };
-
-// Two interleaved AES streams, rounds R0..NR.
-template <int NR, uint32_t TB, int R0>
-__device__ __forceinline__ void aes_rounds2(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
-                                            uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3,
-                                            const RoundKeys &rk, const uint8_t *smem,
-                                            uint32_t lc0, uint32_t lc1, uint4 &oa, uint4 &ob) {
-#pragma unroll
-  for (int r = R0; r < NR; r++) {
-    aes_round<TB>(a0, a1, a2, a3, rk.w[r], smem, lc0, lc1);
-    aes_round<TB>(b0, b1, b2, b3, rk.w[r], smem, lc0, lc1);
-  }
-  oa = aes_rounds<NR, TB, NR>(a0, a1, a2, a3, rk, smem, lc0, lc1);
-  ob = aes_rounds<NR, TB, NR>(b0, b1, b2, b3, rk, smem, lc0, lc1);
-}
 
 // Per-record state handed from the prologue to the bulk kernel (64 bytes).
 struct alignas(16) RecState {
@@ -544,74 +553,64 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   constexpr uint32_t T = kLdsAes;
   const uint32_t k0 = tload<T>(smem, taddr<0>(lc0, c0)) ^ tload<T>(smem, taddr<1>(lc1, c1)) ^
                       rotl(tload<T>(smem, taddr<2>(lc0, c2)) ^ rk.w[1][0], 16);
-  WindowCache wa, wb;
-  // kStreams independent counter blocks per lane per iteration (j, j+16)
-  // give each wave that many AES dependency chains to interleave.
-  constexpr int S = kStreams;
-  const int iters = wave_max((int)((nb + 16 * S - 1) / (16 * S)));
-  for (int it = 0; it < iters; it++) {
-    const uint64_t ja = (uint64_t)it * 16 * S + q, jb = ja + 16;
-    const bool fa = ja < nb && aligned && m.len - ja * 16 >= 16;
-    const bool fb = S == 2 && jb < nb && aligned && m.len - jb * 16 >= 16;
-    uint4 xa = make_uint4(0, 0, 0, 0), xb = make_uint4(0, 0, 0, 0);
-    if (fa) xa = *reinterpret_cast<const uint4 *>(src + ja * 16);
-    if (fb) xb = *reinterpret_cast<const uint4 *>(src + jb * 16);
-    const uint32_t ctra = ctr0 + 1u + (uint32_t)ja;  // inc32 wraps mod 2^32
-    const uint32_t sa = bswap32(ctra) ^ rk.w[0][3];
-    wa.update<T>(ctra, sa, c0, c1, c2, rk, smem, lc0, lc1);
+  WindowCache wc;
+  const uint32_t lds_base = (uint32_t)reinterpret_cast<uintptr_t>(smem);  // LDS offset
+  const int iters = wave_max((int)((nb + 15) / 16));
+  // Full aligned 16-byte blocks of this lane's record; the rest (the partial
+  // last block, or every block of an unaligned record) take the byte path.
+  const uint64_t nfull = aligned ? m.len / 16 : 0;
+  // (Left undefined when not loaded: such a block is never stored or hashed
+  // from this value, and a zero-fill would be a VALU write that the waitcnt
+  // pass orders after the previous store.)
+  auto load_full = [&](uint64_t j) {
+    uint4 v;
+    if (j < nfull) v = *reinterpret_cast<const uint4 *>(src + j * 16);
+    return v;
+  };
+  // One iteration: block j = it*16 + q, plaintext (if full) already in x.
+  auto step = [&](int it, uint4 x) {
+    const uint64_t j = (uint64_t)it * 16 + q;
+    const uint32_t ctr = ctr0 + 1u + (uint32_t)j;  // inc32 wraps mod 2^32
+    const uint32_t s3 = bswap32(ctr) ^ rk.w[0][3];
+    wc.update<T>(ctr, s3, c0, c1, c2, rk, smem, lc0, lc1);
     uint32_t a0, a1, a2, a3;
-    wa.rounds12<T>(k0, sa, a0, a1, a2, a3, smem, lc0, lc1);
-    uint4 ksa, ksb = make_uint4(0, 0, 0, 0), gacc = make_uint4(0, 0, 0, 0);
-    if constexpr (S == 2) {
-      const uint32_t ctrb = ctr0 + 1u + (uint32_t)jb;
-      const uint32_t sb = bswap32(ctrb) ^ rk.w[0][3];
-      wb.update<T>(ctrb, sb, c0, c1, c2, rk, smem, lc0, lc1);
-      uint32_t b0, b1, b2, b3;
-      wb.rounds12<T>(k0, sb, b0, b1, b2, b3, smem, lc0, lc1);
+    wc.rounds12<T>(k0, s3, a0, a1, a2, a3, smem, lc0, lc1);
 #if BSSL_AMD_ABLATE == 2  // diagnostic build: no AES rounds 3..NR (wrong output)
-      ksa = make_uint4(a0, a1, a2, a3);
-      ksb = make_uint4(b0, b1, b2, b3);
+    const uint4 ks = make_uint4(a0, a1, a2, a3);
 #else
-      aes_rounds2<NR, T, 3>(a0, a1, a2, a3, b0, b1, b2, b3, rk, smem, lc0, lc1, ksa, ksb);
+    const uint4 ks = aes_rounds<NR, T, 3>(a0, a1, a2, a3, rk, smem, lc0, lc1);
 #endif
-    } else {
-#if BSSL_AMD_ABLATE == 2
-      ksa = make_uint4(a0, a1, a2, a3);
-#elif BSSL_AMD_ABLATE == 0 && BSSL_AMD_GCM_FUSED
-      ksa = aes_rounds_ghash<NR, T, 3, kLdsGhash + 4 * 8192>(a0, a1, a2, a3, rk, smem, lc0, lc1,
-                                                             acc, gacc, mf0);
-#else
-      ksa = aes_rounds<NR, T, 3>(a0, a1, a2, a3, rk, smem, lc0, lc1);
-#endif
+    uint4 y = xor4(x, ks);
+    if (j < nfull) {
+      *reinterpret_cast<uint4 *>(dst + j * 16) = y;
+    } else if (j < nb) {
+      const uint32_t n = (uint32_t)min<uint64_t>(m.len - j * 16, 16);
+      x = load_partial(src + j * 16, n);
+      y = mask_block(xor4(x, ks), n);
+      store_partial(dst + j * 16, y, n);
     }
-#pragma unroll
-    for (int h = 0; h < S; h++) {
-      const uint64_t j = h ? jb : ja;
-      if (j < nb) {
-        const uint4 ks = h ? ksb : ksa;
-        const bool full = h ? fb : fa;
-        uint4 x, y;
-        if (full) {
-          x = h ? xb : xa;
-          y = xor4(x, ks);
-          *reinterpret_cast<uint4 *>(dst + j * 16) = y;
-        } else {
-          const uint32_t n = (uint32_t)min<uint64_t>(m.len - j * 16, 16);
-          x = load_partial(src + j * 16, n);
-          y = mask_block(xor4(x, ks), n);
-          store_partial(dst + j * 16, y, n);
-        }
+    if (j < nb) {
 #if BSSL_AMD_ABLATE == 1  // diagnostic build: no GHASH multiply (wrong tags)
-        acc = xor4(acc, OPEN ? x : y);
+      acc = xor4(acc, OPEN ? x : y);
 #else
-        if (S == 1 && BSSL_AMD_GCM_FUSED)
-          acc = xor4(gacc, OPEN ? x : y);  // gacc = acc * H^16, computed inside the rounds
-        else
-          acc = xor4(gmul<kLdsGhash + 4 * 8192>(acc, smem, mf0), OPEN ? x : y);
+      acc = xor4(gmul_batched<kLdsGhash + 4 * 8192>(acc, lds_base, mf0), OPEN ? x : y);
 #endif
-      }
     }
+  };
+  // Plaintext is loaded one iteration ahead into two alternating buffers (the
+  // loop is unrolled twice so no register copy forces an early wait): the load
+  // for iteration it+1 is issued before iteration it's store, so waiting for
+  // it never waits for a store (vmcnt counts loads and stores in issue order)
+  // and its latency hides under a whole iteration of AES + GHASH.
+  uint4 x0 = load_full(q);
+  int it = 0;
+  for (; it + 1 < iters; it += 2) {
+    const uint4 x1 = load_full((uint64_t)(it + 1) * 16 + q);
+    step(it, x0);
+    x0 = load_full((uint64_t)(it + 2) * 16 + q);
+    step(it + 1, x1);
   }
+  if (it < iters) step(it, x0);
   // Lane algebra: lane q holds the virtual elements v = q+1+16i of
   // [Y_A, C_0, ..., C_{nb-1}]; rotate so position p holds the lane whose
   // weight is H^(15-p), then tree-combine with H, H^2, H^4, H^8.
