@@ -29,8 +29,10 @@
 //   key at a time; records are visited in tiles of 32 and a tile whose
 //   records use several keys is processed in one pass per distinct key.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "internal.h"
+#include "bs_aes.h"
 
 #ifndef BSSL_AMD_ABLATE
 #define BSSL_AMD_ABLATE 0
@@ -41,6 +43,17 @@ namespace {
 
 // Waves per workgroup (one workgroup per CU: the LDS tables take 104 KiB); a
 // build-time knob for tuning (-DBSSL_AMD_GCM_WAVES=..).
+// Diagnostic build: per-phase s_memtime stamps of one wave of the bitsliced
+// kernel, printed with printf (never in the shipped library).
+#ifndef BSSL_AMD_BS_STAMPS
+#define BSSL_AMD_BS_STAMPS 0
+#endif
+#if BSSL_AMD_BS_STAMPS
+#define BS_STAMP(i) ts[i] = __builtin_amdgcn_s_memtime()
+#else
+#define BS_STAMP(i)
+#endif
+
 #ifndef BSSL_AMD_GHASH_GROUP
 #define BSSL_AMD_GHASH_GROUP 1
 #endif
@@ -100,7 +113,8 @@ __constant__ Tables kTables = make_tables();
 //                    k*256, value v at v*16
 //   [40960, 106496)  AES T0/T1, replicated per bank (see header comment)
 constexpr uint32_t kLdsGhash = 0;
-constexpr uint32_t kGhashLdsBytes = kGhashPowers * 8192;
+constexpr int kTGhashPowers = 5;  // the T-table kernel uses H .. H^16
+constexpr uint32_t kGhashLdsBytes = kTGhashPowers * 8192;
 constexpr uint32_t kLdsAes = kGhashLdsBytes;
 constexpr uint32_t kAesLdsBytes = 256 * 256;
 constexpr uint32_t kLdsBytes = kLdsAes + kAesLdsBytes;
@@ -519,6 +533,73 @@ __global__ __launch_bounds__(256) void gcm_prologue(const GcmKeyDev *__restrict_
   st[rec] = s;
 }
 
+// End of a record (both bulk kernels): combine the L lanes' GHASH
+// accumulators, form the tag, check it (open), write tag/status, and zero the
+// output of a failed record.  Lane algebra: lane q holds the
+// virtual elements v = q+1+L*i of [Y_A, C_0, ..., C_{nb-1}]; rotate so position
+// p holds the lane whose weight is H^(L-1-p), then tree-combine with
+// H, H^2, ..., H^(L/2) (tables 0..log2(L)-1 at kLdsGhash).
+template <bool OPEN, int L>
+__device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const RecordMeta &m,
+                                              const RecState &s, const BatchDesc &b, uint64_t rec,
+                                              bool active, bool live, uint8_t *dst,
+                                              const uint8_t *smem, uint32_t mf0) {
+  constexpr int kLevels = L == 32 ? 5 : L == 16 ? 4 : L == 8 ? 3 : L == 4 ? 2 : -1;
+  static_assert(kLevels > 0, "lanes per record");
+  const int q = threadIdx.x & (L - 1);
+  const int r = (int)((nb + 1) & (L - 1));
+  uint4 a = shfl4(acc, (q + r + L - 1) & (L - 1), L);
+  // Kept as a rolled loop so hipcc does not interleave the dependent
+  // multiplications (which costs ~120 VGPRs when unrolled).
+#pragma unroll 1
+  for (int t = 0; t < kLevels; t++) {
+    const int sh = 1 << t;
+    const uint4 o = shfl_down4(a, sh, L);
+    const uint4 mlt = gmul<0>(a, smem + kLdsGhash + t * 8192, mf0);
+    if ((q & (2 * sh - 1)) == 0) a = xor4(mlt, o);
+  }
+  // Tag (gcm.cc.inc:576-604): ((Z*H) ^ len block) * H ^ E_K(J0), in lane 0.
+  const uint64_t abits = m.ad_len << 3, cbits = m.len << 3;
+  uint4 add = make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
+                         bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits));
+#pragma unroll 1
+  for (int t = 0; t < 2; t++) {
+    a = xor4(gmul<0>(a, smem + kLdsGhash, mf0), add);
+    add = s.ek0;
+  }
+  const uint4 tag = a;
+
+  uint8_t *tagp = b.tags + rec * b.tag_len;
+  int ok = live;
+  if (q == 0) {
+    if (OPEN && live) {
+      const uint32_t tw[4] = {tag.x, tag.y, tag.z, tag.w};
+      uint32_t diff = 0;
+      for (uint32_t i = 0; i < b.tag_len; i++)
+        diff |= ((tw[i >> 2] >> (8 * (i & 3))) & 0xff) ^ tagp[i];
+      ok = diff == 0;  // CRYPTO_memcmp, e_aes.cc.inc:860-864
+    }
+    if (active) {
+      if (!OPEN) {
+        if (ok)
+          store_partial(tagp, tag, b.tag_len);
+        else
+          for (uint32_t i = 0; i < b.tag_len; i++) tagp[i] = 0;
+      }
+      if (b.status) b.status[rec] = ok ? 1 : 0;
+    }
+  }
+  ok = __shfl(ok, 0, L);
+  // Zero the output of a failed record (aead.cc.inc:132-139, 539-547).
+  if (active && !ok) {
+    for (uint64_t j = q; j * 16 < m.len; j += L) {
+      const uint32_t n = (uint32_t)min<uint64_t>(m.len - j * 16, 16);
+      store_partial(dst + j * 16, make_uint4(0, 0, 0, 0), n);
+    }
+  }
+}
+
+
 // ---------------------------------------------------------------------------
 // Bulk kernel: CTR keystream + GHASH + tag for the (up to) 4 records of a
 // wave, 16 lanes per record.  `active` is per group (record in this key pass).
@@ -611,59 +692,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     step(it + 1, x1);
   }
   if (it < iters) step(it, x0);
-  // Lane algebra: lane q holds the virtual elements v = q+1+16i of
-  // [Y_A, C_0, ..., C_{nb-1}]; rotate so position p holds the lane whose
-  // weight is H^(15-p), then tree-combine with H, H^2, H^4, H^8.
-  const int r = (int)((nb + 1) & 15);
-  uint4 a = shfl4(acc, (q + r + 15) & 15, 16);
-  // Kept as a rolled loop so hipcc does not interleave the six dependent
-  // multiplications (which costs ~120 VGPRs when unrolled).
-#pragma unroll 1
-  for (int t = 0; t < 4; t++) {
-    const int sh = 1 << t;
-    const uint4 o = shfl_down4(a, sh, 16);
-    const uint4 mlt = gmul<0>(a, smem + kLdsGhash + t * 8192, mf0);
-    if ((q & (2 * sh - 1)) == 0) a = xor4(mlt, o);
-  }
-  // Tag (gcm.cc.inc:576-604): ((Z*H) ^ len block) * H ^ E_K(J0), in lane 0.
-  const uint64_t abits = m.ad_len << 3, cbits = m.len << 3;
-  uint4 add = make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
-                         bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits));
-#pragma unroll 1
-  for (int t = 0; t < 2; t++) {
-    a = xor4(gmul<0>(a, smem + kLdsGhash, mf0), add);
-    add = s.ek0;
-  }
-  const uint4 tag = a;
-
-  uint8_t *tagp = b.tags + rec * b.tag_len;
-  int ok = live;
-  if (q == 0) {
-    if (OPEN && live) {
-      const uint32_t tw[4] = {tag.x, tag.y, tag.z, tag.w};
-      uint32_t diff = 0;
-      for (uint32_t i = 0; i < b.tag_len; i++)
-        diff |= ((tw[i >> 2] >> (8 * (i & 3))) & 0xff) ^ tagp[i];
-      ok = diff == 0;  // CRYPTO_memcmp, e_aes.cc.inc:860-864
-    }
-    if (active) {
-      if (!OPEN) {
-        if (ok)
-          store_partial(tagp, tag, b.tag_len);
-        else
-          for (uint32_t i = 0; i < b.tag_len; i++) tagp[i] = 0;
-      }
-      if (b.status) b.status[rec] = ok ? 1 : 0;
-    }
-  }
-  ok = __shfl(ok, 0, 16);
-  // Zero the output of a failed record (aead.cc.inc:132-139, 539-547).
-  if (active && !ok) {
-    for (uint64_t j = q; j * 16 < m.len; j += 16) {
-      const uint32_t n = (uint32_t)min<uint64_t>(m.len - j * 16, 16);
-      store_partial(dst + j * 16, make_uint4(0, 0, 0, 0), n);
-    }
-  }
+  finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, smem, mf0);
 }
 
 template <int NR, bool OPEN>
@@ -741,7 +770,276 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
   }
 }
 
+// ---------------------------------------------------------------------------
+// Bitsliced bulk kernel, for batches of long uniform-length records (DESIGN.md
+// §4.2b).  L lanes per record; lane q owns the record's blocks
+// j = 32*L*c + L*n + q of chunk c, n = 0..31, i.e. 32 blocks per chunk that
+// are encrypted together as bit-planes (bs_aes.h: block n in bit n).  The AES
+// is all VALU (v_bitop3 S-box circuit), leaving the LDS to GHASH alone; the
+// per-lane GHASH chain runs over the lane's blocks in order with multiplier
+// H^L and ends in the same rotation + tree as gcm_kernel (finish_record).
+constexpr int kBsWaves = 4;  // per workgroup; 2 workgroups per CU (VGPR-bound)
+constexpr int kBsThreads = kBsWaves * 64;
+constexpr uint32_t kBsLdsBytes = kGhashPowers * 8192;
+
+// acc <- Horner over the lane's 32 chunk blocks j = jc + L*n (< nb) of buf,
+// multiplier H^L (table log2(L)), loads kAhead blocks ahead.  FULL (every
+// block of the chunk exists, wave-uniform): addresses are one base plus
+// constant offsets.  Otherwise loads are unconditional (a block past the end
+// re-reads block 0 of the record, which exists for every record this kernel
+// runs on) and the update is a select -- straight-line code either way, so
+// the waitcnt pass counts the loads exactly.
+template <int L, bool FULL>
+__device__ __forceinline__ uint4 ghash_chunk(uint4 acc, const uint8_t *buf, uint32_t jc,
+                                             uint32_t nb, uint32_t lds_base, uint32_t mf0) {
+  constexpr int kLogL = L == 32 ? 5 : L == 16 ? 4 : 3;
+  constexpr int kAhead = 4;
+  const uint8_t *bp = buf + (uint64_t)jc * 16;
+  auto ld = [&](int n) {
+    const uint32_t j = jc + L * n;
+    if (FULL) return *reinterpret_cast<const uint4 *>(bp + 16 * L * n);
+    return *reinterpret_cast<const uint4 *>(buf + (uint64_t)(j < nb ? j : 0u) * 16);
+  };
+  uint4 cb[32];
+#pragma unroll
+  for (int n = 0; n < kAhead; n++) cb[n] = ld(n);
+#pragma unroll
+  for (int n = 0; n < 32; n++) {
+    if (n + kAhead < 32) cb[n + kAhead] = ld(n + kAhead);
+    const uint4 nx = xor4(gmul_batched<kLdsGhash + kLogL * 8192>(acc, lds_base, mf0), cb[n]);
+    if (FULL || jc + L * n < nb) acc = nx;
+  }
+  return acc;
+}
+
+// dst word `col` of the lane's 32 chunk blocks = src word ^ t[n] (keystream
+// word col of block n).  All loads are issued before the stores.
+template <int L, bool FULL>
+__device__ __forceinline__ void apply_keystream_word(const uint32_t t[32], const uint8_t *src,
+                                                     uint8_t *dst, uint32_t jc, uint32_t nb,
+                                                     int col) {
+  const uint8_t *sp = src + 4 * col;
+  uint8_t *dp = dst + 4 * col;
+  uint32_t x[32];
+  if (FULL) {
+    const uint8_t *sb = sp + (uint64_t)jc * 16;
+    uint8_t *db = dp + (uint64_t)jc * 16;
+#pragma unroll
+    for (int n = 0; n < 32; n++) x[n] = *reinterpret_cast<const uint32_t *>(sb + 16 * L * n);
+#pragma unroll
+    for (int n = 0; n < 32; n++) *reinterpret_cast<uint32_t *>(db + 16 * L * n) = x[n] ^ t[n];
+  } else {
+#pragma unroll
+    for (int n = 0; n < 32; n++) {
+      const uint32_t j = jc + L * n;
+      x[n] = *reinterpret_cast<const uint32_t *>(sp + (uint64_t)(j < nb ? j : 0u) * 16);
+    }
+#pragma unroll
+    for (int n = 0; n < 32; n++) {
+      const uint32_t j = jc + L * n;
+      if (j < nb) *reinterpret_cast<uint32_t *>(dp + (uint64_t)j * 16) = x[n] ^ t[n];
+    }
+  }
+}
+
+template <int NR, bool OPEN, int L>
+__device__ __forceinline__ void process_records_bs(const GcmKeyDev *__restrict__ kp,
+                                                   const BatchDesc &b,
+                                                   const RecState *__restrict__ st, uint64_t rec,
+                                                   bool active, const uint8_t *smem,
+                                                   uint32_t mf0, bool report) {
+#if BSSL_AMD_BS_STAMPS
+  uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  BS_STAMP(0);
+  constexpr int kLogL = L == 32 ? 5 : L == 16 ? 4 : 3;
+  static_assert(L == 8 || L == 16 || L == 32, "lanes per record");
+  const int q = threadIdx.x & (L - 1);
+  RecordMeta m = {0, 0, 0, 0};
+  RecState s;
+  s.j0 = s.ek0 = s.ya = make_uint4(0, 0, 0, 0);
+  s.live = 0;
+  if (active) {
+    m = record_meta(b, rec);
+    s = st[rec];
+  }
+  const bool live = active && s.live;
+  // Eligibility (host): uniform length, multiple of 16, 16-byte aligned
+  // records -- every block of a live record is a full aligned block.
+  const uint64_t nb = live ? m.len / 16 : 0;
+  const uint32_t ctr0 = bswap32(s.j0.w);
+  const uint8_t *src = b.in + m.off;
+  uint8_t *dst = b.out + m.off;
+  uint4 acc = (q == L - 1 && live) ? s.ya : make_uint4(0, 0, 0, 0);
+  const uint32_t lds_base = (uint32_t)reinterpret_cast<uintptr_t>(smem);
+  const uint32_t *rkp = &kp->rk_plain[0][0];
+  const int nchunks = wave_max((int)((nb + 32 * L - 1) / (32 * L)));
+#pragma unroll 1
+  for (int c = 0; c < nchunks; c++) {
+    const uint32_t jc = (uint32_t)(32 * L * c + q);
+    const uint32_t nb32 = (uint32_t)nb;
+    // Every lane of the wave live with all 32 chunk blocks present.
+    const bool full = __all(live && jc + L * 31 < nb32);
+    if (OPEN)
+      acc = full ? ghash_chunk<L, true>(acc, src, jc, nb32, lds_base, mf0)
+                 : ghash_chunk<L, false>(acc, src, jc, nb32, lds_base, mf0);
+    uint32_t p[16][8];
+    {
+      // Round 0 (AddRoundKey) of the counter blocks: words 0..2 are constant
+      // per record (bit masks), word 3 holds the 32 counters.
+      uint32_t w0 = s.j0.x ^ rkp[0], w1 = s.j0.y ^ rkp[1], w2 = s.j0.z ^ rkp[2];
+      // Rebuilt per chunk: hoisted out of the loop, the 96 masks would stay
+      // live (and spill) across the rounds.
+      asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2));
+#pragma unroll
+      for (int k = 0; k < 32; k++) {
+        p[k / 8][k % 8] = 0u - ((w0 >> k) & 1u);
+        p[4 + k / 8][k % 8] = 0u - ((w1 >> k) & 1u);
+        p[8 + k / 8][k % 8] = 0u - ((w2 >> k) & 1u);
+      }
+      const uint32_t cb = ctr0 + 1u + jc;  // inc32: mod 2^32
+      uint32_t t[32];
+#pragma unroll
+      for (int n = 0; n < 32; n++) t[n] = bswap32(cb + (uint32_t)(L * n)) ^ rkp[3];
+      bs_transpose32(t);
+#pragma unroll
+      for (int k = 0; k < 32; k++) p[12 + k / 8][k % 8] = t[k];
+    }
+    BS_STAMP(1);
+#pragma unroll 1
+    for (int r = 1; r < NR; r++) {
+      uint32_t w[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) w[i] = rkp[4 * r + i];
+      bs_round(p, w);
+    }
+    BS_STAMP(2);
+    // Last round one output column (= keystream word c of the 32 blocks) at
+    // a time, transposed back to blocks and applied to word c of each block
+    // with dword loads/stores: the keystream never needs 128 live VGPRs
+    // next to the GHASH state.  (Block indices fit 32 bits: nb < 2^32 by the
+    // GCM length limit.)
+    {
+      uint32_t w[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        w[i] = rkp[4 * NR + i];
+        asm volatile("" : "+s"(w[i]));  // masks are rebuilt per chunk, not hoisted
+      }
+#pragma unroll
+      for (int col = 0; col < 4; col++) {
+        uint32_t t[32];
+        bs_last_round_col(p, w, col, t);
+        bs_transpose32(t);
+        if (full)
+          apply_keystream_word<L, true>(t, src, dst, jc, nb32, col);
+        else
+          apply_keystream_word<L, false>(t, src, dst, jc, nb32, col);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // GHASH over the chunk's ciphertext blocks in order (OPEN: the input was
+    // hashed before it could be overwritten in place, see above).
+    BS_STAMP(3);
+    if (!OPEN) {
+      __builtin_amdgcn_s_waitcnt(0);  // this lane's stores before re-reading them
+      BS_STAMP(4);
+      acc = full ? ghash_chunk<L, true>(acc, dst, jc, nb32, lds_base, mf0)
+                 : ghash_chunk<L, false>(acc, dst, jc, nb32, lds_base, mf0);
+    }
+  }
+  BS_STAMP(5);
+  finish_record<OPEN, L>(acc, nb, m, s, b, rec, active, live, dst, smem, mf0);
+  BS_STAMP(6);
+#if BSSL_AMD_BS_STAMPS
+  if (report && (threadIdx.x & 63) == 0)
+    printf("bs-stamps wave %d: ctr %llu rounds %llu cols %llu wait %llu ghash %llu finish %llu total %llu\n",
+           (int)(threadIdx.x >> 6), (unsigned long long)(ts[1] - ts[0]), (unsigned long long)(ts[2] - ts[1]),
+           (unsigned long long)(ts[3] - ts[2]), (unsigned long long)(ts[4] - ts[3]),
+           (unsigned long long)(ts[5] - ts[4]), (unsigned long long)(ts[6] - ts[5]),
+           (unsigned long long)(ts[6] - ts[0]));
+#else
+  (void)report;
+#endif
+}
+
+template <int NR, bool OPEN, int L>
+__global__ __launch_bounds__(kBsThreads, 2) void gcm_bs_kernel(const GcmKeyDev *__restrict__ keys,
+                                                              BatchDesc b,
+                                                              const RecState *__restrict__ st) {
+  constexpr int kRecPerWaveBs = 64 / L;
+  constexpr int kTile = kBsWaves * kRecPerWaveBs;
+  static_assert(kTile <= 64, "one wave plans a tile with ballots");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kBsLdsBytes];
+  __shared__ uint32_t s_pass_key[kTile];
+  __shared__ uint64_t s_pass_mask[kTile];
+  __shared__ int s_npass;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const uint32_t mf0 = 0xf0u;
+  uint32_t loaded = 0xffffffffu;
+  const uint64_t n = b.num_records;
+  for (uint64_t base = (uint64_t)blockIdx.x * kTile; base < n;
+       base += (uint64_t)gridDim.x * kTile) {
+    __syncthreads();
+    if (wave == 0) {
+      const uint64_t i = base + lane;
+      uint32_t k = (lane < kTile && i < n) ? (b.key_index ? b.key_index[i] : 0u) : 0xffffffffu;
+      if (k != 0xffffffffu && k >= b.num_keys) k = 0;  // flagged dead by the prologue
+      uint64_t pending = __ballot(k != 0xffffffffu);
+      int np = 0;
+      while (pending) {
+        const uint32_t kk = __shfl(k, __builtin_ctzll(pending), 64);
+        const uint64_t mask = __ballot(k == kk) & pending;
+        if (lane == 0) {
+          s_pass_key[np] = kk;
+          s_pass_mask[np] = mask;
+        }
+        pending &= ~mask;
+        np++;
+      }
+      if (lane == 0) s_npass = np;
+    }
+    __syncthreads();
+    const int npass = s_npass;
+    for (int pi = 0; pi < npass; pi++) {
+      const uint32_t k = __builtin_amdgcn_readfirstlane(s_pass_key[pi]);
+      const uint64_t mask = s_pass_mask[pi];
+      if (k != loaded) {
+        __syncthreads();
+        const uint4 *srcp = reinterpret_cast<const uint4 *>(keys[k].htab);
+        for (uint32_t e = tid; e < kBsLdsBytes / 16; e += kBsThreads)
+          reinterpret_cast<uint4 *>(smem + kLdsGhash)[e] = srcp[e];
+        __syncthreads();
+        loaded = k;
+      }
+      const int t = wave * kRecPerWaveBs + lane / L;
+      const bool active = (mask >> t) & 1;
+      process_records_bs<NR, OPEN, L>(keys + k, b, st, base + t, active, smem, mf0,
+                                      blockIdx.x == 0 && base / ((uint64_t)gridDim.x * kTile) == 20);
+    }
+  }
+}
+
 int g_num_cus = 0;
+
+// Lanes per record for the bitsliced kernel, or 0 for the T-table kernel:
+// uniform-length batches of 16-byte-multiple, 16-byte-aligned records long
+// enough to fill 32 blocks per lane.  Opt-in (BSSL_AMD_GCM_BS=1) until it
+// outruns the T-table kernel (DESIGN.md §4.2b has the measurements).
+int bs_lanes(const BatchDesc &b) {
+  static const int enabled = [] {
+    const char *e = getenv("BSSL_AMD_GCM_BS");
+    return e ? atoi(e) : 0;
+  }();
+  if (!enabled || b.lengths || b.offsets) return 0;
+  if ((b.record_len | b.record_stride | reinterpret_cast<uintptr_t>(b.in) |
+       reinterpret_cast<uintptr_t>(b.out)) & 15)
+    return 0;
+  const uint64_t nb = b.record_len / 16;
+  return nb >= 1024 ? 32 : 0;
+}
 
 template <int NR, bool OPEN>
 int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const KernelEvents *ev) {
@@ -758,11 +1056,20 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
     return 2;
   const uint64_t pblocks = (b.num_records + 255) / 256;
   hipLaunchKernelGGL((gcm_prologue<NR>), dim3((unsigned)pblocks), dim3(256), 0, s, keys, b, st);
-  const uint64_t tiles = (b.num_records + kRecPerTile - 1) / kRecPerTile;
-  const unsigned grid = (unsigned)(tiles < (uint64_t)g_num_cus ? tiles : (uint64_t)g_num_cus);
+  const int L = bs_lanes(b);
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
-  hipLaunchKernelGGL((gcm_kernel<NR, OPEN>), dim3(grid), dim3(kThreads), 0, s, keys, b,
-                     (const RecState *)st);
+  if (L) {
+    const uint64_t tiles = (b.num_records + kBsWaves * (64 / L) - 1) / (kBsWaves * (64 / L));
+    const uint64_t slots = 2ull * (uint64_t)g_num_cus;  // 2 workgroups per CU
+    const unsigned grid = (unsigned)(tiles < slots ? tiles : slots);
+    const RecState *cst = st;
+    hipLaunchKernelGGL((gcm_bs_kernel<NR, OPEN, 32>), dim3(grid), dim3(kBsThreads), 0, s, keys, b, cst);
+  } else {
+    const uint64_t tiles = (b.num_records + kRecPerTile - 1) / kRecPerTile;
+    const unsigned grid = (unsigned)(tiles < (uint64_t)g_num_cus ? tiles : (uint64_t)g_num_cus);
+    hipLaunchKernelGGL((gcm_kernel<NR, OPEN>), dim3(grid), dim3(kThreads), 0, s, keys, b,
+                       (const RecState *)st);
+  }
   int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
   hipFreeAsync(st, s);

@@ -2,8 +2,9 @@
 //
 // Device data layout (all resident in HBM, 16-byte aligned):
 //
-//   GcmKeyDev   one per AES-GCM key (41,216 bytes): the AES round keys and
-//               the GHASH multiplication tables for H, H^2, H^4, H^8, H^16.
+//   GcmKeyDev   one per AES-GCM key (49,648 bytes): the AES round keys (T-table
+//               and plain forms) and the GHASH multiplication tables for
+//               H, H^2, H^4, H^8, H^16, H^32.
 //               Equivalent of the reference's GCM128_KEY
 //               (crypto/fipsmodule/aes/internal.h:325-334), re-laid-out for the
 //               LDS-table GHASH of gcm.hip.
@@ -18,7 +19,7 @@
 namespace bssl_amd {
 
 // GHASH table powers held per key: kGhashPow[i] = H^(2^i).
-constexpr int kGhashPowers = 5;           // H, H^2, H^4, H^8, H^16
+constexpr int kGhashPowers = 6;           // H, H^2, H^4, H^8, H^16, H^32
 constexpr int kGhashTableWords = 32 * 16 * 4;  // 32 nibble positions x 16 values x 16 B
 
 struct alignas(16) GcmKeyDev {
@@ -29,12 +30,14 @@ struct alignas(16) GcmKeyDev {
   uint32_t nr;
   uint32_t key_bytes;
   uint32_t pad[2];
+  // The same schedule unrotated (bitsliced kernel: bit masks per round).
+  uint32_t rk_plain[15][4];
   // htab[p][pos][v] = (element with nibble `pos` equal to v) * H^(2^p), as 4
   // little-endian words of the 16 GCM-order bytes.  Nibble position
   // pos = 2*k + 0 is the high nibble of byte k, 2*k + 1 the low nibble.
   uint32_t htab[kGhashPowers][32][16][4];
 };
-static_assert(sizeof(GcmKeyDev) == 240 + 16 + kGhashPowers * 8192, "layout");
+static_assert(sizeof(GcmKeyDev) == 240 + 16 + 240 + kGhashPowers * 8192, "layout");
 
 struct alignas(16) ChaChaKeyDev {
   uint32_t k[8];

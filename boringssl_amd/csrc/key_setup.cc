@@ -162,6 +162,7 @@ bool gcm_key_setup(const uint8_t *key, size_t key_len, GcmKeyDev *out) {
     for (int c = 0; c < 4; c++) {
       uint32_t v = load_le32(w + 16 * r + 4 * c);
       out->rk[r][c] = (r == 0 || r == nr) ? v : rotl32(v, 16);
+      out->rk_plain[r][c] = v;
     }
   uint8_t hb[16] = {0};
   encrypt_block(w, nr, hb, hb);  // H = E_K(0^128), gcm.cc.inc:270-272

@@ -30,6 +30,16 @@ for s in $STEPS; do
       run pmc_c 600 rocprofv3 --kernel-include-regex "${PMC_KERNEL:-gcm_kernel}" --pmc FETCH_SIZE -d gpurun_out/pmc_c -o run --output-format csv -- $PB
       run pmc_d 600 rocprofv3 --kernel-include-regex "${PMC_KERNEL:-gcm_kernel}" --pmc WRITE_SIZE -d gpurun_out/pmc_d -o run --output-format csv -- $PB
       ;;
+    pmcx)
+      # Custom counter passes: PMC_SETS="A B C;D E" (one rocprofv3 pass per set).
+      PB="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --records ${PMC_RECORDS:-262144} ${BENCH_ARGS:-}"
+      i=0
+      IFS=';' read -ra SETS <<< "${PMC_SETS:-SQ_WAVES}"
+      for set in "${SETS[@]}"; do
+        i=$((i+1))
+        run pmcx_$i 600 rocprofv3 --kernel-include-regex "${PMC_KERNEL:-gcm_kernel}" --pmc $set -d gpurun_out/pmcx_$i -o run --output-format csv -- $PB
+      done
+      ;;
     *) echo "unknown step $s" ;;
   esac
 done
