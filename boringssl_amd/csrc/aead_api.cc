@@ -204,6 +204,7 @@ int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch
   d.num_records = batch->num_records;
   d.tag_len = (uint32_t)tag_len;
   d.num_keys = (uint32_t)km->num_keys;
+  d.order = nullptr;
   int rc;
   const KernelEvents *ev = timing_pair();
   if (km->aead->kind == kAeadAesGcm) {

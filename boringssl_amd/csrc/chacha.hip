@@ -265,8 +265,9 @@ __global__ __launch_bounds__(kThreads) void chacha_poly_kernel(
   constexpr int kLog = L == 4 ? 2 : L == 8 ? 3 : 4;
   const int lane = threadIdx.x & 63;
   const int q = lane & (L - 1);
-  const uint64_t rec = ((uint64_t)blockIdx.x * kThreads + threadIdx.x) / L;
-  const bool active = rec < b.num_records;
+  const uint64_t pos = ((uint64_t)blockIdx.x * kThreads + threadIdx.x) / L;
+  const bool active = pos < b.num_records;
+  const uint64_t rec = active && b.order ? b.order[pos] : pos;  // sched.hip order
   RecordMeta m = {0, 0, 0, 0};
   uint32_t kidx = 0;
   if (active) {
@@ -498,15 +499,29 @@ int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, void 
   constexpr int L = 8;  // lanes per record (see chacha_poly_kernel)
   const uint64_t blocks = (b.num_records * L + kThreads - 1) / kThreads;
   if (blocks > 0x7fffffffu) return 1;
+  BatchDesc bo = b;  // with the processing order of a ragged batch
+  uint32_t *order = nullptr;
+  if (wants_length_order(b)) {
+    if (hipMallocAsync(reinterpret_cast<void **>(&order), (b.num_records + 128) * sizeof(uint32_t),
+                       s) != hipSuccess)
+      return 2;
+    const int orc = build_length_order(b.lengths, b.num_records, order, order + b.num_records, s);
+    if (orc) {
+      hipFreeAsync(order, s);
+      return orc;
+    }
+    bo.order = order;
+  }
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
   if (open)
     hipLaunchKernelGGL((chacha_poly_kernel<true, L>), dim3((unsigned)blocks), dim3(kThreads), 0, s,
-                       keys, b);
+                       keys, bo);
   else
     hipLaunchKernelGGL((chacha_poly_kernel<false, L>), dim3((unsigned)blocks), dim3(kThreads), 0,
-                       s, keys, b);
+                       s, keys, bo);
   const int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
+  if (order) hipFreeAsync(order, s);
   return rc;
 }
 

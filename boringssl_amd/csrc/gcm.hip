@@ -424,6 +424,11 @@ __device__ __forceinline__ RecordMeta record_meta(const BatchDesc &b, uint64_t i
   return m;
 }
 
+// Record at processing position i (sched.hip's length order, if any).
+__device__ __forceinline__ uint64_t rec_at(const BatchDesc &b, uint64_t i) {
+  return b.order ? b.order[i] : i;
+}
+
 // Counter-mode cache of one AES stream (see process_records).
 struct WindowCache {
   uint32_t win = 0xffffffffu, k1 = 0, k2 = 0, k3 = 0, l0 = 0, l1 = 0, l2 = 0, l3 = 0;
@@ -729,7 +734,8 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
     if (wave == 0) {
       // Plan the tile: one pass per distinct key, in record order.
       const uint64_t i = base + lane;
-      uint32_t k = (lane < kRecPerTile && i < n) ? (b.key_index ? b.key_index[i] : 0u) : 0xffffffffu;
+      uint32_t k = (lane < kRecPerTile && i < n) ? (b.key_index ? b.key_index[rec_at(b, i)] : 0u)
+                                                 : 0xffffffffu;
       if (k != 0xffffffffu && k >= b.num_keys) k = 0;  // flagged dead by the prologue
       uint64_t pending = __ballot(k != 0xffffffffu);
       int np = 0;
@@ -765,7 +771,8 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
         for (int c = 0; c < 4; c++) rk.w[r][c] = keys[k].rk[r][c];
       const int t = wave * kRecPerWave + g;
       const bool active = (mask >> t) & 1;
-      process_records<NR, OPEN>(rk, b, st, base + t, active, smem, lc0, lc1, mf0);
+      process_records<NR, OPEN>(rk, b, st, active ? rec_at(b, base + t) : 0, active, smem, lc0,
+                                lc1, mf0);
     }
   }
 }
@@ -985,7 +992,8 @@ __global__ __launch_bounds__(kBsThreads, 2) void gcm_bs_kernel(const GcmKeyDev *
     __syncthreads();
     if (wave == 0) {
       const uint64_t i = base + lane;
-      uint32_t k = (lane < kTile && i < n) ? (b.key_index ? b.key_index[i] : 0u) : 0xffffffffu;
+      uint32_t k = (lane < kTile && i < n) ? (b.key_index ? b.key_index[rec_at(b, i)] : 0u)
+                                           : 0xffffffffu;
       if (k != 0xffffffffu && k >= b.num_keys) k = 0;  // flagged dead by the prologue
       uint64_t pending = __ballot(k != 0xffffffffu);
       int np = 0;
@@ -1016,7 +1024,8 @@ __global__ __launch_bounds__(kBsThreads, 2) void gcm_bs_kernel(const GcmKeyDev *
       }
       const int t = wave * kRecPerWaveBs + lane / L;
       const bool active = (mask >> t) & 1;
-      process_records_bs<NR, OPEN, L>(keys + k, b, st, base + t, active, smem, mf0,
+      process_records_bs<NR, OPEN, L>(keys + k, b, st, active ? rec_at(b, base + t) : 0, active,
+                                      smem, mf0,
                                       blockIdx.x == 0 && base / ((uint64_t)gridDim.x * kTile) == 20);
     }
   }
@@ -1029,10 +1038,8 @@ int g_num_cus = 0;
 // enough to fill 32 blocks per lane.  Opt-in (BSSL_AMD_GCM_BS=1) until it
 // outruns the T-table kernel (DESIGN.md §4.2b has the measurements).
 int bs_lanes(const BatchDesc &b) {
-  static const int enabled = [] {
-    const char *e = getenv("BSSL_AMD_GCM_BS");
-    return e ? atoi(e) : 0;
-  }();
+  const char *e = getenv("BSSL_AMD_GCM_BS");
+  const int enabled = e ? atoi(e) : 0;
   if (!enabled || b.lengths || b.offsets) return 0;
   if ((b.record_len | b.record_stride | reinterpret_cast<uintptr_t>(b.in) |
        reinterpret_cast<uintptr_t>(b.out)) & 15)
@@ -1056,6 +1063,22 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
     return 2;
   const uint64_t pblocks = (b.num_records + 255) / 256;
   hipLaunchKernelGGL((gcm_prologue<NR>), dim3((unsigned)pblocks), dim3(256), 0, s, keys, b, st);
+  BatchDesc bo = b;  // with the processing order of a ragged batch
+  uint32_t *order = nullptr;
+  if (wants_length_order(b)) {
+    if (hipMallocAsync(reinterpret_cast<void **>(&order), (b.num_records + 128) * sizeof(uint32_t),
+                       s) != hipSuccess) {
+      hipFreeAsync(st, s);
+      return 2;
+    }
+    const int orc = build_length_order(b.lengths, b.num_records, order, order + b.num_records, s);
+    if (orc) {
+      hipFreeAsync(order, s);
+      hipFreeAsync(st, s);
+      return orc;
+    }
+    bo.order = order;
+  }
   const int L = bs_lanes(b);
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
   if (L) {
@@ -1063,15 +1086,16 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
     const uint64_t slots = 2ull * (uint64_t)g_num_cus;  // 2 workgroups per CU
     const unsigned grid = (unsigned)(tiles < slots ? tiles : slots);
     const RecState *cst = st;
-    hipLaunchKernelGGL((gcm_bs_kernel<NR, OPEN, 32>), dim3(grid), dim3(kBsThreads), 0, s, keys, b, cst);
+    hipLaunchKernelGGL((gcm_bs_kernel<NR, OPEN, 32>), dim3(grid), dim3(kBsThreads), 0, s, keys, bo, cst);
   } else {
     const uint64_t tiles = (b.num_records + kRecPerTile - 1) / kRecPerTile;
     const unsigned grid = (unsigned)(tiles < (uint64_t)g_num_cus ? tiles : (uint64_t)g_num_cus);
-    hipLaunchKernelGGL((gcm_kernel<NR, OPEN>), dim3(grid), dim3(kThreads), 0, s, keys, b,
+    hipLaunchKernelGGL((gcm_kernel<NR, OPEN>), dim3(grid), dim3(kThreads), 0, s, keys, bo,
                        (const RecState *)st);
   }
   int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
+  if (order) hipFreeAsync(order, s);
   hipFreeAsync(st, s);
   return rc;
 }

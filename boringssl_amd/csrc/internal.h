@@ -66,6 +66,9 @@ struct BatchDesc {
   uint64_t num_records;
   uint32_t tag_len;
   uint32_t num_keys;
+  // Processing order (device, num_records entries) or null for 0..n-1; set by
+  // the launchers for ragged batches (sched.hip), never by callers.
+  const uint32_t *order;
 };
 
 // HIP events recorded on the launch stream immediately before and after the
@@ -79,6 +82,14 @@ struct KernelEvents {
 // error code.  `ev` (optional) brackets the bulk kernel.
 int launch_gcm(const GcmKeyDev *keys, const BatchDesc &b, bool open,
                int nr, void *stream, const KernelEvents *ev);
+// Builds `order` (n entries) grouping records by length class, longest first;
+// `scratch` holds 128 uint32.  Returns 0 or a HIP error code.
+int build_length_order(const uint64_t *lengths, uint64_t n, uint32_t *order, uint32_t *scratch,
+                       void *stream);
+// Whether a batch is worth reordering (ragged and large enough).
+inline bool wants_length_order(const BatchDesc &b) {
+  return b.lengths && b.num_records >= 4096 && b.num_records < (uint64_t(1) << 32);
+}
 int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open,
                   void *stream, const KernelEvents *ev);
 int launch_synth(uint64_t first, size_t n, const uint64_t *offsets,

@@ -196,6 +196,65 @@ def test_batch_ragged_vs_oracle(aead, layout):
         assert ok and outs[i] == ct and tags[i] == tag, (i, lens[i], len(ads[i]))
 
 
+@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm", "chacha20-poly1305"])
+@pytest.mark.parametrize("multikey", [False, True])
+def test_batch_large_ragged_reordered(aead, multikey):
+    """>= 4096 ragged records: the launcher processes them in length-class
+    order (sched.hip); outputs must still land per record, as the oracle's."""
+    rng = np.random.default_rng(11 + multikey)
+    n = 5000
+    lens = rng.choice([0, 1, 16, 17, 200, 1350, 4096, 9000, 16384, 16400], size=n).tolist()
+    ins = [rng.integers(0, 256, size=l, dtype=np.uint8).tobytes() for l in lens]
+    nonces = [rng.integers(0, 256, size=12, dtype=np.uint8).tobytes() for _ in range(n)]
+    ads = [rng.integers(0, 256, size=13, dtype=np.uint8).tobytes() for _ in range(n)]
+    nkeys = 7 if multikey else 1
+    keys = [rng.integers(0, 256, size=AEAD_KEYLEN[aead], dtype=np.uint8).tobytes()
+            for _ in range(nkeys)]
+    ki = rng.integers(0, nkeys, size=n).tolist() if multikey else None
+    outs, tags, st = run_batch(aead, keys, ki, ins, nonces, ads, 16, odd=5)
+    assert st.all()
+    for i in range(n):
+        k = keys[ki[i]] if multikey else keys[0]
+        ok, ct, tag = o.seal(ORACLE_ID[aead], k, nonces[i], ins[i], ads[i])
+        assert ok and outs[i] == ct and tags[i] == tag, (i, lens[i])
+    back, _, st = run_batch(aead, keys, ki, outs, nonces, ads, 16, open_=True, tags=tags, odd=5)
+    assert st.all() and back == ins
+
+
+@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm"])
+@pytest.mark.parametrize("rlen", [16384, 17408, 32768])
+def test_bitsliced_gcm_path(aead, rlen, monkeypatch):
+    """The opt-in bitsliced kernel (BSSL_AMD_GCM_BS=1; uniform, 16-byte
+    multiple records of >= 1024 blocks: full and partial 32-block chunks)."""
+    monkeypatch.setenv("BSSL_AMD_GCM_BS", "1")
+    rng = np.random.default_rng(rlen)
+    n = 24
+    key = rng.integers(0, 256, size=AEAD_KEYLEN[aead], dtype=np.uint8).tobytes()
+    pt = rng.integers(0, 256, size=n * rlen, dtype=np.uint8)
+    nonces = rng.integers(0, 256, size=n * 12, dtype=np.uint8)
+    ad = rng.integers(0, 256, size=n * 13, dtype=np.uint8)
+    d_pt, d_ct = _t(pt), torch.zeros(n * rlen, dtype=torch.uint8, device=DEV)
+    d_tags = torch.zeros(n * 16, dtype=torch.uint8, device=DEV)
+    d_st = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    ctx = ba.AEADCtx(aead, key, 16)
+    b = ba.make_batch(n, d_pt, d_ct, d_tags, _t(nonces), 12, _t(ad), record_stride=rlen,
+                      record_len=rlen, ad_stride=13, ad_len=13, status=d_st)
+    ctx.seal_batch_device(b)
+    torch.cuda.synchronize()
+    assert bool(d_st.all())
+    ct, tg = d_ct.cpu().numpy(), d_tags.cpu().numpy()
+    for i in range(n):
+        ok, c, t = o.seal(ORACLE_ID[aead], key, nonces[12 * i:12 * i + 12].tobytes(),
+                          pt[rlen * i:rlen * (i + 1)].tobytes(), ad[13 * i:13 * i + 13].tobytes())
+        assert ok and ct[rlen * i:rlen * (i + 1)].tobytes() == c and tg[16 * i:16 * i + 16].tobytes() == t, i
+    d_back = torch.zeros_like(d_pt)
+    b2 = ba.make_batch(n, d_ct, d_back, d_tags, _t(nonces), 12, _t(ad), record_stride=rlen,
+                       record_len=rlen, ad_stride=13, ad_len=13, status=d_st)
+    ctx.open_batch_device(b2)
+    torch.cuda.synchronize()
+    assert bool(d_st.all()) and torch.equal(d_back, d_pt)
+
+
 def test_batch_gcm_nonce_lengths_and_truncated_tags():
     rng = random.Random(7)
     for nl in (1, 8, 12, 16, 17, 60, 128):
@@ -270,7 +329,9 @@ def synth_device_batch(aead, nkeys, rpk, length, first=0):
     offs[1:] = np.cumsum(padded[:-1])
     total = int(padded.sum())
     d_offs, d_lens = _t(offs.astype(np.int64)), _t(lens.astype(np.int64))
-    d_pt = torch.empty(total, dtype=torch.uint8, device=DEV)
+    # zero-filled so the padding between records is defined (the kernels must
+    # never write it; the in-place round trip below compares whole buffers)
+    d_pt = torch.zeros(total, dtype=torch.uint8, device=DEV)
     d_n = torch.empty(12 * n, dtype=torch.uint8, device=DEV)
     d_a = torch.empty(13 * n, dtype=torch.uint8, device=DEV)
     ba.synth_fill_device(first, n, d_offs, d_lens, d_pt, d_n, d_a)
@@ -300,7 +361,7 @@ def _run_synth_digest(name):
     aead, nkeys, rpk, length = g["aead"], g["nkeys"], g["records_per_key"], g["len"]
     n = nkeys * rpk
     lens, offs, d_offs, d_lens, d_pt, d_n, d_a = synth_device_batch(aead, nkeys, rpk, length)
-    d_out = torch.empty_like(d_pt)
+    d_out = torch.zeros_like(d_pt)
     d_tags = torch.zeros(16 * n, dtype=torch.uint8, device=DEV)
     d_st = torch.zeros(n, dtype=torch.uint8, device=DEV)
     keys = [o.synth_key(k, AEAD_KEYLEN[aead]) for k in range(nkeys)]
