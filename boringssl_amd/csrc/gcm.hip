@@ -107,17 +107,22 @@ constexpr Tables make_tables() {
 __constant__ Tables kTables = make_tables();
 
 // ---------------------------------------------------------------------------
-// LDS layout of the main kernel (one static array, so offsets are link-time
-// constants that fold into the 16-bit ds_read offset field):
-//   [0, 40960)       GHASH nibble tables, power p at p*8192, position k at
-//                    k*256, value v at v*16
-//   [40960, 106496)  AES T0/T1, replicated per bank (see header comment)
+// LDS layout of the T-table kernel (one static array at LDS address 0):
+//   [0, 65536)       GHASH byte table of H^16, "lane-rotated": the product of
+//                    (byte value e at byte position p) x H^16 at e*256 + p*16
+//                    (16 positions side by side in one 256-byte row, so 16
+//                    lanes reading 16 different positions never share a bank)
+//   [65536, 131072)  AES T0/T1, replicated per bank (see header comment); the
+//                    lookup address carries bit 16 (lane constants lc0/lc1)
+//   [131072, ...)    tile plan (keys and record masks of the passes)
+// The bitsliced kernel keeps the nibble tables (kLdsGhash, 8 KiB per power).
 constexpr uint32_t kLdsGhash = 0;
-constexpr int kTGhashPowers = 5;  // the T-table kernel uses H .. H^16
-constexpr uint32_t kGhashLdsBytes = kTGhashPowers * 8192;
-constexpr uint32_t kLdsAes = kGhashLdsBytes;
+constexpr uint32_t kLdsG8 = 0;
+constexpr uint32_t kG8Bytes = 256 * 256;
+constexpr uint32_t kLdsAes = kG8Bytes;
 constexpr uint32_t kAesLdsBytes = 256 * 256;
-constexpr uint32_t kLdsBytes = kLdsAes + kAesLdsBytes;
+constexpr uint32_t kLdsPlan = kLdsAes + kAesLdsBytes;
+constexpr uint32_t kLdsBytes = kLdsPlan + 64 * 16 + 16;
 
 __device__ __forceinline__ uint32_t rotl(uint32_t v, int n) {
   return __builtin_amdgcn_alignbit(v, v, 32 - n);
@@ -162,10 +167,11 @@ __device__ __forceinline__ uint32_t nib(uint32_t v, uint32_t mf0) {
 // ---------------------------------------------------------------------------
 // AES.  State: 4 little-endian column words (byte r of word c = row r).
 // Lookup address of the T(slot) entry for state byte k: v_perm puts byte k at
-// bits 8..15 below which the lane/slot constant `lc` (bits 0..7) sits.
+// bits 8..15 below which the lane/slot constant `lc` (bits 0..7) sits; byte 2
+// of `lc` (the table base's bit 16) is carried along.
 template <int K>
 __device__ __forceinline__ uint32_t taddr(uint32_t lc, uint32_t s) {
-  return __builtin_amdgcn_perm(lc, s, 0x0c0c0004u | (K << 8));
+  return __builtin_amdgcn_perm(lc, s, 0x0c060004u | (K << 8));
 }
 
 template <uint32_t TB>
@@ -266,6 +272,78 @@ __device__ __forceinline__ uint4 aes_rounds(uint32_t s0, uint32_t s1, uint32_t s
   o.w = xor3(__builtin_amdgcn_perm(x31, x30, 0x0c0c0501u),
              __builtin_amdgcn_perm(x33, x32, 0x06020c0cu), rk.w[NR][3]);
   return o;
+}
+
+// ---------------------------------------------------------------------------
+// GHASH multiply by H^16 with the lane-rotated byte table (kLdsG8), spread
+// over the AES rounds of the same iteration.  Lane q (its index within the
+// record's 16 lanes) looks up byte position (t + q) mod 16 in step t, so the
+// 16 lanes of each ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,
+// 28-31}, +32) read 16 different 16-byte slots of the 256-byte row: no bank
+// conflicts, 16 lookups per block instead of 32 nibble lookups.  The input is
+// rotated by q bytes once (r), so step t takes byte t of r with a
+// wave-uniform selector; P[k] byte i holds the slot offset ((4k+i+q) mod 16)*16.
+struct Gh8 {
+  uint32_t r0, r1, r2, r3;  // multiplier input, rotated down by q bytes
+  uint4 g;                  // running sum of the looked-up products
+};
+
+// r byte t = x byte (t + q) mod 16, q = 4*s + bsh (s1 = s&1, s2 = s&2).
+__device__ __forceinline__ void g8_rotate(Gh8 &h, uint4 x, bool s1, bool s2, uint32_t bsh) {
+  const uint32_t e0 = s1 ? x.y : x.x, e1 = s1 ? x.z : x.y, e2 = s1 ? x.w : x.z,
+                 e3 = s1 ? x.x : x.w;
+  const uint32_t d0 = s2 ? e2 : e0, d1 = s2 ? e3 : e1, d2 = s2 ? e0 : e2, d3 = s2 ? e1 : e3;
+  h.r0 = __builtin_amdgcn_alignbyte(d1, d0, bsh);
+  h.r1 = __builtin_amdgcn_alignbyte(d2, d1, bsh);
+  h.r2 = __builtin_amdgcn_alignbyte(d3, d2, bsh);
+  h.r3 = __builtin_amdgcn_alignbyte(d0, d3, bsh);
+}
+
+template <int T>
+__device__ __forceinline__ uint4 g8_load(const Gh8 &h, const uint32_t (&P)[4],
+                                         const uint8_t *smem) {
+  const uint32_t r = T < 4 ? h.r0 : T < 8 ? h.r1 : T < 12 ? h.r2 : h.r3;
+  const uint32_t a =
+      __builtin_amdgcn_perm(r, P[T >> 2], 0x0c0c0000u | ((4u + (T & 3)) << 8) | (T & 3));
+  return *reinterpret_cast<const uint4 *>(smem + kLdsG8 + a);
+}
+
+// One AES round (as aes_round) with GHASH steps 2*GI, 2*GI+1 issued alongside
+// (GI < 8), so the wave keeps 16 x 4-byte + 2 x 16-byte reads in flight.
+template <uint32_t TB, int GI>
+__device__ __forceinline__ void aes_round_g(uint32_t &s0, uint32_t &s1, uint32_t &s2,
+                                            uint32_t &s3, const uint32_t *rkx,
+                                            const uint8_t *smem, uint32_t lc0, uint32_t lc1,
+                                            Gh8 &h, const uint32_t (&P)[4]) {
+  uint4 v0, v1;
+  if constexpr (GI < 8) {
+    v0 = g8_load<2 * GI>(h, P, smem);
+    v1 = g8_load<2 * GI + 1>(h, P, smem);
+  }
+  const uint32_t x00 = tload<TB>(smem, taddr<0>(lc0, s0)), x01 = tload<TB>(smem, taddr<1>(lc1, s1)),
+                 x02 = tload<TB>(smem, taddr<2>(lc0, s2)), x03 = tload<TB>(smem, taddr<3>(lc1, s3));
+  const uint32_t x10 = tload<TB>(smem, taddr<0>(lc0, s1)), x11 = tload<TB>(smem, taddr<1>(lc1, s2)),
+                 x12 = tload<TB>(smem, taddr<2>(lc0, s3)), x13 = tload<TB>(smem, taddr<3>(lc1, s0));
+  const uint32_t x20 = tload<TB>(smem, taddr<0>(lc0, s2)), x21 = tload<TB>(smem, taddr<1>(lc1, s3)),
+                 x22 = tload<TB>(smem, taddr<2>(lc0, s0)), x23 = tload<TB>(smem, taddr<3>(lc1, s1));
+  const uint32_t x30 = tload<TB>(smem, taddr<0>(lc0, s3)), x31 = tload<TB>(smem, taddr<1>(lc1, s0)),
+                 x32 = tload<TB>(smem, taddr<2>(lc0, s1)), x33 = tload<TB>(smem, taddr<3>(lc1, s2));
+  s0 = xor3(x00, x01, rotl(xor3(x02, x03, rkx[0]), 16));
+  s1 = xor3(x10, x11, rotl(xor3(x12, x13, rkx[1]), 16));
+  s2 = xor3(x20, x21, rotl(xor3(x22, x23, rkx[2]), 16));
+  s3 = xor3(x30, x31, rotl(xor3(x32, x33, rkx[3]), 16));
+  if constexpr (GI < 8) h.g = xor4_3(h.g, v0, v1);
+}
+
+template <int GI, int R, int NR, uint32_t TB>
+__device__ __forceinline__ void aes_rounds_g_from(uint32_t &s0, uint32_t &s1, uint32_t &s2,
+                                                  uint32_t &s3, const RoundKeys &rk,
+                                                  const uint8_t *smem, uint32_t lc0, uint32_t lc1,
+                                                  Gh8 &h, const uint32_t (&P)[4]) {
+  if constexpr (R < NR) {
+    aes_round_g<TB, GI>(s0, s1, s2, s3, rk.w[R], smem, lc0, lc1, h, P);
+    aes_rounds_g_from<GI + 1, R + 1, NR, TB>(s0, s1, s2, s3, rk, smem, lc0, lc1, h, P);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -543,12 +621,13 @@ __global__ __launch_bounds__(256) void gcm_prologue(const GcmKeyDev *__restrict_
 // output of a failed record.  Lane algebra: lane q holds the
 // virtual elements v = q+1+L*i of [Y_A, C_0, ..., C_{nb-1}]; rotate so position
 // p holds the lane whose weight is H^(L-1-p), then tree-combine with
-// H, H^2, ..., H^(L/2) (tables 0..log2(L)-1 at kLdsGhash).
+// H, H^2, ..., H^(L/2) (nibble tables 0..log2(L)-1 at `tab`: LDS or the key's
+// global copy).
 template <bool OPEN, int L>
 __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const RecordMeta &m,
                                               const RecState &s, const BatchDesc &b, uint64_t rec,
                                               bool active, bool live, uint8_t *dst,
-                                              const uint8_t *smem, uint32_t mf0) {
+                                              const uint8_t *tab, uint32_t mf0) {
   constexpr int kLevels = L == 32 ? 5 : L == 16 ? 4 : L == 8 ? 3 : L == 4 ? 2 : -1;
   static_assert(kLevels > 0, "lanes per record");
   const int q = threadIdx.x & (L - 1);
@@ -560,7 +639,7 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
   for (int t = 0; t < kLevels; t++) {
     const int sh = 1 << t;
     const uint4 o = shfl_down4(a, sh, L);
-    const uint4 mlt = gmul<0>(a, smem + kLdsGhash + t * 8192, mf0);
+    const uint4 mlt = gmul<0>(a, tab + t * 8192, mf0);
     if ((q & (2 * sh - 1)) == 0) a = xor4(mlt, o);
   }
   // Tag (gcm.cc.inc:576-604): ((Z*H) ^ len block) * H ^ E_K(J0), in lane 0.
@@ -569,7 +648,7 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
                          bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits));
 #pragma unroll 1
   for (int t = 0; t < 2; t++) {
-    a = xor4(gmul<0>(a, smem + kLdsGhash, mf0), add);
+    a = xor4(gmul<0>(a, tab, mf0), add);
     add = s.ek0;
   }
   const uint4 tag = a;
@@ -608,11 +687,13 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
 // ---------------------------------------------------------------------------
 // Bulk kernel: CTR keystream + GHASH + tag for the (up to) 4 records of a
 // wave, 16 lanes per record.  `active` is per group (record in this key pass).
+// `gtab` = the key's nibble tables in global memory (record-end tree only).
 template <int NR, bool OPEN>
 __device__ __forceinline__ void process_records(const RoundKeys &rk, const BatchDesc &b,
                                                 const RecState *__restrict__ st, uint64_t rec,
                                                 bool active, const uint8_t *smem,
-                                                uint32_t lc0, uint32_t lc1, uint32_t mf0) {
+                                                const uint8_t *gtab, uint32_t lc0, uint32_t lc1,
+                                                uint32_t mf0) {
   const int q = threadIdx.x & 15;
   RecordMeta m = {0, 0, 0, 0};
   RecState s;
@@ -632,15 +713,25 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   const bool aligned = ((reinterpret_cast<uintptr_t>(src) |
                          reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
   uint4 acc = (q == 15 && live) ? s.ya : make_uint4(0, 0, 0, 0);
+  // GHASH lane constants (Gh8): rotation by q bytes and the slot offsets.
+  const bool rs1 = (q >> 2) & 1, rs2 = (q >> 3) & 1;
+  const uint32_t rbs = (uint32_t)q & 3u;
+  uint32_t P[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) v |= (uint32_t)(((4 * k + i + q) & 15) << 4) << (8 * i);
+    P[k] = v;
+  }
   // Counter-mode caching (Bernstein-Schwabe): within a 256-counter window only
   // byte 15 of the counter block changes, so round 1 needs one lookup (column
   // 0, row 3) and round 2 four; K0..K3 / L0..L3 hold the constant parts and
   // are recomputed when a lane's counter enters a new window.
-  constexpr uint32_t T = kLdsAes;
+  constexpr uint32_t T = 0;  // the table base (kLdsAes) rides in lc0/lc1
   const uint32_t k0 = tload<T>(smem, taddr<0>(lc0, c0)) ^ tload<T>(smem, taddr<1>(lc1, c1)) ^
                       rotl(tload<T>(smem, taddr<2>(lc0, c2)) ^ rk.w[1][0], 16);
   WindowCache wc;
-  const uint32_t lds_base = (uint32_t)reinterpret_cast<uintptr_t>(smem);  // LDS offset
   const int iters = wave_max((int)((nb + 15) / 16));
   // Full aligned 16-byte blocks of this lane's record; the rest (the partial
   // last block, or every block of an unaligned record) take the byte path.
@@ -654,18 +745,24 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     return v;
   };
   // One iteration: block j = it*16 + q, plaintext (if full) already in x.
+  // The GHASH multiply of the accumulator (acc * H^16, its input known from
+  // the previous iteration) is interleaved with this block's AES rounds.
   auto step = [&](int it, uint4 x) {
     const uint64_t j = (uint64_t)it * 16 + q;
     const uint32_t ctr = ctr0 + 1u + (uint32_t)j;  // inc32 wraps mod 2^32
     const uint32_t s3 = bswap32(ctr) ^ rk.w[0][3];
     wc.update<T>(ctr, s3, c0, c1, c2, rk, smem, lc0, lc1);
+    Gh8 h;
+    g8_rotate(h, acc, rs1, rs2, rbs);
     uint32_t a0, a1, a2, a3;
-    wc.rounds12<T>(k0, s3, a0, a1, a2, a3, smem, lc0, lc1);
-#if BSSL_AMD_ABLATE == 2  // diagnostic build: no AES rounds 3..NR (wrong output)
-    const uint4 ks = make_uint4(a0, a1, a2, a3);
-#else
-    const uint4 ks = aes_rounds<NR, T, 3>(a0, a1, a2, a3, rk, smem, lc0, lc1);
-#endif
+    {
+      const uint4 v0 = g8_load<0>(h, P, smem), v1 = g8_load<1>(h, P, smem);
+      wc.rounds12<T>(k0, s3, a0, a1, a2, a3, smem, lc0, lc1);
+      h.g = xor4(v0, v1);
+    }
+    // Rounds 3..NR-1 carry GHASH steps 2..15 (NR - 3 >= 7 rounds).
+    aes_rounds_g_from<1, 3, NR, T>(a0, a1, a2, a3, rk, smem, lc0, lc1, h, P);
+    const uint4 ks = aes_rounds<NR, T, NR>(a0, a1, a2, a3, rk, smem, lc0, lc1);
     uint4 y = xor4(x, ks);
     if (j < nfull) {
       *reinterpret_cast<uint4 *>(dst + j * 16) = y;
@@ -679,7 +776,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
 #if BSSL_AMD_ABLATE == 1  // diagnostic build: no GHASH multiply (wrong tags)
       acc = xor4(acc, OPEN ? x : y);
 #else
-      acc = xor4(gmul_batched<kLdsGhash + 4 * 8192>(acc, lds_base, mf0), OPEN ? x : y);
+      acc = xor4(h.g, OPEN ? x : y);
 #endif
     }
   };
@@ -697,7 +794,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     step(it + 1, x1);
   }
   if (it < iters) step(it, x0);
-  finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, smem, mf0);
+  finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, gtab, mf0);
 }
 
 template <int NR, bool OPEN>
@@ -707,22 +804,22 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
   static_assert(kRecPerTile <= 64, "one wave plans a tile with ballots");
   __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
   // Pass list of the current tile: key and 64-bit record mask per pass.
-  __shared__ uint32_t s_pass_key[kRecPerTile];
-  __shared__ uint64_t s_pass_mask[kRecPerTile];
-  __shared__ int s_npass;
+  uint32_t *s_pass_key = reinterpret_cast<uint32_t *>(smem + kLdsPlan);
+  uint64_t *s_pass_mask = reinterpret_cast<uint64_t *>(smem + kLdsPlan + 64 * 4);
+  int *s_npass = reinterpret_cast<int *>(smem + kLdsPlan + 64 * 16);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int g = lane >> 4;
 
   // AES tables, replicated per bank: entry idx, slot t, lane l at
-  // idx*256 + t*128 + l*4.  Slot 1 holds T1 = rotl8(T0).
+  // kLdsAes + idx*256 + t*128 + l*4.  Slot 1 holds T1 = rotl8(T0).
   for (int e = tid; e < 256 * 64; e += kThreads) {
     const int idx = e >> 6, slot = (e >> 5) & 1;
     const uint32_t v = kTables.te0[idx];
     reinterpret_cast<uint32_t *>(smem + kLdsAes)[e] = slot ? rotl(v, 8) : v;
   }
-  const uint32_t lc0 = (uint32_t)(lane & 31) * 4u;
+  const uint32_t lc0 = kLdsAes + (uint32_t)(lane & 31) * 4u;
   const uint32_t lc1 = lc0 + 128u;
   const uint32_t mf0 = 0xf0u;
 
@@ -749,18 +846,24 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
         pending &= ~mask;
         np++;
       }
-      if (lane == 0) s_npass = np;
+      if (lane == 0) *s_npass = np;
     }
     __syncthreads();
-    const int npass = s_npass;
+    const int npass = *s_npass;
     for (int pi = 0; pi < npass; pi++) {
       const uint32_t k = __builtin_amdgcn_readfirstlane(s_pass_key[pi]);
       const uint64_t mask = s_pass_mask[pi];
+      const uint8_t *gtab = reinterpret_cast<const uint8_t *>(keys[k].htab);
       if (k != loaded) {
         __syncthreads();
-        const uint4 *srcp = reinterpret_cast<const uint4 *>(keys[k].htab);
-        for (uint32_t e = tid; e < kGhashLdsBytes / 16; e += kThreads)
-          reinterpret_cast<uint4 *>(smem + kLdsGhash)[e] = srcp[e];
+        // Byte table of H^16 from the key's nibble tables (power 4): entry
+        // (e, p) = T[2p][e >> 4] ^ T[2p+1][e & 15] (key_setup.cc layout).
+        const uint4 *t16 = reinterpret_cast<const uint4 *>(keys[k].htab[4]);
+        for (uint32_t e = tid; e < 4096; e += kThreads) {
+          const uint32_t ev = e >> 4, p = e & 15;
+          reinterpret_cast<uint4 *>(smem + kLdsG8)[e] =
+              xor4(t16[(2 * p) * 16 + (ev >> 4)], t16[(2 * p + 1) * 16 + (ev & 15)]);
+        }
         __syncthreads();
         loaded = k;
       }
@@ -771,8 +874,8 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
         for (int c = 0; c < 4; c++) rk.w[r][c] = keys[k].rk[r][c];
       const int t = wave * kRecPerWave + g;
       const bool active = (mask >> t) & 1;
-      process_records<NR, OPEN>(rk, b, st, active ? rec_at(b, base + t) : 0, active, smem, lc0,
-                                lc1, mf0);
+      process_records<NR, OPEN>(rk, b, st, active ? rec_at(b, base + t) : 0, active, smem, gtab,
+                                lc0, lc1, mf0);
     }
   }
 }
@@ -956,7 +1059,7 @@ __device__ __forceinline__ void process_records_bs(const GcmKeyDev *__restrict__
     }
   }
   BS_STAMP(5);
-  finish_record<OPEN, L>(acc, nb, m, s, b, rec, active, live, dst, smem, mf0);
+  finish_record<OPEN, L>(acc, nb, m, s, b, rec, active, live, dst, smem + kLdsGhash, mf0);
   BS_STAMP(6);
 #if BSSL_AMD_BS_STAMPS
   if (report && (threadIdx.x & 63) == 0)
