@@ -57,10 +57,32 @@ namespace {
 #ifndef BSSL_AMD_GHASH_GROUP
 #define BSSL_AMD_GHASH_GROUP 1
 #endif
+#ifndef BSSL_AMD_GCM_PREFETCH
+#define BSSL_AMD_GCM_PREFETCH 1
+#endif
 #ifndef BSSL_AMD_GCM_WAVES
 #define BSSL_AMD_GCM_WAVES 12
 #endif
 constexpr int kWaves = BSSL_AMD_GCM_WAVES;
+#ifndef BSSL_AMD_GCM_STAMPS
+#define BSSL_AMD_GCM_STAMPS 0
+#endif
+#if BSSL_AMD_GCM_STAMPS
+// Diagnostic build: per-wave cycle counts of the T-table kernel's loop and
+// AES rounds (s_memtime, with its own lgkmcnt wait), printed per wave 0.
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+#define g_stamp_rounds stv[0]
+#define g_stamp_iters stv[1]
+#define g_stamp_loop stv[2]
+#endif
+// Per-wave diagnostic counters (stamps build only; see BSSL_AMD_GCM_STAMPS).
+struct StampVec {
+  uint64_t v[3];
+};
 constexpr int kThreads = kWaves * 64;
 constexpr int kRecPerWave = 4;
 constexpr int kRecPerTile = kWaves * kRecPerWave;  // <= 64 (one planning wave)
@@ -335,6 +357,58 @@ __device__ __forceinline__ void aes_round_g(uint32_t &s0, uint32_t &s1, uint32_t
   if constexpr (GI < 8) h.g = xor4_3(h.g, v0, v1);
 }
 
+// Two blocks per lane (S = 2): one round of both AES states with GHASH steps
+// 2*GI, 2*GI+1 of both accumulators (GI < 8): 32 x 4-byte + 4 x 16-byte reads
+// in flight per wave.
+template <uint32_t TB, int GI>
+__device__ __forceinline__ void aes_round2_g(uint32_t (&a)[4], uint32_t (&c)[4],
+                                             const uint32_t *rkx, const uint8_t *smem,
+                                             uint32_t lc0, uint32_t lc1, Gh8 &ha, Gh8 &hc,
+                                             const uint32_t (&P)[4]) {
+  uint4 va0, va1, vc0, vc1;
+  if constexpr (GI < 8) {
+    va0 = g8_load<2 * GI>(ha, P, smem);
+    va1 = g8_load<2 * GI + 1>(ha, P, smem);
+    vc0 = g8_load<2 * GI>(hc, P, smem);
+    vc1 = g8_load<2 * GI + 1>(hc, P, smem);
+  }
+  uint32_t x[2][4][4];
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const uint32_t(&s)[4] = i ? c : a;
+#pragma unroll
+    for (int col = 0; col < 4; col++) {
+      x[i][col][0] = tload<TB>(smem, taddr<0>(lc0, s[col]));
+      x[i][col][1] = tload<TB>(smem, taddr<1>(lc1, s[(col + 1) & 3]));
+      x[i][col][2] = tload<TB>(smem, taddr<2>(lc0, s[(col + 2) & 3]));
+      x[i][col][3] = tload<TB>(smem, taddr<3>(lc1, s[(col + 3) & 3]));
+    }
+  }
+#pragma unroll
+  for (int col = 0; col < 4; col++) {
+    a[col] = xor3(x[0][col][0], x[0][col][1], rotl(xor3(x[0][col][2], x[0][col][3], rkx[col]), 16));
+    c[col] = xor3(x[1][col][0], x[1][col][1], rotl(xor3(x[1][col][2], x[1][col][3], rkx[col]), 16));
+  }
+  if constexpr (GI < 8) {
+    ha.g = xor4_3(ha.g, va0, va1);
+    hc.g = xor4_3(hc.g, vc0, vc1);
+  }
+  // Keep the scheduler from hoisting the next round's work into this one
+  // (it otherwise runs out of registers at 3 waves per SIMD).
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int GI, int R, int NR, uint32_t TB>
+__device__ __forceinline__ void aes_rounds2_g_from(uint32_t (&a)[4], uint32_t (&c)[4],
+                                                   const RoundKeys &rk, const uint8_t *smem,
+                                                   uint32_t lc0, uint32_t lc1, Gh8 &ha, Gh8 &hc,
+                                                   const uint32_t (&P)[4]) {
+  if constexpr (R < NR) {
+    aes_round2_g<TB, GI>(a, c, rk.w[R], smem, lc0, lc1, ha, hc, P);
+    aes_rounds2_g_from<GI + 1, R + 1, NR, TB>(a, c, rk, smem, lc0, lc1, ha, hc, P);
+  }
+}
+
 template <int GI, int R, int NR, uint32_t TB>
 __device__ __forceinline__ void aes_rounds_g_from(uint32_t &s0, uint32_t &s1, uint32_t &s2,
                                                   uint32_t &s3, const RoundKeys &rk,
@@ -398,6 +472,177 @@ __device__ __forceinline__ void lds_read8(const uint32_t a[8], v4u d[8]) {
       : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]),
         "i"(OFF), "i"(OFF + 256), "i"(OFF + 512), "i"(OFF + 768), "i"(OFF + 1024),
         "i"(OFF + 1280), "i"(OFF + 1536), "i"(OFF + 1792));
+}
+
+// Counter-mode cache of one AES stream (see process_records).
+struct WindowCache {
+  uint32_t win = 0xffffffffu, k1 = 0, k2 = 0, k3 = 0, l0 = 0, l1 = 0, l2 = 0, l3 = 0;
+
+  template <uint32_t T>
+  __device__ __forceinline__ void update(uint32_t ctr, uint32_t s3, uint32_t c0, uint32_t c1,
+                                         uint32_t c2, const RoundKeys &rk,
+                                         const uint8_t *smem, uint32_t lc0, uint32_t lc1) {
+    if ((ctr >> 8) == win) return;
+    win = ctr >> 8;
+    k1 = round_col<T>(smem, lc0, lc1, c1, c2, s3, c0, rk.w[1][1]);
+    k2 = round_col<T>(smem, lc0, lc1, c2, s3, c0, c1, rk.w[1][2]);
+    k3 = round_col<T>(smem, lc0, lc1, s3, c0, c1, c2, rk.w[1][3]);
+    l0 = tload<T>(smem, taddr<1>(lc1, k1)) ^
+         rotl(tload<T>(smem, taddr<2>(lc0, k2)) ^ tload<T>(smem, taddr<3>(lc1, k3)) ^
+                  rk.w[2][0], 16);
+    l1 = tload<T>(smem, taddr<0>(lc0, k1)) ^ tload<T>(smem, taddr<1>(lc1, k2)) ^
+         rotl(tload<T>(smem, taddr<2>(lc0, k3)) ^ rk.w[2][1], 16);
+    l2 = tload<T>(smem, taddr<0>(lc0, k2)) ^ tload<T>(smem, taddr<1>(lc1, k3)) ^
+         rotl(tload<T>(smem, taddr<3>(lc1, k1)) ^ rk.w[2][2], 16);
+    l3 = tload<T>(smem, taddr<0>(lc0, k3)) ^
+         rotl(tload<T>(smem, taddr<2>(lc0, k1)) ^ tload<T>(smem, taddr<3>(lc1, k2)) ^
+                  rk.w[2][3], 16);
+  }
+
+  // Rounds 1 and 2 of a counter block whose round-0 word 3 is s3.
+  template <uint32_t T>
+  __device__ __forceinline__ void rounds12(uint32_t k0, uint32_t s3, uint32_t &u0, uint32_t &u1,
+                                           uint32_t &u2, uint32_t &u3, const uint8_t *smem,
+                                           uint32_t lc0, uint32_t lc1) const {
+    const uint32_t t0 = k0 ^ rotl(tload<T>(smem, taddr<3>(lc1, s3)), 16);
+    u0 = tload<T>(smem, taddr<0>(lc0, t0)) ^ l0;
+    u1 = rotl(tload<T>(smem, taddr<3>(lc1, t0)), 16) ^ l1;
+    u2 = rotl(tload<T>(smem, taddr<2>(lc0, t0)), 16) ^ l2;
+    u3 = tload<T>(smem, taddr<1>(lc1, t0)) ^ l3;
+  }
+};
+
+#include "gcm_rounds.inc"
+
+__device__ __forceinline__ uint4 as_uint4(v4u v) { return make_uint4(v.x, v.y, v.z, v.w); }
+
+// Materializes v here: an empty volatile asm using it keeps hipcc from
+// sinking the XORs that produce it past the following asm rounds (which
+// would keep every round's 16-byte GHASH reads live at once).
+__device__ __forceinline__ void pin4(uint4 &v) {
+  asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+}
+
+// GHASH byte-table selector of step T (see g8_load).
+template <int T>
+constexpr uint32_t g8_sel() {
+  return 0x0c0c0000u | ((4u + (T & 3)) << 8) | (T & 3);
+}
+
+// GHASH steps carried by middle round i (rounds 3..NR-1 -> i = 0..NR-4) of
+// the one-block-per-lane kernel: AES-128 has 7 such rounds (3,3,2,2,2,2,2),
+// AES-192/256 spread 2 per round over the first 8.
+template <int NR>
+constexpr int g_steps(int i) {
+  if (NR == 10) return i < 2 ? 3 : 2;
+  return i < 8 ? 2 : 0;
+}
+template <int NR>
+constexpr int g_first(int i) {
+  int t = 0;
+  for (int k = 0; k < i; k++) t += g_steps<NR>(k);
+  return t;
+}
+
+template <int T>
+__device__ __forceinline__ uint32_t gh_word(const Gh8 &h) {
+  return T < 4 ? h.r0 : T < 8 ? h.r1 : T < 12 ? h.r2 : h.r3;
+}
+
+// Middle rounds 3..NR-1 of one state (inline-asm rounds, gcm_rounds.inc),
+// with round i carrying GHASH steps g_first(i) .. +g_steps(i) and, for the
+// next block of the lane, its cached rounds 1 and 2 (software pipelining:
+// the next iteration starts at round 3): round i = 0 issues the round-1
+// lookup of `xs` (its round-0 word 3), round i = 1 the four round-2 lookups.
+template <int I, int NR>
+__device__ __forceinline__ void rounds_s1(uint32_t (&a)[4], const RoundKeys &rk, uint32_t lc0,
+                                          uint32_t lc1, Gh8 &h, const uint32_t (&P)[4],
+                                          uint32_t &xs, const WindowCache &wc, uint32_t k0,
+                                          uint32_t (&nx)[4]) {
+  constexpr int R = I + 3;
+  if constexpr (R < NR) {
+    constexpr int NG = g_steps<NR>(I);
+    constexpr int T = g_first<NR>(I);
+    constexpr int X = I == 0 ? 1 : I == 1 ? 4 : 0;
+    uint32_t xo[X > 0 ? X : 1];
+    if constexpr (NG > 0) {
+      const uint32_t gr[3] = {gh_word<T>(h), gh_word<T + 1>(h),
+                                            gh_word<(NG > 2 ? T + 2 : T)>(h)};
+      const uint32_t gp[3] = {P[T >> 2], P[(T + 1) >> 2],
+                                            P[(NG > 2 ? T + 2 : T) >> 2]};
+      const uint32_t gsel[3] = {g8_sel<T>(), g8_sel<T + 1>(),
+                                              g8_sel<(NG > 2 ? T + 2 : T)>()};
+      v4u gv[NG > 0 ? NG : 1];
+      if constexpr (X == 1 && NG == 3)
+        asm_round_s1_x1_g3(a, rk.w[R], lc0, lc1, gr, gp, gsel, gv, xs, xo);
+      else if constexpr (X == 1 && NG == 2)
+        asm_round_s1_x1_g2(a, rk.w[R], lc0, lc1, gr, gp, gsel, gv, xs, xo);
+      else if constexpr (X == 4 && NG == 3)
+        asm_round_s1_x4_g3(a, rk.w[R], lc0, lc1, gr, gp, gsel, gv, xs, xo);
+      else if constexpr (X == 4 && NG == 2)
+        asm_round_s1_x4_g2(a, rk.w[R], lc0, lc1, gr, gp, gsel, gv, xs, xo);
+      else if constexpr (NG == 3)
+        asm_round_s1_x0_g3(a, rk.w[R], lc0, lc1, gr, gp, gsel, gv);
+      else
+        asm_round_s1_x0_g2(a, rk.w[R], lc0, lc1, gr, gp, gsel, gv);
+      if constexpr (NG == 3)
+        h.g = xor4(xor4_3(h.g, as_uint4(gv[0]), as_uint4(gv[1])), as_uint4(gv[2]));
+      else
+        h.g = xor4_3(h.g, as_uint4(gv[0]), as_uint4(gv[1]));
+      pin4(h.g);
+    } else {
+      if constexpr (X == 1)
+        asm_round_s1_x1_g0(a, rk.w[R], lc0, lc1, xs, xo);
+      else if constexpr (X == 4)
+        asm_round_s1_x4_g0(a, rk.w[R], lc0, lc1, xs, xo);
+      else
+        asm_round_s1_x0_g0(a, rk.w[R], lc0, lc1);
+    }
+    if constexpr (X == 1) {
+      xs = k0 ^ rotl(xo[0], 16);  // round-1 output word 0 of the next block
+    } else if constexpr (X == 4) {
+      // Round-2 output of the next block (WindowCache::rounds12), to nx.
+      xo[0] ^= wc.l0;
+      xo[1] = rotl(xo[1], 16) ^ wc.l1;
+      xo[2] = rotl(xo[2], 16) ^ wc.l2;
+      xo[3] ^= wc.l3;
+    }
+    if constexpr (X == 4) {
+      nx[0] = xo[0];
+      nx[1] = xo[1];
+      nx[2] = xo[2];
+      nx[3] = xo[3];
+    }
+    rounds_s1<I + 1, NR>(a, rk, lc0, lc1, h, P, xs, wc, k0, nx);
+  }
+}
+
+// Rounds R..NR-1 of S = 2 states as inline-asm rounds (gcm_rounds.inc);
+// round index GI (from 1) carries GHASH steps 2*GI, 2*GI+1 of each state's
+// Gh8 while GI < 8.
+template <int S, int GI, int R, int NR>
+__device__ __forceinline__ void rounds_asm(uint32_t (&a)[4], uint32_t (&c)[4], const RoundKeys &rk,
+                                           uint32_t lc0, uint32_t lc1, Gh8 &ha, Gh8 &hc,
+                                           const uint32_t (&P)[4]) {
+  static_assert(S == 2, "two states");
+  if constexpr (R < NR) {
+    if constexpr (GI < 8) {
+      constexpr int T = 2 * GI;
+      const uint32_t gr[4] = {gh_word<T>(ha), gh_word<T + 1>(ha), gh_word<T>(hc),
+                              gh_word<T + 1>(hc)};
+      const uint32_t gp[2] = {P[T >> 2], P[(T + 1) >> 2]};
+      const uint32_t gsel[2] = {g8_sel<T>(), g8_sel<T + 1>()};
+      v4u gv[4];
+      asm_round_s2_x0_g2(a, c, rk.w[R], lc0, lc1, gr, gp, gsel, gv);
+      ha.g = xor4_3(ha.g, as_uint4(gv[0]), as_uint4(gv[1]));
+      hc.g = xor4_3(hc.g, as_uint4(gv[2]), as_uint4(gv[3]));
+      pin4(ha.g);
+      pin4(hc.g);
+    } else {
+      asm_round_s2_x0_g0(a, c, rk.w[R], lc0, lc1);
+    }
+    rounds_asm<S, GI + 1, R + 1, NR>(a, c, rk, lc0, lc1, ha, hc, P);
+  }
 }
 
 template <uint32_t TB, int W>
@@ -507,43 +752,6 @@ __device__ __forceinline__ uint64_t rec_at(const BatchDesc &b, uint64_t i) {
   return b.order ? b.order[i] : i;
 }
 
-// Counter-mode cache of one AES stream (see process_records).
-struct WindowCache {
-  uint32_t win = 0xffffffffu, k1 = 0, k2 = 0, k3 = 0, l0 = 0, l1 = 0, l2 = 0, l3 = 0;
-
-  template <uint32_t T>
-  __device__ __forceinline__ void update(uint32_t ctr, uint32_t s3, uint32_t c0, uint32_t c1,
-                                         uint32_t c2, const RoundKeys &rk,
-                                         const uint8_t *smem, uint32_t lc0, uint32_t lc1) {
-    if ((ctr >> 8) == win) return;
-    win = ctr >> 8;
-    k1 = round_col<T>(smem, lc0, lc1, c1, c2, s3, c0, rk.w[1][1]);
-    k2 = round_col<T>(smem, lc0, lc1, c2, s3, c0, c1, rk.w[1][2]);
-    k3 = round_col<T>(smem, lc0, lc1, s3, c0, c1, c2, rk.w[1][3]);
-    l0 = tload<T>(smem, taddr<1>(lc1, k1)) ^
-         rotl(tload<T>(smem, taddr<2>(lc0, k2)) ^ tload<T>(smem, taddr<3>(lc1, k3)) ^
-                  rk.w[2][0], 16);
-    l1 = tload<T>(smem, taddr<0>(lc0, k1)) ^ tload<T>(smem, taddr<1>(lc1, k2)) ^
-         rotl(tload<T>(smem, taddr<2>(lc0, k3)) ^ rk.w[2][1], 16);
-    l2 = tload<T>(smem, taddr<0>(lc0, k2)) ^ tload<T>(smem, taddr<1>(lc1, k3)) ^
-         rotl(tload<T>(smem, taddr<3>(lc1, k1)) ^ rk.w[2][2], 16);
-    l3 = tload<T>(smem, taddr<0>(lc0, k3)) ^
-         rotl(tload<T>(smem, taddr<2>(lc0, k1)) ^ tload<T>(smem, taddr<3>(lc1, k2)) ^
-                  rk.w[2][3], 16);
-  }
-
-  // Rounds 1 and 2 of a counter block whose round-0 word 3 is s3.
-  template <uint32_t T>
-  __device__ __forceinline__ void rounds12(uint32_t k0, uint32_t s3, uint32_t &u0, uint32_t &u1,
-                                           uint32_t &u2, uint32_t &u3, const uint8_t *smem,
-                                           uint32_t lc0, uint32_t lc1) const {
-    const uint32_t t0 = k0 ^ rotl(tload<T>(smem, taddr<3>(lc1, s3)), 16);
-    u0 = tload<T>(smem, taddr<0>(lc0, t0)) ^ l0;
-    u1 = rotl(tload<T>(smem, taddr<3>(lc1, t0)), 16) ^ l1;
-    u2 = rotl(tload<T>(smem, taddr<2>(lc0, t0)), 16) ^ l2;
-    u3 = tload<T>(smem, taddr<1>(lc1, t0)) ^ l3;
-  }
-};
 
 // Per-record state handed from the prologue to the bulk kernel (64 bytes).
 struct alignas(16) RecState {
@@ -693,7 +901,11 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
                                                 const RecState *__restrict__ st, uint64_t rec,
                                                 bool active, const uint8_t *smem,
                                                 const uint8_t *gtab, uint32_t lc0, uint32_t lc1,
-                                                uint32_t mf0) {
+                                                uint32_t mf0, StampVec &stamps) {
+  (void)stamps;
+#if BSSL_AMD_GCM_STAMPS
+  uint64_t *stv = stamps.v;
+#endif
   const int q = threadIdx.x & 15;
   RecordMeta m = {0, 0, 0, 0};
   RecState s;
@@ -741,31 +953,66 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   // pass orders after the previous store.)
   auto load_full = [&](uint64_t j) {
     uint4 v;
+#if BSSL_AMD_ABLATE == 3 || BSSL_AMD_ABLATE == 4  // diagnostic: no plaintext loads
+    v = make_uint4((uint32_t)j, 1, 2, 3);
+#else
     if (j < nfull) v = *reinterpret_cast<const uint4 *>(src + j * 16);
+#endif
     return v;
   };
-  // One iteration: block j = it*16 + q, plaintext (if full) already in x.
-  // The GHASH multiply of the accumulator (acc * H^16, its input known from
-  // the previous iteration) is interleaved with this block's AES rounds.
-  auto step = [&](int it, uint4 x) {
-    const uint64_t j = (uint64_t)it * 16 + q;
-    const uint32_t ctr = ctr0 + 1u + (uint32_t)j;  // inc32 wraps mod 2^32
+  // One iteration: block j = it*16 + q, plaintext (if full) already in x,
+  // its AES state after the cached rounds 1-2 in `cur` (computed during the
+  // previous iteration).  The GHASH multiply of the accumulator (acc * H^16,
+  // its input known from the previous iteration) and rounds 1-2 of the next
+  // block j + 16 are interleaved with this block's rounds 3..NR.
+  uint32_t cur[4];
+  {
+    const uint32_t ctr = ctr0 + 1u + (uint32_t)q;
     const uint32_t s3 = bswap32(ctr) ^ rk.w[0][3];
     wc.update<T>(ctr, s3, c0, c1, c2, rk, smem, lc0, lc1);
+    wc.rounds12<T>(k0, s3, cur[0], cur[1], cur[2], cur[3], smem, lc0, lc1);
+  }
+  auto step = [&](int it, uint4 x) {
+    const uint64_t j = (uint64_t)it * 16 + q;
+    const uint32_t ctrn = ctr0 + 1u + (uint32_t)(j + 16);  // next block, inc32 mod 2^32
+    uint32_t xs = bswap32(ctrn) ^ rk.w[0][3];
+    wc.update<T>(ctrn, xs, c0, c1, c2, rk, smem, lc0, lc1);
     Gh8 h;
     g8_rotate(h, acc, rs1, rs2, rbs);
-    uint32_t a0, a1, a2, a3;
-    {
-      const uint4 v0 = g8_load<0>(h, P, smem), v1 = g8_load<1>(h, P, smem);
-      wc.rounds12<T>(k0, s3, a0, a1, a2, a3, smem, lc0, lc1);
-      h.g = xor4(v0, v1);
-    }
-    // Rounds 3..NR-1 carry GHASH steps 2..15 (NR - 3 >= 7 rounds).
-    aes_rounds_g_from<1, 3, NR, T>(a0, a1, a2, a3, rk, smem, lc0, lc1, h, P);
-    const uint4 ks = aes_rounds<NR, T, NR>(a0, a1, a2, a3, rk, smem, lc0, lc1);
+    h.g = make_uint4(0, 0, 0, 0);
+    uint32_t sa[4] = {cur[0], cur[1], cur[2], cur[3]};
+#if BSSL_AMD_ABLATE == 2 || BSSL_AMD_ABLATE == 5  // diagnostic: no AES rounds 3..NR
+    wc.rounds12<T>(k0, xs, cur[0], cur[1], cur[2], cur[3], smem, lc0, lc1);
+#if BSSL_AMD_ABLATE == 2  // (GHASH steps kept)
+    h.g = xor4_3(h.g, g8_load<0>(h, P, smem), g8_load<1>(h, P, smem));
+    h.g = xor4_3(h.g, g8_load<2>(h, P, smem), g8_load<3>(h, P, smem));
+    h.g = xor4_3(h.g, g8_load<4>(h, P, smem), g8_load<5>(h, P, smem));
+    h.g = xor4_3(h.g, g8_load<6>(h, P, smem), g8_load<7>(h, P, smem));
+    h.g = xor4_3(h.g, g8_load<8>(h, P, smem), g8_load<9>(h, P, smem));
+    h.g = xor4_3(h.g, g8_load<10>(h, P, smem), g8_load<11>(h, P, smem));
+    h.g = xor4_3(h.g, g8_load<12>(h, P, smem), g8_load<13>(h, P, smem));
+    h.g = xor4_3(h.g, g8_load<14>(h, P, smem), g8_load<15>(h, P, smem));
+#endif
+#else
+#if BSSL_AMD_GCM_STAMPS
+    const uint64_t st0 = stamp();
+#endif
+    rounds_s1<0, NR>(sa, rk, lc0, lc1, h, P, xs, wc, k0, cur);
+    asm_last_s1(sa, rk.w[NR], lc0);
+#if BSSL_AMD_GCM_STAMPS
+    g_stamp_rounds += stamp() - st0;
+    g_stamp_iters++;
+#endif
+#endif
+    const uint4 ks = make_uint4(sa[0], sa[1], sa[2], sa[3]);
     uint4 y = xor4(x, ks);
+#if BSSL_AMD_ABLATE == 4 || BSSL_AMD_ABLATE == 6  // diagnostic: no stores
+    if (j < nfull) {
+      asm volatile("" ::"v"(y.x), "v"(y.y), "v"(y.z), "v"(y.w));
+#else
     if (j < nfull) {
       *reinterpret_cast<uint4 *>(dst + j * 16) = y;
+#endif
     } else if (j < nb) {
       const uint32_t n = (uint32_t)min<uint64_t>(m.len - j * 16, 16);
       x = load_partial(src + j * 16, n);
@@ -785,6 +1032,24 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   // for iteration it+1 is issued before iteration it's store, so waiting for
   // it never waits for a store (vmcnt counts loads and stores in issue order)
   // and its latency hides under a whole iteration of AES + GHASH.
+#if BSSL_AMD_GCM_STAMPS
+  const uint64_t sl0 = stamp();
+#endif
+#if BSSL_AMD_GCM_PREFETCH == 2
+  // Two iterations ahead (three buffers).
+  uint4 x0 = load_full(q), x1 = load_full(16 + q);
+  int it = 0;
+  for (; it + 2 < iters; it += 3) {
+    const uint4 x2 = load_full((uint64_t)(it + 2) * 16 + q);
+    step(it, x0);
+    x0 = load_full((uint64_t)(it + 3) * 16 + q);
+    step(it + 1, x1);
+    x1 = load_full((uint64_t)(it + 4) * 16 + q);
+    step(it + 2, x2);
+  }
+  if (it < iters) step(it, x0);
+  if (it + 1 < iters) step(it + 1, x1);
+#else
   uint4 x0 = load_full(q);
   int it = 0;
   for (; it + 1 < iters; it += 2) {
@@ -794,13 +1059,129 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     step(it + 1, x1);
   }
   if (it < iters) step(it, x0);
+#endif
+#if BSSL_AMD_GCM_STAMPS
+  g_stamp_loop += stamp() - sl0;
+#endif
   finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, gtab, mf0);
 }
 
+// Two blocks per lane (S = 2): iteration `it` covers the record's blocks
+// 32*it .. 32*it+31; lane q encrypts jA = 32*it + q and jB = jA + 16.  GHASH
+// runs as 32 virtual lanes (u = j mod 32; lane q holds u = q in accA and
+// u = q + 16 in accB) with Horner multiplier H^32 (byte table of H^32 in LDS).
+// At the end virtual lanes u and u+16 are merged into one 16-lane
+// accumulator: with M = nb + 1 GHASH elements, lane u's weight is
+// H^((M-2-u) mod 32), so the heavier one is multiplied by H^16 and the sum
+// carries weight H^((M-2-q) mod 16) -- exactly finish_record<16>'s algebra.
 template <int NR, bool OPEN>
+__device__ __forceinline__ void process_records2(const RoundKeys &rk, const BatchDesc &b,
+                                                 const RecState *__restrict__ st, uint64_t rec,
+                                                 bool active, const uint8_t *smem,
+                                                 const uint8_t *gtab, uint32_t lc0, uint32_t lc1,
+                                                 uint32_t mf0) {
+  const int q = threadIdx.x & 15;
+  RecordMeta m = {0, 0, 0, 0};
+  RecState s;
+  s.j0 = s.ek0 = s.ya = make_uint4(0, 0, 0, 0);
+  s.live = 0;
+  if (active) {
+    m = record_meta(b, rec);
+    s = st[rec];
+  }
+  const bool live = active && s.live;
+  const uint64_t nb = live ? (m.len + 15) / 16 : 0;
+  const uint32_t ctr0 = bswap32(s.j0.w);
+  const uint32_t c0 = s.j0.x ^ rk.w[0][0], c1 = s.j0.y ^ rk.w[0][1], c2 = s.j0.z ^ rk.w[0][2];
+  const uint8_t *src = b.in + m.off;
+  uint8_t *dst = b.out + m.off;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(src) |
+                         reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+  uint4 accA = make_uint4(0, 0, 0, 0);
+  uint4 accB = (q == 15 && live) ? s.ya : make_uint4(0, 0, 0, 0);
+  const bool rs1 = (q >> 2) & 1, rs2 = (q >> 3) & 1;
+  const uint32_t rbs = (uint32_t)q & 3u;
+  uint32_t P[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) v |= (uint32_t)(((4 * k + i + q) & 15) << 4) << (8 * i);
+    P[k] = v;
+  }
+  constexpr uint32_t T = 0;  // the table base (kLdsAes) rides in lc0/lc1
+  const uint32_t k0 = tload<T>(smem, taddr<0>(lc0, c0)) ^ tload<T>(smem, taddr<1>(lc1, c1)) ^
+                      rotl(tload<T>(smem, taddr<2>(lc0, c2)) ^ rk.w[1][0], 16);
+  WindowCache wa, wb;
+  const int iters = wave_max((int)((nb + 31) / 32));
+  const uint64_t nfull = aligned ? m.len / 16 : 0;
+  auto load_full = [&](uint64_t j) {
+    uint4 v;
+    if (j < nfull) v = *reinterpret_cast<const uint4 *>(src + j * 16);
+    return v;
+  };
+  // Output and hash update of one block (ks = its keystream).
+  auto finish_block = [&](uint64_t j, uint4 x, uint4 ks, uint4 g, uint4 &acc) {
+    uint4 y = xor4(x, ks);
+    if (j < nfull) {
+      *reinterpret_cast<uint4 *>(dst + j * 16) = y;
+    } else if (j < nb) {
+      const uint32_t n = (uint32_t)min<uint64_t>(m.len - j * 16, 16);
+      x = load_partial(src + j * 16, n);
+      y = mask_block(xor4(x, ks), n);
+      store_partial(dst + j * 16, y, n);
+    }
+    if (j < nb) acc = xor4(g, OPEN ? x : y);
+  };
+  auto step = [&](int it, uint4 xa, uint4 xb) {
+    const uint64_t ja = (uint64_t)it * 32 + q, jb = ja + 16;
+    const uint32_t ctra = ctr0 + 1u + (uint32_t)ja, ctrb = ctra + 16u;  // inc32 mod 2^32
+    const uint32_t s3a = bswap32(ctra) ^ rk.w[0][3], s3b = bswap32(ctrb) ^ rk.w[0][3];
+    wa.update<T>(ctra, s3a, c0, c1, c2, rk, smem, lc0, lc1);
+    wb.update<T>(ctrb, s3b, c0, c1, c2, rk, smem, lc0, lc1);
+    Gh8 ha, hb;
+    g8_rotate(ha, accA, rs1, rs2, rbs);
+    g8_rotate(hb, accB, rs1, rs2, rbs);
+    uint32_t sa[4], sb[4];
+    {
+      const uint4 va0 = g8_load<0>(ha, P, smem), va1 = g8_load<1>(ha, P, smem);
+      const uint4 vb0 = g8_load<0>(hb, P, smem), vb1 = g8_load<1>(hb, P, smem);
+      wa.rounds12<T>(k0, s3a, sa[0], sa[1], sa[2], sa[3], smem, lc0, lc1);
+      wb.rounds12<T>(k0, s3b, sb[0], sb[1], sb[2], sb[3], smem, lc0, lc1);
+      ha.g = xor4(va0, va1);
+      hb.g = xor4(vb0, vb1);
+    }
+    rounds_asm<2, 1, 3, NR>(sa, sb, rk, lc0, lc1, ha, hb, P);
+    asm_last_s2(sa, sb, rk.w[NR], lc0);
+    const uint4 ksa = make_uint4(sa[0], sa[1], sa[2], sa[3]);
+    const uint4 ksb = make_uint4(sb[0], sb[1], sb[2], sb[3]);
+    finish_block(ja, xa, ksa, ha.g, accA);
+    finish_block(jb, xb, ksb, hb.g, accB);
+  };
+  // Plaintext one iteration ahead (see process_records).
+  uint4 xa0 = load_full(q), xb0 = load_full(q + 16);
+  int it = 0;
+  for (; it + 1 < iters; it += 2) {
+    const uint4 xa1 = load_full((uint64_t)(it + 1) * 32 + q),
+                xb1 = load_full((uint64_t)(it + 1) * 32 + 16 + q);
+    step(it, xa0, xb0);
+    xa0 = load_full((uint64_t)(it + 2) * 32 + q);
+    xb0 = load_full((uint64_t)(it + 2) * 32 + 16 + q);
+    step(it + 1, xa1, xb1);
+  }
+  if (it < iters) step(it, xa0, xb0);
+  // Merge virtual lanes q and q+16 (weights H^wa, H^(wa+-16)).
+  const uint32_t wA = (uint32_t)((nb + 1 + 62 - (uint64_t)q) & 31);  // (M-2-q) mod 32
+  const uint4 heavy = wA >= 16 ? accA : accB, light = wA >= 16 ? accB : accA;
+  const uint4 acc = xor4(gmul<0>(heavy, gtab + 4 * 8192, mf0), light);
+  finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, gtab, mf0);
+}
+
+template <int NR, bool OPEN, int S>
 __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restrict__ keys,
                                                       BatchDesc b,
-                                                      const RecState *__restrict__ st) {
+                                                      const RecState *__restrict__ st,
+                                                      uint32_t *__restrict__ units) {
   static_assert(kRecPerTile <= 64, "one wave plans a tile with ballots");
   __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
   // Pass list of the current tile: key and 64-bit record mask per pass.
@@ -824,7 +1205,50 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
   const uint32_t mf0 = 0xf0u;
 
   uint32_t loaded = 0xffffffffu;
+  StampVec stamps = {{0, 0, 0}};
   const uint64_t n = b.num_records;
+  if (!b.key_index) {
+    // One key for the whole batch: no tiles or passes.  Each wave takes the
+    // next unit of kRecPerWave records (in processing order) from a
+    // grid-wide counter, so waves that the SIMD arbiter favours (older
+    // waves issue first) simply process more units instead of waiting at a
+    // per-tile barrier for the slowest wave.
+    const uint4 *t16 = reinterpret_cast<const uint4 *>(keys[0].htab[3 + S]);
+    for (uint32_t e = tid; e < 4096; e += kThreads) {
+      const uint32_t ev = e >> 4, p = e & 15;
+      reinterpret_cast<uint4 *>(smem + kLdsG8)[e] =
+          xor4(t16[(2 * p) * 16 + (ev >> 4)], t16[(2 * p + 1) * 16 + (ev & 15)]);
+    }
+    __syncthreads();
+    RoundKeys rk;
+#pragma unroll
+    for (int r = 0; r <= NR; r++)
+#pragma unroll
+      for (int c = 0; c < 4; c++) rk.w[r][c] = keys[0].rk[r][c];
+    const uint8_t *gtab = reinterpret_cast<const uint8_t *>(keys[0].htab);
+    for (;;) {
+      uint32_t u = 0;
+      if (lane == 0) u = atomicAdd(units, 1u);
+      u = __builtin_amdgcn_readfirstlane(__shfl(u, 0, 64));
+      const uint64_t first = (uint64_t)u * kRecPerWave;
+      if (first >= n) break;
+      const uint64_t i = first + g;
+      const bool active = i < n;
+      if constexpr (S == 2)
+        process_records2<NR, OPEN>(rk, b, st, active ? rec_at(b, i) : 0, active, smem, gtab, lc0,
+                                   lc1, mf0);
+      else
+        process_records<NR, OPEN>(rk, b, st, active ? rec_at(b, i) : 0, active, smem, gtab, lc0,
+                                  lc1, mf0, stamps);
+    }
+#if BSSL_AMD_GCM_STAMPS
+    if (blockIdx.x < 2 && (tid & 63) == 0)
+      printf("stamps block %d wave %d: iters %llu  cycles/iter %.0f  rounds3..NR/iter %.0f\n",
+             (int)blockIdx.x, wave, (unsigned long long)stamps.v[1],
+             (double)stamps.v[2] / (double)stamps.v[1], (double)stamps.v[0] / (double)stamps.v[1]);
+#endif
+    return;
+  }
   for (uint64_t base = (uint64_t)blockIdx.x * kRecPerTile; base < n;
        base += (uint64_t)gridDim.x * kRecPerTile) {
     __syncthreads();
@@ -856,9 +1280,9 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
       const uint8_t *gtab = reinterpret_cast<const uint8_t *>(keys[k].htab);
       if (k != loaded) {
         __syncthreads();
-        // Byte table of H^16 from the key's nibble tables (power 4): entry
-        // (e, p) = T[2p][e >> 4] ^ T[2p+1][e & 15] (key_setup.cc layout).
-        const uint4 *t16 = reinterpret_cast<const uint4 *>(keys[k].htab[4]);
+        // Byte table of H^(16 S) from the key's nibble tables (power 3+S):
+        // entry (e, p) = T[2p][e >> 4] ^ T[2p+1][e & 15] (key_setup.cc layout).
+        const uint4 *t16 = reinterpret_cast<const uint4 *>(keys[k].htab[3 + S]);
         for (uint32_t e = tid; e < 4096; e += kThreads) {
           const uint32_t ev = e >> 4, p = e & 15;
           reinterpret_cast<uint4 *>(smem + kLdsG8)[e] =
@@ -874,10 +1298,20 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
         for (int c = 0; c < 4; c++) rk.w[r][c] = keys[k].rk[r][c];
       const int t = wave * kRecPerWave + g;
       const bool active = (mask >> t) & 1;
-      process_records<NR, OPEN>(rk, b, st, active ? rec_at(b, base + t) : 0, active, smem, gtab,
-                                lc0, lc1, mf0);
+      if constexpr (S == 2)
+        process_records2<NR, OPEN>(rk, b, st, active ? rec_at(b, base + t) : 0, active, smem,
+                                   gtab, lc0, lc1, mf0);
+      else
+        process_records<NR, OPEN>(rk, b, st, active ? rec_at(b, base + t) : 0, active, smem,
+                                  gtab, lc0, lc1, mf0, stamps);
     }
   }
+#if BSSL_AMD_GCM_STAMPS
+  if (blockIdx.x < 2 && (tid & 63) == 0)
+    printf("stamps block %d wave %d: iters %llu  cycles/iter %.0f  rounds3..NR/iter %.0f\n",
+           (int)blockIdx.x, wave, (unsigned long long)stamps.v[1],
+           (double)stamps.v[2] / (double)stamps.v[1], (double)stamps.v[0] / (double)stamps.v[1]);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1151,6 +1585,14 @@ int bs_lanes(const BatchDesc &b) {
   return nb >= 1024 ? 32 : 0;
 }
 
+// Blocks per lane of the T-table kernel: 1 by default (two blocks per lane
+// measured slower); BSSL_AMD_GCM_S=2 selects the
+// two-block kernel (tuning).
+int gcm_blocks_per_lane(const BatchDesc &) {
+  const char *e = getenv("BSSL_AMD_GCM_S");
+  return (e && atoi(e) == 2) ? 2 : 1;
+}
+
 template <int NR, bool OPEN>
 int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const KernelEvents *ev) {
   if (!g_num_cus) {
@@ -1160,10 +1602,17 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
         hipSuccess)
       return 1;
   }
+  // Per-record state plus one extra entry whose first word is the unit
+  // counter of gcm_kernel's one-key mode.
   RecState *st = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void **>(&st), b.num_records * sizeof(RecState), s) !=
+  if (hipMallocAsync(reinterpret_cast<void **>(&st), (b.num_records + 1) * sizeof(RecState), s) !=
       hipSuccess)
     return 2;
+  uint32_t *units = reinterpret_cast<uint32_t *>(st + b.num_records);
+  if (hipMemsetAsync(units, 0, sizeof(RecState), s) != hipSuccess) {
+    hipFreeAsync(st, s);
+    return 2;
+  }
   const uint64_t pblocks = (b.num_records + 255) / 256;
   hipLaunchKernelGGL((gcm_prologue<NR>), dim3((unsigned)pblocks), dim3(256), 0, s, keys, b, st);
   BatchDesc bo = b;  // with the processing order of a ragged batch
@@ -1193,8 +1642,12 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
   } else {
     const uint64_t tiles = (b.num_records + kRecPerTile - 1) / kRecPerTile;
     const unsigned grid = (unsigned)(tiles < (uint64_t)g_num_cus ? tiles : (uint64_t)g_num_cus);
-    hipLaunchKernelGGL((gcm_kernel<NR, OPEN>), dim3(grid), dim3(kThreads), 0, s, keys, bo,
-                       (const RecState *)st);
+    if (gcm_blocks_per_lane(b) == 2)
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, 2>), dim3(grid), dim3(kThreads), 0, s, keys, bo,
+                         (const RecState *)st, units);
+    else
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, 1>), dim3(grid), dim3(kThreads), 0, s, keys, bo,
+                         (const RecState *)st, units);
   }
   int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
