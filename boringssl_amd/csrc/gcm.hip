@@ -61,7 +61,7 @@ namespace {
 #define BSSL_AMD_GCM_PREFETCH 1
 #endif
 #ifndef BSSL_AMD_GCM_WAVES
-#define BSSL_AMD_GCM_WAVES 12
+#define BSSL_AMD_GCM_WAVES 16
 #endif
 constexpr int kWaves = BSSL_AMD_GCM_WAVES;
 #ifndef BSSL_AMD_GCM_STAMPS
@@ -330,96 +330,6 @@ __device__ __forceinline__ uint4 g8_load(const Gh8 &h, const uint32_t (&P)[4],
   return *reinterpret_cast<const uint4 *>(smem + kLdsG8 + a);
 }
 
-// One AES round (as aes_round) with GHASH steps 2*GI, 2*GI+1 issued alongside
-// (GI < 8), so the wave keeps 16 x 4-byte + 2 x 16-byte reads in flight.
-template <uint32_t TB, int GI>
-__device__ __forceinline__ void aes_round_g(uint32_t &s0, uint32_t &s1, uint32_t &s2,
-                                            uint32_t &s3, const uint32_t *rkx,
-                                            const uint8_t *smem, uint32_t lc0, uint32_t lc1,
-                                            Gh8 &h, const uint32_t (&P)[4]) {
-  uint4 v0, v1;
-  if constexpr (GI < 8) {
-    v0 = g8_load<2 * GI>(h, P, smem);
-    v1 = g8_load<2 * GI + 1>(h, P, smem);
-  }
-  const uint32_t x00 = tload<TB>(smem, taddr<0>(lc0, s0)), x01 = tload<TB>(smem, taddr<1>(lc1, s1)),
-                 x02 = tload<TB>(smem, taddr<2>(lc0, s2)), x03 = tload<TB>(smem, taddr<3>(lc1, s3));
-  const uint32_t x10 = tload<TB>(smem, taddr<0>(lc0, s1)), x11 = tload<TB>(smem, taddr<1>(lc1, s2)),
-                 x12 = tload<TB>(smem, taddr<2>(lc0, s3)), x13 = tload<TB>(smem, taddr<3>(lc1, s0));
-  const uint32_t x20 = tload<TB>(smem, taddr<0>(lc0, s2)), x21 = tload<TB>(smem, taddr<1>(lc1, s3)),
-                 x22 = tload<TB>(smem, taddr<2>(lc0, s0)), x23 = tload<TB>(smem, taddr<3>(lc1, s1));
-  const uint32_t x30 = tload<TB>(smem, taddr<0>(lc0, s3)), x31 = tload<TB>(smem, taddr<1>(lc1, s0)),
-                 x32 = tload<TB>(smem, taddr<2>(lc0, s1)), x33 = tload<TB>(smem, taddr<3>(lc1, s2));
-  s0 = xor3(x00, x01, rotl(xor3(x02, x03, rkx[0]), 16));
-  s1 = xor3(x10, x11, rotl(xor3(x12, x13, rkx[1]), 16));
-  s2 = xor3(x20, x21, rotl(xor3(x22, x23, rkx[2]), 16));
-  s3 = xor3(x30, x31, rotl(xor3(x32, x33, rkx[3]), 16));
-  if constexpr (GI < 8) h.g = xor4_3(h.g, v0, v1);
-}
-
-// Two blocks per lane (S = 2): one round of both AES states with GHASH steps
-// 2*GI, 2*GI+1 of both accumulators (GI < 8): 32 x 4-byte + 4 x 16-byte reads
-// in flight per wave.
-template <uint32_t TB, int GI>
-__device__ __forceinline__ void aes_round2_g(uint32_t (&a)[4], uint32_t (&c)[4],
-                                             const uint32_t *rkx, const uint8_t *smem,
-                                             uint32_t lc0, uint32_t lc1, Gh8 &ha, Gh8 &hc,
-                                             const uint32_t (&P)[4]) {
-  uint4 va0, va1, vc0, vc1;
-  if constexpr (GI < 8) {
-    va0 = g8_load<2 * GI>(ha, P, smem);
-    va1 = g8_load<2 * GI + 1>(ha, P, smem);
-    vc0 = g8_load<2 * GI>(hc, P, smem);
-    vc1 = g8_load<2 * GI + 1>(hc, P, smem);
-  }
-  uint32_t x[2][4][4];
-#pragma unroll
-  for (int i = 0; i < 2; i++) {
-    const uint32_t(&s)[4] = i ? c : a;
-#pragma unroll
-    for (int col = 0; col < 4; col++) {
-      x[i][col][0] = tload<TB>(smem, taddr<0>(lc0, s[col]));
-      x[i][col][1] = tload<TB>(smem, taddr<1>(lc1, s[(col + 1) & 3]));
-      x[i][col][2] = tload<TB>(smem, taddr<2>(lc0, s[(col + 2) & 3]));
-      x[i][col][3] = tload<TB>(smem, taddr<3>(lc1, s[(col + 3) & 3]));
-    }
-  }
-#pragma unroll
-  for (int col = 0; col < 4; col++) {
-    a[col] = xor3(x[0][col][0], x[0][col][1], rotl(xor3(x[0][col][2], x[0][col][3], rkx[col]), 16));
-    c[col] = xor3(x[1][col][0], x[1][col][1], rotl(xor3(x[1][col][2], x[1][col][3], rkx[col]), 16));
-  }
-  if constexpr (GI < 8) {
-    ha.g = xor4_3(ha.g, va0, va1);
-    hc.g = xor4_3(hc.g, vc0, vc1);
-  }
-  // Keep the scheduler from hoisting the next round's work into this one
-  // (it otherwise runs out of registers at 3 waves per SIMD).
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int GI, int R, int NR, uint32_t TB>
-__device__ __forceinline__ void aes_rounds2_g_from(uint32_t (&a)[4], uint32_t (&c)[4],
-                                                   const RoundKeys &rk, const uint8_t *smem,
-                                                   uint32_t lc0, uint32_t lc1, Gh8 &ha, Gh8 &hc,
-                                                   const uint32_t (&P)[4]) {
-  if constexpr (R < NR) {
-    aes_round2_g<TB, GI>(a, c, rk.w[R], smem, lc0, lc1, ha, hc, P);
-    aes_rounds2_g_from<GI + 1, R + 1, NR, TB>(a, c, rk, smem, lc0, lc1, ha, hc, P);
-  }
-}
-
-template <int GI, int R, int NR, uint32_t TB>
-__device__ __forceinline__ void aes_rounds_g_from(uint32_t &s0, uint32_t &s1, uint32_t &s2,
-                                                  uint32_t &s3, const RoundKeys &rk,
-                                                  const uint8_t *smem, uint32_t lc0, uint32_t lc1,
-                                                  Gh8 &h, const uint32_t (&P)[4]) {
-  if constexpr (R < NR) {
-    aes_round_g<TB, GI>(s0, s1, s2, s3, rk.w[R], smem, lc0, lc1, h, P);
-    aes_rounds_g_from<GI + 1, R + 1, NR, TB>(s0, s1, s2, s3, rk, smem, lc0, lc1, h, P);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // GHASH: x * H^(2^p); the tables of power p start at byte TB of `tab`
 // (LDS in the main kernel, global memory in the prologue).
@@ -614,34 +524,6 @@ __device__ __forceinline__ void rounds_s1(uint32_t (&a)[4], const RoundKeys &rk,
       nx[3] = xo[3];
     }
     rounds_s1<I + 1, NR>(a, rk, lc0, lc1, h, P, xs, wc, k0, nx);
-  }
-}
-
-// Rounds R..NR-1 of S = 2 states as inline-asm rounds (gcm_rounds.inc);
-// round index GI (from 1) carries GHASH steps 2*GI, 2*GI+1 of each state's
-// Gh8 while GI < 8.
-template <int S, int GI, int R, int NR>
-__device__ __forceinline__ void rounds_asm(uint32_t (&a)[4], uint32_t (&c)[4], const RoundKeys &rk,
-                                           uint32_t lc0, uint32_t lc1, Gh8 &ha, Gh8 &hc,
-                                           const uint32_t (&P)[4]) {
-  static_assert(S == 2, "two states");
-  if constexpr (R < NR) {
-    if constexpr (GI < 8) {
-      constexpr int T = 2 * GI;
-      const uint32_t gr[4] = {gh_word<T>(ha), gh_word<T + 1>(ha), gh_word<T>(hc),
-                              gh_word<T + 1>(hc)};
-      const uint32_t gp[2] = {P[T >> 2], P[(T + 1) >> 2]};
-      const uint32_t gsel[2] = {g8_sel<T>(), g8_sel<T + 1>()};
-      v4u gv[4];
-      asm_round_s2_x0_g2(a, c, rk.w[R], lc0, lc1, gr, gp, gsel, gv);
-      ha.g = xor4_3(ha.g, as_uint4(gv[0]), as_uint4(gv[1]));
-      hc.g = xor4_3(hc.g, as_uint4(gv[2]), as_uint4(gv[3]));
-      pin4(ha.g);
-      pin4(hc.g);
-    } else {
-      asm_round_s2_x0_g0(a, c, rk.w[R], lc0, lc1);
-    }
-    rounds_asm<S, GI + 1, R + 1, NR>(a, c, rk, lc0, lc1, ha, hc, P);
   }
 }
 
@@ -1066,118 +948,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, gtab, mf0);
 }
 
-// Two blocks per lane (S = 2): iteration `it` covers the record's blocks
-// 32*it .. 32*it+31; lane q encrypts jA = 32*it + q and jB = jA + 16.  GHASH
-// runs as 32 virtual lanes (u = j mod 32; lane q holds u = q in accA and
-// u = q + 16 in accB) with Horner multiplier H^32 (byte table of H^32 in LDS).
-// At the end virtual lanes u and u+16 are merged into one 16-lane
-// accumulator: with M = nb + 1 GHASH elements, lane u's weight is
-// H^((M-2-u) mod 32), so the heavier one is multiplied by H^16 and the sum
-// carries weight H^((M-2-q) mod 16) -- exactly finish_record<16>'s algebra.
 template <int NR, bool OPEN>
-__device__ __forceinline__ void process_records2(const RoundKeys &rk, const BatchDesc &b,
-                                                 const RecState *__restrict__ st, uint64_t rec,
-                                                 bool active, const uint8_t *smem,
-                                                 const uint8_t *gtab, uint32_t lc0, uint32_t lc1,
-                                                 uint32_t mf0) {
-  const int q = threadIdx.x & 15;
-  RecordMeta m = {0, 0, 0, 0};
-  RecState s;
-  s.j0 = s.ek0 = s.ya = make_uint4(0, 0, 0, 0);
-  s.live = 0;
-  if (active) {
-    m = record_meta(b, rec);
-    s = st[rec];
-  }
-  const bool live = active && s.live;
-  const uint64_t nb = live ? (m.len + 15) / 16 : 0;
-  const uint32_t ctr0 = bswap32(s.j0.w);
-  const uint32_t c0 = s.j0.x ^ rk.w[0][0], c1 = s.j0.y ^ rk.w[0][1], c2 = s.j0.z ^ rk.w[0][2];
-  const uint8_t *src = b.in + m.off;
-  uint8_t *dst = b.out + m.off;
-  const bool aligned = ((reinterpret_cast<uintptr_t>(src) |
-                         reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
-  uint4 accA = make_uint4(0, 0, 0, 0);
-  uint4 accB = (q == 15 && live) ? s.ya : make_uint4(0, 0, 0, 0);
-  const bool rs1 = (q >> 2) & 1, rs2 = (q >> 3) & 1;
-  const uint32_t rbs = (uint32_t)q & 3u;
-  uint32_t P[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) v |= (uint32_t)(((4 * k + i + q) & 15) << 4) << (8 * i);
-    P[k] = v;
-  }
-  constexpr uint32_t T = 0;  // the table base (kLdsAes) rides in lc0/lc1
-  const uint32_t k0 = tload<T>(smem, taddr<0>(lc0, c0)) ^ tload<T>(smem, taddr<1>(lc1, c1)) ^
-                      rotl(tload<T>(smem, taddr<2>(lc0, c2)) ^ rk.w[1][0], 16);
-  WindowCache wa, wb;
-  const int iters = wave_max((int)((nb + 31) / 32));
-  const uint64_t nfull = aligned ? m.len / 16 : 0;
-  auto load_full = [&](uint64_t j) {
-    uint4 v;
-    if (j < nfull) v = *reinterpret_cast<const uint4 *>(src + j * 16);
-    return v;
-  };
-  // Output and hash update of one block (ks = its keystream).
-  auto finish_block = [&](uint64_t j, uint4 x, uint4 ks, uint4 g, uint4 &acc) {
-    uint4 y = xor4(x, ks);
-    if (j < nfull) {
-      *reinterpret_cast<uint4 *>(dst + j * 16) = y;
-    } else if (j < nb) {
-      const uint32_t n = (uint32_t)min<uint64_t>(m.len - j * 16, 16);
-      x = load_partial(src + j * 16, n);
-      y = mask_block(xor4(x, ks), n);
-      store_partial(dst + j * 16, y, n);
-    }
-    if (j < nb) acc = xor4(g, OPEN ? x : y);
-  };
-  auto step = [&](int it, uint4 xa, uint4 xb) {
-    const uint64_t ja = (uint64_t)it * 32 + q, jb = ja + 16;
-    const uint32_t ctra = ctr0 + 1u + (uint32_t)ja, ctrb = ctra + 16u;  // inc32 mod 2^32
-    const uint32_t s3a = bswap32(ctra) ^ rk.w[0][3], s3b = bswap32(ctrb) ^ rk.w[0][3];
-    wa.update<T>(ctra, s3a, c0, c1, c2, rk, smem, lc0, lc1);
-    wb.update<T>(ctrb, s3b, c0, c1, c2, rk, smem, lc0, lc1);
-    Gh8 ha, hb;
-    g8_rotate(ha, accA, rs1, rs2, rbs);
-    g8_rotate(hb, accB, rs1, rs2, rbs);
-    uint32_t sa[4], sb[4];
-    {
-      const uint4 va0 = g8_load<0>(ha, P, smem), va1 = g8_load<1>(ha, P, smem);
-      const uint4 vb0 = g8_load<0>(hb, P, smem), vb1 = g8_load<1>(hb, P, smem);
-      wa.rounds12<T>(k0, s3a, sa[0], sa[1], sa[2], sa[3], smem, lc0, lc1);
-      wb.rounds12<T>(k0, s3b, sb[0], sb[1], sb[2], sb[3], smem, lc0, lc1);
-      ha.g = xor4(va0, va1);
-      hb.g = xor4(vb0, vb1);
-    }
-    rounds_asm<2, 1, 3, NR>(sa, sb, rk, lc0, lc1, ha, hb, P);
-    asm_last_s2(sa, sb, rk.w[NR], lc0);
-    const uint4 ksa = make_uint4(sa[0], sa[1], sa[2], sa[3]);
-    const uint4 ksb = make_uint4(sb[0], sb[1], sb[2], sb[3]);
-    finish_block(ja, xa, ksa, ha.g, accA);
-    finish_block(jb, xb, ksb, hb.g, accB);
-  };
-  // Plaintext one iteration ahead (see process_records).
-  uint4 xa0 = load_full(q), xb0 = load_full(q + 16);
-  int it = 0;
-  for (; it + 1 < iters; it += 2) {
-    const uint4 xa1 = load_full((uint64_t)(it + 1) * 32 + q),
-                xb1 = load_full((uint64_t)(it + 1) * 32 + 16 + q);
-    step(it, xa0, xb0);
-    xa0 = load_full((uint64_t)(it + 2) * 32 + q);
-    xb0 = load_full((uint64_t)(it + 2) * 32 + 16 + q);
-    step(it + 1, xa1, xb1);
-  }
-  if (it < iters) step(it, xa0, xb0);
-  // Merge virtual lanes q and q+16 (weights H^wa, H^(wa+-16)).
-  const uint32_t wA = (uint32_t)((nb + 1 + 62 - (uint64_t)q) & 31);  // (M-2-q) mod 32
-  const uint4 heavy = wA >= 16 ? accA : accB, light = wA >= 16 ? accB : accA;
-  const uint4 acc = xor4(gmul<0>(heavy, gtab + 4 * 8192, mf0), light);
-  finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, gtab, mf0);
-}
-
-template <int NR, bool OPEN, int S>
 __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restrict__ keys,
                                                       BatchDesc b,
                                                       const RecState *__restrict__ st,
@@ -1213,7 +984,7 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
     // grid-wide counter, so waves that the SIMD arbiter favours (older
     // waves issue first) simply process more units instead of waiting at a
     // per-tile barrier for the slowest wave.
-    const uint4 *t16 = reinterpret_cast<const uint4 *>(keys[0].htab[3 + S]);
+    const uint4 *t16 = reinterpret_cast<const uint4 *>(keys[0].htab[4]);
     for (uint32_t e = tid; e < 4096; e += kThreads) {
       const uint32_t ev = e >> 4, p = e & 15;
       reinterpret_cast<uint4 *>(smem + kLdsG8)[e] =
@@ -1234,12 +1005,8 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
       if (first >= n) break;
       const uint64_t i = first + g;
       const bool active = i < n;
-      if constexpr (S == 2)
-        process_records2<NR, OPEN>(rk, b, st, active ? rec_at(b, i) : 0, active, smem, gtab, lc0,
-                                   lc1, mf0);
-      else
-        process_records<NR, OPEN>(rk, b, st, active ? rec_at(b, i) : 0, active, smem, gtab, lc0,
-                                  lc1, mf0, stamps);
+      process_records<NR, OPEN>(rk, b, st, active ? rec_at(b, i) : 0, active, smem, gtab, lc0,
+                                lc1, mf0, stamps);
     }
 #if BSSL_AMD_GCM_STAMPS
     if (blockIdx.x < 2 && (tid & 63) == 0)
@@ -1280,9 +1047,9 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
       const uint8_t *gtab = reinterpret_cast<const uint8_t *>(keys[k].htab);
       if (k != loaded) {
         __syncthreads();
-        // Byte table of H^(16 S) from the key's nibble tables (power 3+S):
-        // entry (e, p) = T[2p][e >> 4] ^ T[2p+1][e & 15] (key_setup.cc layout).
-        const uint4 *t16 = reinterpret_cast<const uint4 *>(keys[k].htab[3 + S]);
+        // Byte table of H^16 from the key's nibble tables (power 4): entry
+        // (e, p) = T[2p][e >> 4] ^ T[2p+1][e & 15] (key_setup.cc layout).
+        const uint4 *t16 = reinterpret_cast<const uint4 *>(keys[k].htab[4]);
         for (uint32_t e = tid; e < 4096; e += kThreads) {
           const uint32_t ev = e >> 4, p = e & 15;
           reinterpret_cast<uint4 *>(smem + kLdsG8)[e] =
@@ -1298,12 +1065,8 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
         for (int c = 0; c < 4; c++) rk.w[r][c] = keys[k].rk[r][c];
       const int t = wave * kRecPerWave + g;
       const bool active = (mask >> t) & 1;
-      if constexpr (S == 2)
-        process_records2<NR, OPEN>(rk, b, st, active ? rec_at(b, base + t) : 0, active, smem,
-                                   gtab, lc0, lc1, mf0);
-      else
-        process_records<NR, OPEN>(rk, b, st, active ? rec_at(b, base + t) : 0, active, smem,
-                                  gtab, lc0, lc1, mf0, stamps);
+      process_records<NR, OPEN>(rk, b, st, active ? rec_at(b, base + t) : 0, active, smem, gtab,
+                                lc0, lc1, mf0, stamps);
     }
   }
 #if BSSL_AMD_GCM_STAMPS
@@ -1396,7 +1159,6 @@ __device__ __forceinline__ void process_records_bs(const GcmKeyDev *__restrict__
   uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   BS_STAMP(0);
-  constexpr int kLogL = L == 32 ? 5 : L == 16 ? 4 : 3;
   static_assert(L == 8 || L == 16 || L == 32, "lanes per record");
   const int q = threadIdx.x & (L - 1);
   RecordMeta m = {0, 0, 0, 0};
@@ -1585,14 +1347,6 @@ int bs_lanes(const BatchDesc &b) {
   return nb >= 1024 ? 32 : 0;
 }
 
-// Blocks per lane of the T-table kernel: 1 by default (two blocks per lane
-// measured slower); BSSL_AMD_GCM_S=2 selects the
-// two-block kernel (tuning).
-int gcm_blocks_per_lane(const BatchDesc &) {
-  const char *e = getenv("BSSL_AMD_GCM_S");
-  return (e && atoi(e) == 2) ? 2 : 1;
-}
-
 template <int NR, bool OPEN>
 int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const KernelEvents *ev) {
   if (!g_num_cus) {
@@ -1642,12 +1396,8 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
   } else {
     const uint64_t tiles = (b.num_records + kRecPerTile - 1) / kRecPerTile;
     const unsigned grid = (unsigned)(tiles < (uint64_t)g_num_cus ? tiles : (uint64_t)g_num_cus);
-    if (gcm_blocks_per_lane(b) == 2)
-      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, 2>), dim3(grid), dim3(kThreads), 0, s, keys, bo,
-                         (const RecState *)st, units);
-    else
-      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, 1>), dim3(grid), dim3(kThreads), 0, s, keys, bo,
-                         (const RecState *)st, units);
+    hipLaunchKernelGGL((gcm_kernel<NR, OPEN>), dim3(grid), dim3(kThreads), 0, s, keys, bo,
+                       (const RecState *)st, units);
   }
   int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
