@@ -43,7 +43,13 @@ CONFIGS = {
                 "config3: ChaCha20-Poly1305 seal, 1M x 1350 B records per GPU"),
     "config4": ("aes-256-gcm", 32, 1 << 22, "mixed",
                 "config4: AES-256-GCM seal, 4M records of 64 B-16 KiB (mixed) per GPU"),
+    # 64K keys x 64 records over 8 GPUs: per GPU 8192 keys x 64 records of
+    # 16 KiB (BSSL_AMD_KEYSET, key_index per record, records grouped by key).
+    "config5": ("aes-128-gcm", 16, 8192 * 64, 16384,
+                "config5: AES-128-GCM seal, 8192 keys x 64 records x 16 KiB per GPU "
+                "(64K keys over 8 GPUs), keyset"),
 }
+RECORDS_PER_KEY = {"config5": 64}
 
 
 def synth_key(k, key_len):
@@ -72,6 +78,7 @@ METRICS = {
     "config2": METRIC,
     "config3": "GiB/s device-resident AEAD seal (ChaCha20-Poly1305, 1350 B records)",
     "config4": "GiB/s device-resident AEAD seal (AES-256-GCM, mixed 64 B-16 KiB records)",
+    "config5": "GiB/s device-resident AEAD seal (AES-128-GCM, 16 KiB records, 64 records per key)",
 }
 
 
@@ -205,14 +212,24 @@ def main():
     d_tags = torch.empty(16 * nrec, dtype=torch.uint8, device=dev)
     d_status = torch.zeros(nrec, dtype=torch.uint8, device=dev)
     ba.synth_fill_device(first, nrec, d_offs, d_lens, d_pt, d_nonce, d_ad)
-    ctx = ba.AEADCtx(aead, synth_key(0, key_len), 16)
     uniform = length != "mixed"
+    rpk = RECORDS_PER_KEY.get(args.config)
+    d_kidx = None
+    if rpk:
+        # Keys of this rank's shard: global key ids first/rpk .. (synth_key).
+        nkeys = (nrec + rpk - 1) // rpk
+        k0 = first // rpk
+        ctx = ba.Keyset(aead, b"".join(synth_key(k0 + k, key_len) for k in range(nkeys)), nkeys,
+                        16)
+        d_kidx = torch.from_numpy((np.arange(nrec) // rpk).astype(np.int32)).to(dev)
+    else:
+        ctx = ba.AEADCtx(aead, synth_key(0, key_len), 16)
     batch = ba.make_batch(nrec, d_pt, d_ct, d_tags, d_nonce, 12, d_ad,
                           offsets=None if uniform else d_offs,
                           lengths=None if uniform else d_lens,
                           record_stride=int(padded[0]) if uniform else 0,
                           record_len=int(length) if uniform else 0,
-                          ad_stride=13, ad_len=13, status=d_status)
+                          ad_stride=13, ad_len=13, status=d_status, key_index=d_kidx)
     stream = torch.cuda.current_stream()
     torch.cuda.synchronize()
 

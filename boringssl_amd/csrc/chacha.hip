@@ -258,8 +258,16 @@ __device__ __forceinline__ P preduce(PAcc a) {
 // [Y_A, U_0, U_1, ...] of 4-block units, element v = u in lane u mod L, with
 // Horner's rule in R = r^4 at stride L (multiplier R^L), then the rotation +
 // log2(L)-level tree of gcm.hip's lane algebra.
+#ifndef BSSL_AMD_CHACHA_WPE
+#define BSSL_AMD_CHACHA_WPE 0
+#endif
+#if BSSL_AMD_CHACHA_WPE
+#define CHACHA_OCC __attribute__((amdgpu_waves_per_eu(BSSL_AMD_CHACHA_WPE)))
+#else
+#define CHACHA_OCC
+#endif
 template <bool OPEN, int L>
-__global__ __launch_bounds__(kThreads) void chacha_poly_kernel(
+__global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
     const ChaChaKeyDev *__restrict__ keys, BatchDesc b) {
   static_assert(L == 4 || L == 8 || L == 16, "lanes per record");
   constexpr int kLog = L == 4 ? 2 : L == 8 ? 3 : 4;
