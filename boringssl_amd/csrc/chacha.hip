@@ -7,11 +7,16 @@
 // poly1305.cc) / the fused chacha20_poly1305_seal_avx2 (chacha20_poly1305_
 // x86_64.pl:861).  Design:
 //
-// * L = 8 lanes per record, 8 records per wave.  The record's ChaCha blocks
+// * L = 4 lanes per record, 16 records per wave (8 lanes measured 16 % slower:
+//   the per-record serial Poly1305 work -- powers of r, lane tree, final
+//   reduction -- is amortized over fewer blocks per lane).  The record's ChaCha blocks
 //   u = 0..n (u = 0: the Poly1305 key block, counter 0; u >= 1: data block u-1,
 //   counter u, RFC 8439) are dealt round-robin to the lanes: one lane per
 //   64-byte block, keystream XORed with the input in registers.  Folding the
 //   key block into slot 0 keeps a 1350-byte record at 23 blocks in 24 slots.
+// * Registers: the powers of r live in LDS (per record) and the first
+//   ciphertext block waits in LDS while they are built, so the kernel fits
+//   128 VGPRs (4 waves per SIMD).
 // * Poly1305: the four 16-byte Poly blocks of data block d form one unit
 //   U = M0 r^3 + M1 r^2 + M2 r + M3.  A lane folds its units with Horner's
 //   rule in R = r^4 at stride L (multiplier R^L), one lazily reduced sum of
@@ -49,6 +54,10 @@ __device__ __forceinline__ void chacha_block(const uint32_t key[8], uint32_t ctr
   uint32_t x0 = 0x61707865, x1 = 0x3320646e, x2 = 0x79622d32, x3 = 0x6b206574;
   uint32_t x4 = key[0], x5 = key[1], x6 = key[2], x7 = key[3];
   uint32_t x8 = key[4], x9 = key[5], x10 = key[6], x11 = key[7];
+  // Opaque copies: otherwise hipcc hoists the key-only first steps of the
+  // column round out of the block loop and keeps them live (registers).
+  asm volatile("" : "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7), "+v"(x8), "+v"(x9), "+v"(x10),
+               "+v"(x11));
   uint32_t x12 = ctr, x13 = nonce[0], x14 = nonce[1], x15 = nonce[2];
 #pragma unroll
   for (int i = 0; i < 10; i++) {
@@ -259,18 +268,30 @@ __device__ __forceinline__ P preduce(PAcc a) {
 // Horner's rule in R = r^4 at stride L (multiplier R^L), then the rotation +
 // log2(L)-level tree of gcm.hip's lane algebra.
 #ifndef BSSL_AMD_CHACHA_WPE
-#define BSSL_AMD_CHACHA_WPE 0
+#define BSSL_AMD_CHACHA_WPE 4
 #endif
 #if BSSL_AMD_CHACHA_WPE
 #define CHACHA_OCC __attribute__((amdgpu_waves_per_eu(BSSL_AMD_CHACHA_WPE)))
 #else
 #define CHACHA_OCC
 #endif
+#ifndef BSSL_AMD_CHACHA_STAMPS
+#define BSSL_AMD_CHACHA_STAMPS 0
+#endif
+#if BSSL_AMD_CHACHA_STAMPS  // diagnostic build: per-phase cycles of sample waves
+#define CSTAMP(i) ts[i] = __builtin_amdgcn_s_memtime()
+#else
+#define CSTAMP(i)
+#endif
 template <bool OPEN, int L>
 __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
     const ChaChaKeyDev *__restrict__ keys, BatchDesc b) {
-  static_assert(L == 4 || L == 8 || L == 16, "lanes per record");
-  constexpr int kLog = L == 4 ? 2 : L == 8 ? 3 : 4;
+#if BSSL_AMD_CHACHA_STAMPS
+  uint64_t ts[5] = {0, 0, 0, 0, 0};
+#endif
+  CSTAMP(0);
+  static_assert(L == 2 || L == 4 || L == 8 || L == 16, "lanes per record");
+  constexpr int kLog = L == 2 ? 1 : L == 4 ? 2 : L == 8 ? 3 : 4;
   const int lane = threadIdx.x & 63;
   const int q = lane & (L - 1);
   const uint64_t pos = ((uint64_t)blockIdx.x * kThreads + threadIdx.x) / L;
@@ -362,9 +383,18 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
   chacha_block(key, (uint32_t)q, nonce, ks);
   const bool have0 = q >= 1 && (uint64_t)q <= nblk;
   if (have0) crypt_block((uint64_t)q, ks, pre, c0);
+  CSTAMP(1);
   uint32_t kw[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) kw[i] = __shfl(ks[i], 0, L);
+  // The first block's ciphertext waits in LDS while the powers of r are
+  // built (the register peak of the kernel otherwise).
+  __shared__ uint4 s_c0[kThreads][4];
+  if (have0) {
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      s_c0[threadIdx.x][i] = make_uint4(c0[4 * i], c0[4 * i + 1], c0[4 * i + 2], c0[4 * i + 3]);
+  }
   P pw[kLog + 4];  // pw[k] = r^(2^k), k = 0 .. kLog + 2  (r^(4L))
   uint32_t s[4];
   {
@@ -382,10 +412,33 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
 #pragma unroll
     for (int k = 1; k <= kLog + 2; k++) pw[k] = pmul(pw[k - 1], pw[k - 1]);
   }
-  const P &r = pw[0];
-  const P r2 = pw[1];
-  const P r3 = pmul(r2, r);
-  const P &rstride = pw[kLog + 2];  // R^L = r^(4L)
+  // The record's powers of r go to LDS (slot per record, written by its lane
+  // 0, read back by all L lanes as broadcasts): kept in registers across the
+  // ChaCha rounds they cost ~35 VGPRs and thereby a wave per SIMD.
+  // Slot layout: pw[0..kLog+2] then r^3, 5 limbs each.
+  __shared__ uint32_t s_pow[kThreads / L][5 * (kLog + 4)];
+  uint32_t *const mypow = s_pow[threadIdx.x / L];
+  if (q == 0) {
+    const P r3v = pmul(pw[1], pw[0]);
+#pragma unroll
+    for (int k = 0; k <= kLog + 2; k++)
+#pragma unroll
+      for (int i = 0; i < 5; i++) mypow[5 * k + i] = pw[k].h[i];
+#pragma unroll
+    for (int i = 0; i < 5; i++) mypow[5 * (kLog + 3) + i] = r3v.h[i];
+  }
+  __builtin_amdgcn_wave_barrier();
+  // Power k (k = kLog + 3: r^3), re-read at each use (the address is
+  // laundered so the loads are not hoisted out of the loops).
+  auto pwr = [&](int k) {
+    uint32_t off = 5 * k;
+    asm volatile("" : "+v"(off));
+    P o;
+#pragma unroll
+    for (int i = 0; i < 5; i++) o.h[i] = mypow[off + i];
+    return o;
+  };
+  constexpr int kR3 = kLog + 3, kStride = kLog + 2;  // r^3, R^L = r^(4L)
 
   // AD: exclusive Horner in r over the zero-padded 16-byte blocks, stride L.
   P ya = pzero();
@@ -404,12 +457,12 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
       if (nab == 1) ya = ad_block(0);
     } else {
       P acc = pzero();
-      for (uint64_t k = q; k < nab; k += L) acc = padd(pmul(acc, pw[kLog]), ad_block(k));
+      for (uint64_t k = q; k < nab; k += L) acc = padd(pmul(acc, pwr(kLog)), ad_block(k));
       P a = pshfl(acc, (q + (int)(nab % L)) & (L - 1), L);
 #pragma unroll
       for (int t = 0; t < kLog; t++) {
         const int sh = 1 << t;
-        const P mm = pmul(a, pw[t]);
+        const P mm = pmul(a, pwr(t));
         const P o = pshfl_down(a, sh, L);
         if ((q & (2 * sh - 1)) == 0) a = padd(mm, o);
       }
@@ -425,19 +478,33 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
     const uint64_t d = u - 1;
     if (d < nunits) {
       PAcc t = pacc_zero();
-      pmac(t, acc, rstride);
-      pmac(t, pblock(c[0], c[1], c[2], c[3]), r3);
-      pmac(t, pblock(c[4], c[5], c[6], c[7]), r2);
-      pmac(t, pblock(c[8], c[9], c[10], c[11]), r);
+      pmac(t, acc, pwr(kStride));
+      pmac(t, pblock(c[0], c[1], c[2], c[3]), pwr(kR3));
+      pmac(t, pblock(c[4], c[5], c[6], c[7]), pwr(1));
+      pmac(t, pblock(c[8], c[9], c[10], c[11]), pwr(0));
       acc = padd(preduce(t), pblock(c[12], c[13], c[14], c[15]));
     } else {
       P tt = pblock(c[0], c[1], c[2], c[3]);
-      for (uint32_t k = 1; k < tail_blocks; k++)
-        tt = padd(pmul(tt, r), pblock(c[4 * k], c[4 * k + 1], c[4 * k + 2], c[4 * k + 3]));
+      // (constant indices: a runtime index would move c[] to scratch)
+#pragma unroll
+      for (uint32_t k = 1; k < 4; k++)
+        if (k < tail_blocks)
+          tt = padd(pmul(tt, pwr(0)), pblock(c[4 * k], c[4 * k + 1], c[4 * k + 2], c[4 * k + 3]));
       tail = tt;
     }
   };
-  if (have0) absorb((uint64_t)q, c0);
+  if (have0) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint4 v = s_c0[threadIdx.x][i];
+      c0[4 * i] = v.x;
+      c0[4 * i + 1] = v.y;
+      c0[4 * i + 2] = v.z;
+      c0[4 * i + 3] = v.w;
+    }
+    absorb((uint64_t)q, c0);
+  }
+  CSTAMP(2);
   for (int it = 1; it < iters; it++) {
     const uint64_t u = (uint64_t)it * L + q;
     prefetch(u, pre);
@@ -449,6 +516,7 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
     }
   }
 
+  CSTAMP(3);
   // Combine the lanes: M = nunits + 1 virtual elements; lane p takes the
   // accumulator of lane (p + M mod L) and the tree weights position p by
   // R^(L-1-p).
@@ -456,7 +524,7 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
 #pragma unroll
   for (int t = 0; t < kLog; t++) {
     const int sh = 1 << t;
-    const P mm = pmul(z, pw[t + 2]);
+    const P mm = pmul(z, pwr(t + 2));
     const P o = pshfl_down(z, sh, L);
     if ((q & (2 * sh - 1)) == 0) z = padd(mm, o);
   }
@@ -464,12 +532,13 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
   tail = pshfl(tail, (int)((nunits + 1) % L), L);
   const int tmax = wave_max((int)tail_blocks);
   for (int k = 0; k < tmax; k++)
-    if ((uint32_t)k < tail_blocks) z = pmul(z, r);
+    if ((uint32_t)k < tail_blocks) z = pmul(z, pwr(0));
   if (tail_blocks) z = padd(z, tail);
   // h = ((Z r) + L) r with L = le64(ad_len) || le64(ct_len) (+2^128).
   const P lb = pblock((uint32_t)m.ad_len, (uint32_t)(m.ad_len >> 32), (uint32_t)m.len,
                       (uint32_t)(m.len >> 32));
-  const P h = pmul(padd(pmul(z, r), lb), r);
+  const P rr = pwr(0);
+  const P h = pmul(padd(pmul(z, rr), lb), rr);
   uint32_t tag[4];
   poly_finish(h, s, tag);
 
@@ -496,6 +565,15 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
       for (uint64_t i = 0; i < n; i++) dst[j * 16 + i] = 0;
     }
   }
+#if BSSL_AMD_CHACHA_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  CSTAMP(4);
+  if ((blockIdx.x & 2047) == 5 && threadIdx.x == 64)
+    printf("cstamps blk %d: start->blk0 %llu setup %llu loop %llu finish %llu total %llu\n",
+           (int)blockIdx.x, (unsigned long long)(ts[1] - ts[0]), (unsigned long long)(ts[2] - ts[1]),
+           (unsigned long long)(ts[3] - ts[2]), (unsigned long long)(ts[4] - ts[3]),
+           (unsigned long long)(ts[4] - ts[0]));
+#endif
 }
 
 }  // namespace
@@ -504,7 +582,10 @@ int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, void 
                   const KernelEvents *ev) {
   if (b.num_records == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  constexpr int L = 8;  // lanes per record (see chacha_poly_kernel)
+#ifndef BSSL_AMD_CHACHA_L
+#define BSSL_AMD_CHACHA_L 4
+#endif
+  constexpr int L = BSSL_AMD_CHACHA_L;  // lanes per record (see chacha_poly_kernel)
   const uint64_t blocks = (b.num_records * L + kThreads - 1) / kThreads;
   if (blocks > 0x7fffffffu) return 1;
   BatchDesc bo = b;  // with the processing order of a ragged batch
