@@ -183,7 +183,7 @@ const KernelEvents *timing_pair() {
 
 // Launch a batch over device buffers.  Returns 1 on success.
 int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch, bool open,
-              bool use_key_index, void *stream) {
+              bool use_key_index, void *stream, const uint8_t *valid = nullptr) {
   BatchDesc d;
   d.in = batch->in;
   d.out = batch->out;
@@ -205,6 +205,7 @@ int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch
   d.tag_len = (uint32_t)tag_len;
   d.num_keys = (uint32_t)km->num_keys;
   d.order = nullptr;
+  d.valid = valid;
   int rc;
   const KernelEvents *ev = timing_pair();
   if (km->aead->kind == kAeadAesGcm) {
@@ -238,12 +239,6 @@ bool check_batch(const EVP_AEAD *aead, const BSSL_AMD_BATCH *b) {
     }
   } else if (b->nonce_len != 12) {  // e_chacha20poly1305.cc:127-130
     PUT_ERROR(CIPHER_R_UNSUPPORTED_NONCE_SIZE);
-    return false;
-  }
-  if (aead->tls) {
-    // The stateful tls12/tls13 variants check nonce monotonicity record by
-    // record in order on the host; batches of them are not supported.
-    PUT_ERROR(CIPHER_R_CTRL_NOT_IMPLEMENTED);
     return false;
   }
   return true;
@@ -894,7 +889,28 @@ int EVP_AEAD_CTX_seal_batch_device(const EVP_AEAD_CTX *ctx, const BSSL_AMD_BATCH
                                    void *hip_stream) {
   if (!ctx || !ctx->aead || !check_batch(ctx->aead, batch)) return 0;
   if (batch->num_records == 0) return 1;
-  return run_batch(state_of(ctx)->km, ctx->tag_len, batch, false, false, hip_stream);
+  CtxState *st = state_of(ctx);
+  if (!ctx->aead->tls)
+    return run_batch(st->km, ctx->tag_len, batch, false, false, hip_stream);
+  if (batch->nonce_len != 12) {  // e_aes.cc.inc:1077-1080, 1168-1171 (seal only)
+    PUT_ERROR(CIPHER_R_UNSUPPORTED_NONCE_SIZE);
+    return 0;
+  }
+  // tls12/tls13: the records are N sealv calls in order, each with the
+  // monotonic-nonce check (tls_scan.hip); records that fail it fail like the
+  // reference call (zeroed output, status 0) and leave the state unchanged.
+  hipStream_t s = reinterpret_cast<hipStream_t>(hip_stream);
+  uint8_t *valid = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void **>(&valid), batch->num_records, s) != hipSuccess) {
+    PUT_ERROR(ERR_R_MALLOC_FAILURE);
+    return 0;
+  }
+  int ok = tls_nonce_scan(batch->nonces, batch->num_records, ctx->aead->tls,
+                          &st->min_next_nonce, &st->mask, valid, hip_stream) == 0;
+  if (!ok) PUT_ERROR(ERR_R_INTERNAL_ERROR);
+  if (ok) ok = run_batch(st->km, ctx->tag_len, batch, false, false, hip_stream, valid);
+  hipFreeAsync(valid, s);
+  return ok;
 }
 
 int EVP_AEAD_CTX_open_batch_device(const EVP_AEAD_CTX *ctx, const BSSL_AMD_BATCH *batch,
@@ -941,6 +957,10 @@ size_t BSSL_AMD_KEYSET_num_keys(const BSSL_AMD_KEYSET *ks) { return ks ? ks->km-
 int BSSL_AMD_KEYSET_seal_batch_device(const BSSL_AMD_KEYSET *ks, const BSSL_AMD_BATCH *batch,
                                       void *hip_stream) {
   if (!ks || !check_batch(ks->km->aead, batch)) return 0;
+  if (ks->km->aead->tls) {  // per-key nonce state: one EVP_AEAD_CTX per key instead
+    PUT_ERROR(CIPHER_R_CTRL_NOT_IMPLEMENTED);
+    return 0;
+  }
   if (batch->num_records == 0) return 1;
   return run_batch(ks->km, ks->tag_len, batch, false, true, hip_stream);
 }

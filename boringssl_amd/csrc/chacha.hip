@@ -308,7 +308,8 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
   }
   // e_chacha20poly1305.cc:127-142: 12-byte nonce, < 2^32 - 1 blocks.
   const bool bad = active && (kidx >= b.num_keys || b.nonce_len != 12 ||
-                              m.len >= (uint64_t(1) << 32) * 64 - 64);
+                              m.len >= (uint64_t(1) << 32) * 64 - 64 ||
+                              (b.valid && !b.valid[rec]));
   const bool live = active && !bad;
   uint32_t key[8], nonce[3];
   {

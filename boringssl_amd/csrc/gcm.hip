@@ -664,7 +664,8 @@ __global__ __launch_bounds__(256) void gcm_prologue(const GcmKeyDev *__restrict_
   const uint32_t k = b.key_index ? b.key_index[rec] : 0u;
   // e_aes.cc.inc:790 (empty nonce), gcm.cc.inc:368,409 (length limits).
   const bool live = k < b.num_keys && b.nonce_len != 0 &&
-                    m.len <= ((uint64_t(1) << 36) - 32) && m.ad_len <= (uint64_t(1) << 61);
+                    m.len <= ((uint64_t(1) << 36) - 32) && m.ad_len <= (uint64_t(1) << 61) &&
+                    (!b.valid || b.valid[rec]);  // tls12/tls13 nonce check (tls_scan.hip)
   RecState s;
   s.live = live;
   s.pad[0] = s.pad[1] = s.pad[2] = 0;

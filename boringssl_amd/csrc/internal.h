@@ -69,6 +69,10 @@ struct BatchDesc {
   // Processing order (device, num_records entries) or null for 0..n-1; set by
   // the launchers for ragged batches (sched.hip), never by callers.
   const uint32_t *order;
+  // Per-record precondition flags (device, 1 = the record may be sealed) or
+  // null: the tls12/tls13 nonce checks of tls_scan.hip.  A record with flag 0
+  // fails like a reference call that returned 0 (zeroed output, status 0).
+  const uint8_t *valid;
 };
 
 // HIP events recorded on the launch stream immediately before and after the
@@ -92,6 +96,11 @@ inline bool wants_length_order(const BatchDesc &b) {
 }
 int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open,
                   void *stream, const KernelEvents *ev);
+// tls12 / tls13 nonce checks over a batch of seal calls (tls_scan.hip):
+// writes valid[i] (device) and advances the context's nonce state in place
+// (min_next_nonce, mask); synchronises `stream`.  Returns 0 or an error code.
+int tls_nonce_scan(const uint8_t *nonces, uint64_t n, int tls, uint64_t *min_next,
+                   uint64_t *mask, uint8_t *valid, void *stream);
 int launch_synth(uint64_t first, size_t n, const uint64_t *offsets,
                  const uint64_t *lengths, uint8_t *pt, uint8_t *nonces,
                  uint8_t *ads, void *stream);

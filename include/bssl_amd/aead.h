@@ -215,7 +215,15 @@ typedef struct bssl_amd_batch_st {
  * ignored), enqueued on `hip_stream` (NULL = default stream).  Returns 1 if
  * the batch was launched (per-record results in status/tags), 0 on an
  * argument error (pushed to the error queue).  Asynchronous with respect to
- * the host. */
+ * the host.
+ *
+ * For the stateful EVP_aead_aes_*_gcm_tls12 / _tls13 contexts a sealed batch
+ * is N calls in record order, each with the reference's monotonic-nonce check
+ * (e_aes.cc.inc:1071-1100, 1162-1202; nonce_len must be 12): a record whose
+ * nonce fails it gets status 0 and zeroed output/tag, and the context's nonce
+ * state advances as after the N calls.  These seal calls synchronise
+ * `hip_stream` (the state lives in the host-side context).  Keysets reject
+ * the tls variants (CIPHER_R_CTRL_NOT_IMPLEMENTED). */
 BSSL_AMD_EXPORT int EVP_AEAD_CTX_seal_batch_device(const EVP_AEAD_CTX *ctx,
                                                    const BSSL_AMD_BATCH *batch,
                                                    void *hip_stream);

@@ -421,3 +421,149 @@ def test_plain_c_caller_on_gpu(tmp_path):
                            "-lbssl_amd", f"-Wl,-rpath,{libdir}", "-o", str(exe)])
     out = subprocess.check_output([str(exe)], text=True, timeout=120).strip()
     assert out == "f9ff3fa1f8bade711aa97c0f652d67fe"  # SURVEY.md 8(c), reference output
+
+
+# ---------------------------------------------------------------------------
+# tls12 / tls13 AEADs: the stateful monotonic-nonce check, single records and
+# batches (a batch = N sealv calls in record order).
+
+U64_MAX = (1 << 64) - 1
+
+
+def _tls_rule(kind, nonces, state):
+    """Restatement of aead_aes_gcm_tls12_sealv (e_aes.cc.inc:1071-1100) and
+    aead_aes_gcm_tls13_sealv (:1162-1202): which calls pass the nonce check;
+    `state` (min_next, mask) is advanced in place."""
+    ok = []
+    for nz in nonces:
+        given = int.from_bytes(nz[4:12], "big")
+        if kind == 12:
+            good = given != U64_MAX and given >= state["min_next"]
+            if good:
+                state["min_next"] = given + 1
+        elif state["min_next"] == 0:
+            state["mask"], state["min_next"], good = given, 1, True
+        else:
+            c = given ^ state["mask"]
+            good = c != U64_MAX and c >= state["min_next"]
+            if good:
+                state["min_next"] = c + 1
+        ok.append(good)
+    return ok
+
+
+def _tls_nonces(kind, rng, n):
+    """Mostly increasing sequence numbers with repeats, steps back, gaps and
+    the all-ones counter, in the record nonce layout of each variant
+    (ssl/ssl_aead_ctx.cc:326-365: TLS 1.2 GCM fixed 4 B || explicit 8 B,
+    TLS 1.3 fixed_iv XOR (0^4 || be64(seq)))."""
+    seqs, s = [], 0
+    for i in range(n):
+        r = rng.random()
+        if r < 0.1:
+            s = max(0, s - rng.randint(1, 3))
+        elif r < 0.2:
+            pass
+        elif r < 0.25:
+            s += rng.randint(2, 50)
+        else:
+            s += 1
+        seqs.append(s)
+    seqs[n // 2] = U64_MAX
+    if kind == 13:
+        seqs[0] = 0  # the first record sets the mask
+        iv = bytes(rng.getrandbits(8) for _ in range(12))
+        return [bytes(a ^ b for a, b in zip(iv, bytes(4) + q.to_bytes(8, "big"))) for q in seqs]
+    fixed = bytes(rng.getrandbits(8) for _ in range(4))
+    return [fixed + q.to_bytes(8, "big") for q in seqs]
+
+
+def _tls_batch(ctx, ins, nonces, ads):
+    inbuf, offs = _pack(ins)
+    adbuf, ad_offs = _pack(ads, 1)
+    n = len(ins)
+    d_in = _t(inbuf)
+    d_out = torch.full_like(d_in, 0x5a)
+    d_tags = torch.full((16 * n,), 0x5a, dtype=torch.uint8, device=DEV)
+    d_status = torch.full((n,), 7, dtype=torch.uint8, device=DEV)
+    b = ba.make_batch(n, d_in, d_out, d_tags, _t(np.frombuffer(b"".join(nonces), np.uint8).copy()),
+                      12, _t(adbuf), offsets=_t(offs.astype(np.int64)),
+                      lengths=_t(np.array([len(x) for x in ins], np.int64)),
+                      ad_offsets=_t(ad_offs.astype(np.int64)),
+                      ad_lengths=_t(np.array([len(x) for x in ads], np.int64)), status=d_status)
+    ctx.seal_batch_device(b)
+    torch.cuda.synchronize()
+    out, tg, st = d_out.cpu().numpy(), d_tags.cpu().numpy().tobytes(), d_status.cpu().numpy()
+    return ([out[int(offs[i]):int(offs[i]) + len(ins[i])].tobytes() for i in range(n)],
+            [tg[16 * i:16 * i + 16] for i in range(n)], st)
+
+
+@pytest.mark.parametrize("aead", ["aes-128-gcm-tls12", "aes-256-gcm-tls12", "aes-128-gcm-tls13",
+                                  "aes-256-gcm-tls13"])
+def test_tls_nonce_check_batches(aead):
+    kind = 12 if "tls12" in aead else 13
+    rng = random.Random(kind * 7 + len(aead))
+    key = bytes(rng.getrandbits(8) for _ in range(32 if "256" in aead else 16))
+    n = 700
+    nonces = _tls_nonces(kind, rng, n)
+    ins = [bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 1, 15, 16, 17, 100, 1350])))
+           for _ in range(n)]
+    ads = [bytes(rng.getrandbits(8) for _ in range(13)) for _ in range(n)]
+    state = {"min_next": 0, "mask": 0}
+    expect = _tls_rule(kind, nonces, state)
+    assert 0 < sum(expect) < n
+    # The same calls as two device batches on one context, then one more
+    # single-record call: the nonce state carries across them.
+    ctx = ba.AEADCtx(aead, key, 16)
+    half = n // 2
+    outs, tags, st = _tls_batch(ctx, ins[:half], nonces[:half], ads[:half])
+    outs2, tags2, st2 = _tls_batch(ctx, ins[half:], nonces[half:], ads[half:])
+    outs, tags, st = outs + outs2, tags + tags2, list(st) + list(st2)
+    for i in range(n):
+        if expect[i]:
+            ok, ct, tag = o.seal(o.AES_GCM, key, nonces[i], ins[i], ads[i])
+            assert ok and st[i] == 1 and outs[i] == ct and tags[i] == tag, i
+        else:
+            assert st[i] == 0 and outs[i] == bytes(len(ins[i])) and tags[i] == bytes(16), i
+    # Next call: a nonce one below the state must fail, the state's own must pass.
+    nxt = state["min_next"]
+    for delta, good in ((-1, False), (0, True)):
+        c = nxt + delta
+        if kind == 13:
+            c ^= state["mask"]
+        nonce = nonces[0][:4] + c.to_bytes(8, "big")
+        if good:
+            ok, ct, tag = o.seal(o.AES_GCM, key, nonce, b"abc", b"")
+            assert ctx.seal(nonce, b"abc") == ct + tag
+        else:
+            with pytest.raises(ba.AEADError) as e:
+                ctx.seal(nonce, b"abc")
+            assert e.value.reason == ba.CIPHER_R_INVALID_NONCE
+    # Sequential single-record calls on a fresh context agree with the batch.
+    ctx1 = ba.AEADCtx(aead, key, 16)
+    seq_ok = []
+    for i in range(n):
+        try:
+            r = ctx1.seal(nonces[i], ins[i], ads[i])
+            seq_ok.append(True)
+            assert r == outs[i] + tags[i], i
+        except ba.AEADError as e:
+            assert e.reason == ba.CIPHER_R_INVALID_NONCE
+            seq_ok.append(False)
+    assert seq_ok == expect
+
+
+def test_tls_batch_rejections():
+    """Keysets reject the stateful variants; tls seal batches need 12-byte
+    nonces (open batches accept any, as aead_aes_gcm_openv_detached)."""
+    key = bytes(range(16))
+    with pytest.raises(ba.AEADError) as e:
+        ks = ba.Keyset("aes-128-gcm-tls13", key, 1, 16)
+        d = torch.zeros(64, dtype=torch.uint8, device=DEV)
+        ks.seal_batch_device(ba.make_batch(1, d, d, d, d, 12, d, record_len=16, record_stride=16))
+    assert e.value.reason == ba.CIPHER_R_CTRL_NOT_IMPLEMENTED
+    ctx = ba.AEADCtx("aes-128-gcm-tls12", key, 16)
+    d = torch.zeros(64, dtype=torch.uint8, device=DEV)
+    with pytest.raises(ba.AEADError) as e:
+        ctx.seal_batch_device(ba.make_batch(1, d, d, d, d, 8, d, record_len=16, record_stride=16))
+    assert e.value.reason == ba.CIPHER_R_UNSUPPORTED_NONCE_SIZE
