@@ -41,6 +41,7 @@ CIPHER_R_BAD_KEY_LENGTH = 102
 CIPHER_R_BUFFER_TOO_SMALL = 103
 CIPHER_R_CTRL_NOT_IMPLEMENTED = 104
 CIPHER_R_INVALID_NONCE_SIZE = 111
+CIPHER_R_INVALID_OPERATION = 112
 CIPHER_R_OUTPUT_ALIASES_INPUT = 115
 CIPHER_R_TAG_TOO_LARGE = 116
 CIPHER_R_TOO_LARGE = 117
@@ -52,7 +53,7 @@ EVP_AEAD_DEFAULT_TAG_LENGTH = 0
 evp_aead_open = 0
 evp_aead_seal = 1
 
-# Every symbol include/bssl_amd/aead.h declares (checked by tests/test_abi.py).
+# Every symbol include/bssl_amd/*.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = [
     "EVP_aead_aes_128_gcm", "EVP_aead_aes_192_gcm", "EVP_aead_aes_256_gcm",
     "EVP_aead_chacha20_poly1305", "EVP_aead_aes_128_gcm_tls12", "EVP_aead_aes_256_gcm_tls12",
@@ -70,7 +71,13 @@ EXPORTED_SYMBOLS = [
     "BSSL_AMD_set_device", "BSSL_AMD_device_count", "BSSL_AMD_synth_fill_device",
     "BSSL_AMD_set_kernel_timing", "BSSL_AMD_collect_kernel_times", "BSSL_AMD_last_kernel_ms",
     "BSSL_AMD_last_kernel_name",
+    # include/bssl_amd/tls.h
+    "BSSL_AMD_TLS_AEAD_new", "BSSL_AMD_TLS_AEAD_free", "BSSL_AMD_TLS_AEAD_prefix_len",
+    "BSSL_AMD_TLS_AEAD_suffix_len", "BSSL_AMD_TLS_AEAD_sequence",
+    "BSSL_AMD_TLS_AEAD_seal_records_device", "BSSL_AMD_TLS_AEAD_open_records_device",
 ]
+TLS1_2_VERSION = 0x0303
+TLS1_3_VERSION = 0x0304
 
 
 class EVP_AEAD_CTX(ctypes.Structure):
@@ -93,6 +100,14 @@ class BSSL_AMD_BATCH(ctypes.Structure):
         ("nonces", _P), ("nonce_len", _S), ("ad", _P), ("ad_offsets", _P), ("ad_lengths", _P),
         ("ad_stride", ctypes.c_uint64), ("ad_len", ctypes.c_uint64), ("tags", _P),
         ("status", _P), ("key_index", _P),
+    ]
+
+
+class BSSL_AMD_TLS_RECORDS(ctypes.Structure):
+    _fields_ = [
+        ("num_records", _S), ("in_", _P), ("out", _P), ("offsets", _P), ("lengths", _P),
+        ("record_stride", ctypes.c_uint64), ("record_len", ctypes.c_uint64), ("types", _P),
+        ("type", ctypes.c_uint8), ("prefix", _P), ("suffix", _P), ("status", _P),
     ]
 
 
@@ -136,6 +151,13 @@ _SIGS = {
     "BSSL_AMD_collect_kernel_times": (_S, [ctypes.POINTER(ctypes.c_double), _S]),
     "BSSL_AMD_last_kernel_ms": (ctypes.c_double, []),
     "BSSL_AMD_last_kernel_name": (ctypes.c_char_p, []),
+    "BSSL_AMD_TLS_AEAD_new": (_P, [_I, ctypes.c_uint16, _P, _P, _S, _P, _S, ctypes.c_uint64]),
+    "BSSL_AMD_TLS_AEAD_free": (None, [_P]),
+    "BSSL_AMD_TLS_AEAD_prefix_len": (_S, [_P]),
+    "BSSL_AMD_TLS_AEAD_suffix_len": (_S, [_P]),
+    "BSSL_AMD_TLS_AEAD_sequence": (ctypes.c_uint64, [_P]),
+    "BSSL_AMD_TLS_AEAD_seal_records_device": (_I, [_P, ctypes.POINTER(BSSL_AMD_TLS_RECORDS), _P]),
+    "BSSL_AMD_TLS_AEAD_open_records_device": (_I, [_P, ctypes.POINTER(BSSL_AMD_TLS_RECORDS), _P]),
 }
 for _name in EXPORTED_SYMBOLS:
     _f = getattr(_lib, _name)
@@ -299,6 +321,67 @@ def _stream_ptr(stream):
 
 def _dptr(t):
     return None if t is None else t.data_ptr()
+
+
+class TlsAead:
+    """BSSL_AMD_TLS_AEAD: one direction of a TLS 1.2 / 1.3 connection (the
+    reference's SSLAEADContext) sealing / opening device batches of records."""
+
+    def __init__(self, direction, version, aead, key, fixed_iv, seq=0):
+        if isinstance(aead, str):
+            aead = EVP_aead(aead)
+        key, fixed_iv = bytes(key), bytes(fixed_iv)
+        self.h = _lib.BSSL_AMD_TLS_AEAD_new(direction, version, aead, key, len(key), fixed_iv,
+                                            len(fixed_iv), seq)
+        if not self.h:
+            _fail("BSSL_AMD_TLS_AEAD_new")
+
+    @property
+    def prefix_len(self):
+        return _lib.BSSL_AMD_TLS_AEAD_prefix_len(self.h)
+
+    @property
+    def suffix_len(self):
+        return _lib.BSSL_AMD_TLS_AEAD_suffix_len(self.h)
+
+    @property
+    def sequence(self):
+        return _lib.BSSL_AMD_TLS_AEAD_sequence(self.h)
+
+    def seal_records_device(self, recs, stream=None):
+        if not _lib.BSSL_AMD_TLS_AEAD_seal_records_device(self.h, ctypes.byref(recs),
+                                                          _stream_ptr(stream)):
+            _fail("BSSL_AMD_TLS_AEAD_seal_records_device")
+
+    def open_records_device(self, recs, stream=None):
+        if not _lib.BSSL_AMD_TLS_AEAD_open_records_device(self.h, ctypes.byref(recs),
+                                                          _stream_ptr(stream)):
+            _fail("BSSL_AMD_TLS_AEAD_open_records_device")
+
+    def close(self):
+        if self.h:
+            _lib.BSSL_AMD_TLS_AEAD_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover
+            pass
+
+
+def make_tls_records(num_records, inp, out, prefix, suffix, *, offsets=None, lengths=None,
+                     record_stride=0, record_len=0, types=None, type_=23, status=None):
+    """BSSL_AMD_TLS_RECORDS from torch device tensors (keeps references)."""
+    r = BSSL_AMD_TLS_RECORDS()
+    r.num_records = num_records
+    r.in_, r.out = _dptr(inp), _dptr(out)
+    r.offsets, r.lengths = _dptr(offsets), _dptr(lengths)
+    r.record_stride, r.record_len = record_stride, record_len
+    r.types, r.type = _dptr(types), type_
+    r.prefix, r.suffix, r.status = _dptr(prefix), _dptr(suffix), _dptr(status)
+    r._refs = (inp, out, offsets, lengths, types, prefix, suffix, status)
+    return r
 
 
 def make_batch(num_records, inp, out, tags, nonces, nonce_len, ad=None, *, offsets=None,

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "bssl_amd/aead.h"
+#include "bssl_amd/tls.h"
 #include "internal.h"
 
 using namespace bssl_amd;
@@ -206,6 +207,9 @@ int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch
   d.num_keys = (uint32_t)km->num_keys;
   d.order = nullptr;
   d.valid = valid;
+  d.extra = nullptr;
+  d.extra_out = nullptr;
+  d.extra_len = d.extra_stride = d.extra_out_stride = d.tag_stride = 0;
   int rc;
   const KernelEvents *ev = timing_pair();
   if (km->aead->kind == kAeadAesGcm) {
@@ -906,7 +910,7 @@ int EVP_AEAD_CTX_seal_batch_device(const EVP_AEAD_CTX *ctx, const BSSL_AMD_BATCH
     return 0;
   }
   int ok = tls_nonce_scan(batch->nonces, batch->num_records, ctx->aead->tls,
-                          &st->min_next_nonce, &st->mask, valid, hip_stream) == 0;
+                          &st->min_next_nonce, &st->mask, valid, 0, hip_stream) == 0;
   if (!ok) PUT_ERROR(ERR_R_INTERNAL_ERROR);
   if (ok) ok = run_batch(st->km, ctx->tag_len, batch, false, false, hip_stream, valid);
   hipFreeAsync(valid, s);
@@ -1007,5 +1011,231 @@ size_t BSSL_AMD_collect_kernel_times(double *out_ms, size_t max) {
 
 double BSSL_AMD_last_kernel_ms(void) { return t_timing.last_ms; }
 const char *BSSL_AMD_last_kernel_name(void) { return t_timing.last_name; }
+
+}  // extern "C"
+
+// ---- TLS record layer over device batches (bssl_amd/tls.h) ---------------
+// SSLAEADContext (ssl/ssl_aead_ctx.cc) + do_seal_record / tls_open_record
+// (ssl/tls_record.cc) for a batch of records; the per-record nonce, header,
+// AD and inner type are built on the device (tls_records.hip) and the records
+// go through the same bulk kernels as any batch.
+
+struct bssl_amd_tls_aead_st {
+  EVP_AEAD_CTX ctx;
+  bool seal;
+  bool tls13;
+  bool xor_nonce;
+  uint32_t explicit_len;
+  uint8_t fixed_iv[12];
+  uint64_t seq;
+};
+
+namespace {
+
+const EVP_AEAD *tls_record_aead(const EVP_AEAD *aead, bool tls13) {
+  // ssl_cipher_get_evp_aead (ssl/ssl_cipher.cc): the nonce-checking variants
+  // for AES-GCM in TLS 1.2 / 1.3.
+  if (aead == &kAes128Gcm) return tls13 ? &kAes128GcmTls13 : &kAes128GcmTls12;
+  if (aead == &kAes256Gcm) return tls13 ? &kAes256GcmTls13 : &kAes256GcmTls12;
+  if (aead == &kChaChaPoly) return aead;
+  return nullptr;
+}
+
+int tls_records(BSSL_AMD_TLS_AEAD *t, const BSSL_AMD_TLS_RECORDS *r, void *stream) {
+  if (!t || !r || (r->num_records && (!r->in || !r->out || !r->prefix || !r->suffix))) {
+    PUT_ERROR(ERR_R_SHOULD_NOT_HAVE_BEEN_CALLED);
+    return 0;
+  }
+  const uint64_t n = r->num_records;
+  if (n == 0) return 1;
+  // tls_record.cc:305-308: the sequence number must not wrap.
+  if (t->seq > UINT64_MAX - n) {
+    PUT_ERROR(ERR_R_OVERFLOW);
+    return 0;
+  }
+  if (!t->seal && t->tls13 && !r->types) {  // open returns the inner types
+    PUT_ERROR(ERR_R_SHOULD_NOT_HAVE_BEEN_CALLED);
+    return 0;
+  }
+  const EVP_AEAD_CTX *ctx = &t->ctx;
+  CtxState *st = state_of(ctx);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint32_t ad_stride = t->tls13 ? 5 : 13;
+  const uint32_t extra_len = t->tls13 ? 1 : 0;
+  const uint32_t tag_len = ctx->tag_len;
+  const uint32_t prefix_len = 5 + t->explicit_len;
+  const uint32_t suffix_len = extra_len + tag_len;
+  // Scratch: nonces (12 B), AD, inner types (seal, TLS 1.3) and flags per record.
+  uint8_t *buf = nullptr;
+  const size_t bytes = n * (12 + ad_stride + 1 + 1);
+  if (hipMallocAsync(reinterpret_cast<void **>(&buf), bytes, s) != hipSuccess) {
+    PUT_ERROR(ERR_R_MALLOC_FAILURE);
+    return 0;
+  }
+  uint8_t *d_nonce = buf, *d_ad = d_nonce + 12 * n, *d_type = d_ad + ad_stride * n,
+          *d_valid = d_type + n;
+  int ok = hipMemsetAsync(d_valid, 1, n, s) == hipSuccess;
+  TlsPrepare p;
+  p.n = n;
+  p.lengths = r->lengths;
+  p.record_len = r->record_len;
+  p.types = r->types;
+  p.type = r->type;
+  memcpy(p.fixed_iv, t->fixed_iv, 12);
+  p.seq = t->seq;
+  p.xor_nonce = t->xor_nonce;
+  p.tls13 = t->tls13;
+  p.record_version = 0x0303;  // tls_record_version: TLS 1.3 records say TLS 1.2
+  p.explicit_len = t->explicit_len;
+  p.extra_len = extra_len;
+  p.tag_len = tag_len;
+  p.prefix_len = prefix_len;
+  p.ad_stride = ad_stride;
+  p.open = !t->seal;
+  p.nonces = d_nonce;
+  p.prefix = r->prefix;
+  p.ad = d_ad;
+  p.extra = d_type;
+  p.valid = d_valid;
+  if (ok) ok = launch_tls_prepare(p, stream) == 0;
+  if (ok && t->seal && ctx->aead->tls)  // the AEAD's own nonce check (sealv)
+    ok = tls_nonce_scan(d_nonce, n, ctx->aead->tls, &st->min_next_nonce, &st->mask, d_valid, 1,
+                        stream) == 0;
+  if (ok) {
+    BatchDesc d;
+    memset(&d, 0, sizeof(d));
+    d.in = r->in;
+    d.out = r->out;
+    d.offsets = r->offsets;
+    d.lengths = r->lengths;
+    d.record_stride = r->record_stride;
+    d.record_len = r->record_len;
+    d.nonces = d_nonce;
+    d.nonce_len = 12;
+    d.ad = d_ad;
+    d.ad_stride = ad_stride;
+    d.ad_len = ad_stride;
+    d.tags = r->suffix + extra_len;
+    d.tag_stride = suffix_len;
+    d.status = r->status;
+    d.num_records = n;
+    d.tag_len = tag_len;
+    d.num_keys = 1;
+    d.valid = d_valid;
+    if (extra_len) {
+      d.extra_len = extra_len;
+      if (t->seal) {  // inner type in, its ciphertext to the suffix
+        d.extra = d_type;
+        d.extra_stride = 1;
+        d.extra_out = r->suffix;
+        d.extra_out_stride = suffix_len;
+      } else {        // sealed inner type from the suffix, plaintext type out
+        d.extra = r->suffix;
+        d.extra_stride = suffix_len;
+        d.extra_out = r->types;
+        d.extra_out_stride = 1;
+      }
+    }
+    const KernelEvents *ev = timing_pair();
+    const int rc = ctx->aead->kind == kAeadAesGcm
+                       ? launch_gcm(static_cast<const GcmKeyDev *>(st->km->dev), d, !t->seal,
+                                    st->km->nr, stream, ev)
+                       : launch_chacha(static_cast<const ChaChaKeyDev *>(st->km->dev), d,
+                                       !t->seal, stream, ev);
+    t_timing.last_name = ctx->aead->kind == kAeadAesGcm ? "gcm_kernel" : "chacha_poly_kernel";
+    ok = rc == 0;
+    // TLS 1.2 open reports the header type (tls_record.cc:197-235).
+    if (ok && !t->seal && !t->tls13 && r->types)
+      ok = hipMemcpy2DAsync(r->types, 1, r->prefix, prefix_len, 1, n, hipMemcpyDeviceToDevice,
+                            s) == hipSuccess;
+  }
+  hipFreeAsync(buf, s);
+  if (!ok) {
+    PUT_ERROR(ERR_R_INTERNAL_ERROR);
+    return 0;
+  }
+  t->seq += n;
+  return 1;
+}
+
+}  // namespace
+
+extern "C" {
+
+BSSL_AMD_TLS_AEAD *BSSL_AMD_TLS_AEAD_new(enum evp_aead_direction_t direction, uint16_t version,
+                                         const EVP_AEAD *aead, const uint8_t *key,
+                                         size_t key_len, const uint8_t *fixed_iv,
+                                         size_t fixed_iv_len, uint64_t seq) {
+  // SSLAEADContext::Create (ssl_aead_ctx.cc:44-123), AEAD suites only.
+  if ((version != BSSL_AMD_TLS1_2_VERSION && version != BSSL_AMD_TLS1_3_VERSION) || !aead ||
+      !fixed_iv) {
+    PUT_ERROR(ERR_R_SHOULD_NOT_HAVE_BEEN_CALLED);
+    return nullptr;
+  }
+  const bool tls13 = version == BSSL_AMD_TLS1_3_VERSION;
+  const EVP_AEAD *rec_aead = tls_record_aead(aead, tls13);
+  if (!rec_aead) {
+    PUT_ERROR(CIPHER_R_UNSUPPORTED_KEY_SIZE);
+    return nullptr;
+  }
+  // TLS 1.3 and TLS 1.2 ChaCha20-Poly1305 XOR a 12-byte IV with the sequence
+  // number; TLS 1.2 AES-GCM prepends a 4-byte IV to an 8-byte explicit nonce.
+  const bool xor_nonce = tls13 || aead->kind == kAeadChaChaPoly;
+  if (fixed_iv_len != (xor_nonce ? 12u : 4u)) {
+    PUT_ERROR(CIPHER_R_INVALID_NONCE_SIZE);
+    return nullptr;
+  }
+  BSSL_AMD_TLS_AEAD *t = new (std::nothrow) bssl_amd_tls_aead_st;
+  if (!t) {
+    PUT_ERROR(ERR_R_MALLOC_FAILURE);
+    return nullptr;
+  }
+  EVP_AEAD_CTX_zero(&t->ctx);
+  if (!EVP_AEAD_CTX_init_with_direction(&t->ctx, rec_aead, key, key_len,
+                                        EVP_AEAD_DEFAULT_TAG_LENGTH, direction)) {
+    delete t;
+    return nullptr;
+  }
+  t->seal = direction == evp_aead_seal;
+  t->tls13 = tls13;
+  t->xor_nonce = xor_nonce;
+  t->explicit_len = xor_nonce ? 0 : 8;
+  memset(t->fixed_iv, 0, sizeof(t->fixed_iv));
+  memcpy(t->fixed_iv, fixed_iv, fixed_iv_len);
+  t->seq = seq;
+  return t;
+}
+
+void BSSL_AMD_TLS_AEAD_free(BSSL_AMD_TLS_AEAD *t) {
+  if (!t) return;
+  EVP_AEAD_CTX_cleanup(&t->ctx);
+  delete t;
+}
+
+size_t BSSL_AMD_TLS_AEAD_prefix_len(const BSSL_AMD_TLS_AEAD *t) { return 5 + t->explicit_len; }
+
+size_t BSSL_AMD_TLS_AEAD_suffix_len(const BSSL_AMD_TLS_AEAD *t) {
+  return (t->tls13 ? 1 : 0) + t->ctx.tag_len;
+}
+
+uint64_t BSSL_AMD_TLS_AEAD_sequence(const BSSL_AMD_TLS_AEAD *t) { return t->seq; }
+
+int BSSL_AMD_TLS_AEAD_seal_records_device(BSSL_AMD_TLS_AEAD *t, const BSSL_AMD_TLS_RECORDS *r,
+                                          void *hip_stream) {
+  if (t && !t->seal) {
+    PUT_ERROR(CIPHER_R_INVALID_OPERATION);
+    return 0;
+  }
+  return tls_records(t, r, hip_stream);
+}
+
+int BSSL_AMD_TLS_AEAD_open_records_device(BSSL_AMD_TLS_AEAD *t, const BSSL_AMD_TLS_RECORDS *r,
+                                          void *hip_stream) {
+  if (t && t->seal) {
+    PUT_ERROR(CIPHER_R_INVALID_OPERATION);
+    return 0;
+  }
+  return tls_records(t, r, hip_stream);
+}
 
 }  // extern "C"

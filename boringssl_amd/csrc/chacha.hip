@@ -260,6 +260,35 @@ __device__ __forceinline__ P preduce(PAcc a) {
   return o;
 }
 
+// A data block that reaches into the record's extra bytes (BatchDesc::extra;
+// at most one per record): byte k < len from/to the record, k >= len from/to
+// the extra arrays (XT kernels only).
+__device__ __forceinline__ void crypt_block_x(const uint8_t *src, uint8_t *dst, uint64_t len,
+                                           const uint8_t *xin, uint8_t *xout, uint64_t p0,
+                                           uint32_t n, const uint32_t *ks, uint32_t *x,
+                                           uint32_t *y) {
+  for (int i = 0; i < 16; i++) {
+    uint32_t w = 0;
+    for (uint32_t t = 0; t < 4; t++) {
+      const uint64_t k = p0 + 4 * i + t;
+      if (4u * i + t < n) w |= (uint32_t)(k < len ? src[k] : xin[k - len]) << (8 * t);
+    }
+    x[i] = w;
+    const uint32_t mask = n >= 4u * i + 4 ? 0xffffffffu
+                          : n <= 4u * i   ? 0u
+                                          : ((1u << (8 * (n - 4 * i))) - 1u);
+    y[i] = (w ^ ks[i]) & mask;
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    const uint64_t k = p0 + i;
+    const uint8_t cb = (uint8_t)(y[i >> 2] >> (8 * (i & 3)));
+    if (k < len)
+      dst[k] = cb;
+    else
+      xout[k - len] = cb;
+  }
+}
+
 // ChaCha20-Poly1305 over L lanes per record (64/L records per wave).
 // ChaCha blocks u = 0..nblk of a record are dealt round-robin to the lanes
 // (u = it*L + q): u = 0 is the Poly1305 key block (counter 0), u >= 1 the data
@@ -283,7 +312,7 @@ __device__ __forceinline__ P preduce(PAcc a) {
 #else
 #define CSTAMP(i)
 #endif
-template <bool OPEN, int L>
+template <bool OPEN, int L, bool XT>
 __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
     const ChaChaKeyDev *__restrict__ keys, BatchDesc b) {
 #if BSSL_AMD_CHACHA_STAMPS
@@ -308,7 +337,7 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
   }
   // e_chacha20poly1305.cc:127-142: 12-byte nonce, < 2^32 - 1 blocks.
   const bool bad = active && (kidx >= b.num_keys || b.nonce_len != 12 ||
-                              m.len >= (uint64_t(1) << 32) * 64 - 64 ||
+                              m.len + b.extra_len >= (uint64_t(1) << 32) * 64 - 64 ||
                               (b.valid && !b.valid[rec]));
   const bool live = active && !bad;
   uint32_t key[8], nonce[3];
@@ -320,8 +349,15 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
 #pragma unroll
     for (int i = 0; i < 3; i++) nonce[i] = load_le32_bytes(np + 4 * i, live ? 4 : 0);
   }
-  const uint64_t nblk = live ? (m.len + 63) / 64 : 0;  // ChaCha data blocks
-  const uint64_t npoly = live ? (m.len + 15) / 16 : 0;
+  // Message = the record's `in` bytes then b.extra_len extra bytes
+  // (BatchDesc::extra, the TLS 1.3 inner type), whose ciphertext goes to
+  // their own output.
+  const uint32_t xlen = XT ? b.extra_len : 0;
+  const uint64_t vlen = m.len + xlen;
+  const uint8_t *xin = xlen ? batch_extra_in(b, rec) : nullptr;
+  uint8_t *xout = xlen ? batch_extra_out(b, rec) : nullptr;
+  const uint64_t nblk = live ? (vlen + 63) / 64 : 0;  // ChaCha data blocks
+  const uint64_t npoly = live ? (vlen + 15) / 16 : 0;
   const uint64_t nunits = npoly / 4;                   // full 4-block units
   const uint32_t tail_blocks = (uint32_t)(npoly & 3);
   const uint8_t *src = b.in + m.off;
@@ -335,7 +371,7 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
   // (issued before the ChaCha rounds so the HBM latency hides under them).
   auto prefetch = [&](uint64_t u, uint4 pre[4]) {
     const uint64_t d = u - 1;
-    if (u >= 1 && u <= nblk && aligned && m.len - 64 * d >= 64) {
+    if (u >= 1 && u <= nblk && aligned && m.len >= 64 * d + 64) {
       const uint4 *sp = reinterpret_cast<const uint4 *>(src + 64 * d);
 #pragma unroll
       for (int i = 0; i < 4; i++) pre[i] = sp[i];
@@ -343,9 +379,9 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
   };
   auto crypt_block = [&](uint64_t u, const uint32_t ks[16], const uint4 pre[4], uint32_t c[16]) {
     const uint64_t d = u - 1;
-    const uint64_t rem = m.len - 64 * d;
+    const uint64_t rem = vlen - 64 * d;
     uint32_t x[16], y[16];
-    if (rem >= 64 && aligned) {
+    if (m.len >= 64 * d + 64 && aligned) {
       uint4 *dp = reinterpret_cast<uint4 *>(dst + 64 * d);
 #pragma unroll
       for (int i = 0; i < 4; i++) {
@@ -357,7 +393,7 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
 #pragma unroll
       for (int i = 0; i < 4; i++)
         dp[i] = make_uint4(y[4 * i], y[4 * i + 1], y[4 * i + 2], y[4 * i + 3]);
-    } else {
+    } else if (!XT) {
       const uint8_t *sp = src + 64 * d;
       uint8_t *dp = dst + 64 * d;
       const uint32_t n = (uint32_t)min<uint64_t>(rem, 64);
@@ -370,6 +406,9 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
         y[i] = (x[i] ^ ks[i]) & mask;
       }
       for (uint32_t i = 0; i < n; i++) dp[i] = (uint8_t)(y[i >> 2] >> (8 * (i & 3)));
+    } else {
+      crypt_block_x(src, dst, m.len, xin, xout, 64 * d, (uint32_t)min<uint64_t>(rem, 64), ks, x,
+                    y);
     }
 #pragma unroll
     for (int i = 0; i < 16; i++) c[i] = OPEN ? x[i] : y[i];
@@ -536,14 +575,14 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
     if ((uint32_t)k < tail_blocks) z = pmul(z, pwr(0));
   if (tail_blocks) z = padd(z, tail);
   // h = ((Z r) + L) r with L = le64(ad_len) || le64(ct_len) (+2^128).
-  const P lb = pblock((uint32_t)m.ad_len, (uint32_t)(m.ad_len >> 32), (uint32_t)m.len,
-                      (uint32_t)(m.len >> 32));
+  const P lb = pblock((uint32_t)m.ad_len, (uint32_t)(m.ad_len >> 32), (uint32_t)vlen,
+                      (uint32_t)(vlen >> 32));
   const P rr = pwr(0);
   const P h = pmul(padd(pmul(z, rr), lb), rr);
   uint32_t tag[4];
   poly_finish(h, s, tag);
 
-  uint8_t *tagp = b.tags + rec * b.tag_len;
+  uint8_t *tagp = batch_tag(b, rec);
   int ok = live;
   if (q == 0) {
     if (OPEN && live) {
@@ -565,6 +604,8 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
       const uint64_t n = min<uint64_t>(m.len - j * 16, 16);
       for (uint64_t i = 0; i < n; i++) dst[j * 16 + i] = 0;
     }
+    if (q == 0)
+      for (uint32_t i = 0; i < xlen; i++) xout[i] = 0;
   }
 #if BSSL_AMD_CHACHA_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
@@ -603,12 +644,18 @@ int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, void 
     bo.order = order;
   }
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
-  if (open)
-    hipLaunchKernelGGL((chacha_poly_kernel<true, L>), dim3((unsigned)blocks), dim3(kThreads), 0, s,
-                       keys, bo);
+  if (open && b.extra_len)
+    hipLaunchKernelGGL((chacha_poly_kernel<true, L, true>), dim3((unsigned)blocks),
+                       dim3(kThreads), 0, s, keys, bo);
+  else if (open)
+    hipLaunchKernelGGL((chacha_poly_kernel<true, L, false>), dim3((unsigned)blocks),
+                       dim3(kThreads), 0, s, keys, bo);
+  else if (b.extra_len)
+    hipLaunchKernelGGL((chacha_poly_kernel<false, L, true>), dim3((unsigned)blocks),
+                       dim3(kThreads), 0, s, keys, bo);
   else
-    hipLaunchKernelGGL((chacha_poly_kernel<false, L>), dim3((unsigned)blocks), dim3(kThreads), 0,
-                       s, keys, bo);
+    hipLaunchKernelGGL((chacha_poly_kernel<false, L, false>), dim3((unsigned)blocks),
+                       dim3(kThreads), 0, s, keys, bo);
   const int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
   if (order) hipFreeAsync(order, s);

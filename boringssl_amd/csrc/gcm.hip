@@ -616,8 +616,11 @@ __device__ __forceinline__ int wave_max(int v) {
   return v;
 }
 
+// len = the record's `in` bytes; xlen = extra bytes sealed after them
+// (BatchDesc::extra), so the message is len + xlen bytes.
 struct RecordMeta {
   uint64_t off, len, ad_off, ad_len;
+  uint32_t xlen;
 };
 
 __device__ __forceinline__ RecordMeta record_meta(const BatchDesc &b, uint64_t i) {
@@ -626,7 +629,45 @@ __device__ __forceinline__ RecordMeta record_meta(const BatchDesc &b, uint64_t i
   m.len = b.lengths ? b.lengths[i] : b.record_len;
   m.ad_off = b.ad_offsets ? b.ad_offsets[i] : i * b.ad_stride;
   m.ad_len = b.ad_lengths ? b.ad_lengths[i] : b.ad_len;
+  m.xlen = b.extra_len;
   return m;
+}
+
+// Bytes [p0, p0 + n) of a record's message: `in` bytes below len, then the
+// extra bytes (load), and the same split for the output (store).
+__device__ __forceinline__ uint4 load_partial_x(const uint8_t *src, uint64_t len,
+                                                const uint8_t *x, uint64_t p0, uint32_t n) {
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (uint32_t i = 0; i < n; i++) {
+    const uint64_t k = p0 + i;
+    w[i >> 2] |= (uint32_t)(k < len ? src[k] : x[k - len]) << (8 * (i & 3));
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void store_partial_x(uint8_t *dst, uint64_t len, uint8_t *x,
+                                                uint64_t p0, uint4 v, uint32_t n) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  for (uint32_t i = 0; i < n; i++) {
+    const uint64_t k = p0 + i;
+    const uint8_t c = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    if (k < len)
+      dst[k] = c;
+    else
+      x[k - len] = c;
+  }
+}
+
+// The block of a record that reaches into its extra bytes (one per record at
+// most; only in the XT kernels).  Returns the masked output block; `x`
+// receives the input block.
+__device__ __forceinline__ uint4 crypt_partial_x(const uint8_t *src, uint8_t *dst, uint64_t len,
+                                              const uint8_t *xin, uint8_t *xout, uint64_t p0,
+                                              uint4 ks, uint32_t n, uint4 &x) {
+  x = load_partial_x(src, len, xin, p0, n);
+  const uint4 y = mask_block(make_uint4(x.x ^ ks.x, x.y ^ ks.y, x.z ^ ks.z, x.w ^ ks.w), n);
+  store_partial_x(dst, len, xout, p0, y, n);
+  return y;
 }
 
 // Record at processing position i (sched.hip's length order, if any).
@@ -664,7 +705,8 @@ __global__ __launch_bounds__(256) void gcm_prologue(const GcmKeyDev *__restrict_
   const uint32_t k = b.key_index ? b.key_index[rec] : 0u;
   // e_aes.cc.inc:790 (empty nonce), gcm.cc.inc:368,409 (length limits).
   const bool live = k < b.num_keys && b.nonce_len != 0 &&
-                    m.len <= ((uint64_t(1) << 36) - 32) && m.ad_len <= (uint64_t(1) << 61) &&
+                    m.len + m.xlen <= ((uint64_t(1) << 36) - 32) &&
+                    m.ad_len <= (uint64_t(1) << 61) &&
                     (!b.valid || b.valid[rec]);  // tls12/tls13 nonce check (tls_scan.hip)
   RecState s;
   s.live = live;
@@ -734,7 +776,7 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
     if ((q & (2 * sh - 1)) == 0) a = xor4(mlt, o);
   }
   // Tag (gcm.cc.inc:576-604): ((Z*H) ^ len block) * H ^ E_K(J0), in lane 0.
-  const uint64_t abits = m.ad_len << 3, cbits = m.len << 3;
+  const uint64_t abits = m.ad_len << 3, cbits = (m.len + m.xlen) << 3;
   uint4 add = make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
                          bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits));
 #pragma unroll 1
@@ -744,7 +786,7 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
   }
   const uint4 tag = a;
 
-  uint8_t *tagp = b.tags + rec * b.tag_len;
+  uint8_t *tagp = batch_tag(b, rec);
   int ok = live;
   if (q == 0) {
     if (OPEN && live) {
@@ -771,6 +813,8 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
       const uint32_t n = (uint32_t)min<uint64_t>(m.len - j * 16, 16);
       store_partial(dst + j * 16, make_uint4(0, 0, 0, 0), n);
     }
+    if (q == 0)
+      for (uint32_t i = 0; i < m.xlen; i++) batch_extra_out(b, rec)[i] = 0;
   }
 }
 
@@ -779,7 +823,7 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
 // Bulk kernel: CTR keystream + GHASH + tag for the (up to) 4 records of a
 // wave, 16 lanes per record.  `active` is per group (record in this key pass).
 // `gtab` = the key's nibble tables in global memory (record-end tree only).
-template <int NR, bool OPEN>
+template <int NR, bool OPEN, bool XT>
 __device__ __forceinline__ void process_records(const RoundKeys &rk, const BatchDesc &b,
                                                 const RecState *__restrict__ st, uint64_t rec,
                                                 bool active, const uint8_t *smem,
@@ -790,7 +834,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   uint64_t *stv = stamps.v;
 #endif
   const int q = threadIdx.x & 15;
-  RecordMeta m = {0, 0, 0, 0};
+  RecordMeta m = {0, 0, 0, 0, 0};
   RecState s;
   s.j0 = s.ek0 = s.ya = make_uint4(0, 0, 0, 0);
   s.live = 0;
@@ -799,8 +843,13 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     s = st[rec];
   }
   const bool live = active && s.live;
-  const uint64_t nb = live ? (m.len + 15) / 16 : 0;
+  if constexpr (!XT) m.xlen = 0;  // (the launcher picks XT iff extra_len != 0)
+  const uint64_t nb = live ? (m.len + m.xlen + 15) / 16 : 0;
   const uint32_t ctr0 = bswap32(s.j0.w);
+  // Extra bytes after the record (TLS 1.3 inner type, XT kernels): read from /
+  // written to their own arrays by the byte path (BatchDesc::extra).
+  const uint8_t *xin = XT ? batch_extra_in(b, rec) : nullptr;
+  uint8_t *xout = XT ? batch_extra_out(b, rec) : nullptr;
   // Round 0 of the counter blocks: words 0..2 are constant per record.
   const uint32_t c0 = s.j0.x ^ rk.w[0][0], c1 = s.j0.y ^ rk.w[0][1], c2 = s.j0.z ^ rk.w[0][2];
   const uint8_t *src = b.in + m.off;
@@ -897,10 +946,14 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
       *reinterpret_cast<uint4 *>(dst + j * 16) = y;
 #endif
     } else if (j < nb) {
-      const uint32_t n = (uint32_t)min<uint64_t>(m.len - j * 16, 16);
-      x = load_partial(src + j * 16, n);
-      y = mask_block(xor4(x, ks), n);
-      store_partial(dst + j * 16, y, n);
+      const uint32_t n = (uint32_t)min<uint64_t>(m.len + m.xlen - j * 16, 16);
+      if constexpr (XT) {
+        y = crypt_partial_x(src, dst, m.len, xin, xout, j * 16, ks, n, x);
+      } else {
+        x = load_partial(src + j * 16, n);
+        y = mask_block(xor4(x, ks), n);
+        store_partial(dst + j * 16, y, n);
+      }
     }
     if (j < nb) {
 #if BSSL_AMD_ABLATE == 1  // diagnostic build: no GHASH multiply (wrong tags)
@@ -949,7 +1002,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, gtab, mf0);
 }
 
-template <int NR, bool OPEN>
+template <int NR, bool OPEN, bool XT>
 __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restrict__ keys,
                                                       BatchDesc b,
                                                       const RecState *__restrict__ st,
@@ -1006,7 +1059,7 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
       if (first >= n) break;
       const uint64_t i = first + g;
       const bool active = i < n;
-      process_records<NR, OPEN>(rk, b, st, active ? rec_at(b, i) : 0, active, smem, gtab, lc0,
+      process_records<NR, OPEN, XT>(rk, b, st, active ? rec_at(b, i) : 0, active, smem, gtab, lc0,
                                 lc1, mf0, stamps);
     }
 #if BSSL_AMD_GCM_STAMPS
@@ -1066,7 +1119,7 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
         for (int c = 0; c < 4; c++) rk.w[r][c] = keys[k].rk[r][c];
       const int t = wave * kRecPerWave + g;
       const bool active = (mask >> t) & 1;
-      process_records<NR, OPEN>(rk, b, st, active ? rec_at(b, base + t) : 0, active, smem, gtab,
+      process_records<NR, OPEN, XT>(rk, b, st, active ? rec_at(b, base + t) : 0, active, smem, gtab,
                                 lc0, lc1, mf0, stamps);
     }
   }
@@ -1162,7 +1215,7 @@ __device__ __forceinline__ void process_records_bs(const GcmKeyDev *__restrict__
   BS_STAMP(0);
   static_assert(L == 8 || L == 16 || L == 32, "lanes per record");
   const int q = threadIdx.x & (L - 1);
-  RecordMeta m = {0, 0, 0, 0};
+  RecordMeta m = {0, 0, 0, 0, 0};
   RecState s;
   s.j0 = s.ek0 = s.ya = make_uint4(0, 0, 0, 0);
   s.live = 0;
@@ -1340,7 +1393,7 @@ int g_num_cus = 0;
 int bs_lanes(const BatchDesc &b) {
   const char *e = getenv("BSSL_AMD_GCM_BS");
   const int enabled = e ? atoi(e) : 0;
-  if (!enabled || b.lengths || b.offsets) return 0;
+  if (!enabled || b.lengths || b.offsets || b.extra_len || b.tag_stride) return 0;
   if ((b.record_len | b.record_stride | reinterpret_cast<uintptr_t>(b.in) |
        reinterpret_cast<uintptr_t>(b.out)) & 15)
     return 0;
@@ -1397,8 +1450,12 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
   } else {
     const uint64_t tiles = (b.num_records + kRecPerTile - 1) / kRecPerTile;
     const unsigned grid = (unsigned)(tiles < (uint64_t)g_num_cus ? tiles : (uint64_t)g_num_cus);
-    hipLaunchKernelGGL((gcm_kernel<NR, OPEN>), dim3(grid), dim3(kThreads), 0, s, keys, bo,
-                       (const RecState *)st, units);
+    if (b.extra_len)
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, true>), dim3(grid), dim3(kThreads), 0, s, keys, bo,
+                         (const RecState *)st, units);
+    else
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false>), dim3(grid), dim3(kThreads), 0, s, keys, bo,
+                         (const RecState *)st, units);
   }
   int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);

@@ -73,7 +73,30 @@ struct BatchDesc {
   // null: the tls12/tls13 nonce checks of tls_scan.hip.  A record with flag 0
   // fails like a reference call that returned 0 (zeroed output, status 0).
   const uint8_t *valid;
+  // Extra trailing message bytes (the reference's `extra_in` of seal_scatter,
+  // aead.cc.inc:163-209; the TLS 1.3 inner content type): extra_len bytes per
+  // record, read at extra + i*extra_stride and sealed (opened) after the
+  // record's `in` bytes; their output goes to extra_out + i*extra_out_stride.
+  // Tags are at tags + i*tag_stride (0 = tag_len).  Set by the TLS record
+  // layer only; the public batch leaves them 0/null.
+  const uint8_t *extra;
+  uint8_t *extra_out;
+  uint32_t extra_len;
+  uint32_t extra_stride;
+  uint32_t extra_out_stride;
+  uint32_t tag_stride;
 };
+
+// Tag / extra addresses of record i.
+inline __host__ __device__ uint8_t *batch_tag(const BatchDesc &b, uint64_t i) {
+  return b.tags + i * (b.tag_stride ? b.tag_stride : b.tag_len);
+}
+inline __host__ __device__ const uint8_t *batch_extra_in(const BatchDesc &b, uint64_t i) {
+  return b.extra + i * b.extra_stride;
+}
+inline __host__ __device__ uint8_t *batch_extra_out(const BatchDesc &b, uint64_t i) {
+  return b.extra_out + i * b.extra_out_stride;
+}
 
 // HIP events recorded on the launch stream immediately before and after the
 // dominant (bulk) kernel of a batch, for kernel-level timing.
@@ -98,9 +121,32 @@ int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open,
                   void *stream, const KernelEvents *ev);
 // tls12 / tls13 nonce checks over a batch of seal calls (tls_scan.hip):
 // writes valid[i] (device) and advances the context's nonce state in place
-// (min_next_nonce, mask); synchronises `stream`.  Returns 0 or an error code.
+// (min_next_nonce, mask); synchronises `stream`.  and_into: valid[i] &= the
+// check instead of =.  Returns 0 or an error code.
 int tls_nonce_scan(const uint8_t *nonces, uint64_t n, int tls, uint64_t *min_next,
-                   uint64_t *mask, uint8_t *valid, void *stream);
+                   uint64_t *mask, uint8_t *valid, int and_into, void *stream);
+// TLS record layer (tls_records.hip): per-record nonce, header/prefix, AD and
+// inner type of a batch of records with sequence numbers seq .. seq + n - 1.
+struct TlsPrepare {
+  uint64_t n;
+  const uint64_t *lengths;  // or record_len for all
+  uint64_t record_len;
+  const uint8_t *types;     // or `type` for all
+  uint8_t type;
+  uint8_t fixed_iv[12];
+  uint64_t seq;
+  int xor_nonce;            // fixed_iv XOR seq (TLS 1.3, TLS 1.2 ChaCha) vs fixed || seq
+  int tls13;
+  uint16_t record_version;  // header and TLS 1.2 AD version (0x0303)
+  uint32_t explicit_len;    // 8 for TLS 1.2 AES-GCM, else 0
+  uint32_t extra_len;       // 1 for TLS 1.3 (inner type), else 0
+  uint32_t tag_len;
+  uint32_t prefix_len;      // 5 + explicit_len
+  uint32_t ad_stride;       // 13 (TLS 1.2) or 5 (TLS 1.3)
+  int open;                 // records are received: header/explicit nonce read from prefix
+  uint8_t *nonces, *prefix, *ad, *extra, *valid;
+};
+int launch_tls_prepare(const TlsPrepare &p, void *stream);
 int launch_synth(uint64_t first, size_t n, const uint64_t *offsets,
                  const uint64_t *lengths, uint8_t *pt, uint8_t *nonces,
                  uint8_t *ads, void *stream);

@@ -43,13 +43,14 @@ __global__ void tls_counters(const uint8_t *__restrict__ nonces, uint64_t n,
 
 __global__ void tls_valid(const uint8_t *__restrict__ nonces, uint64_t n,
                           const uint64_t *__restrict__ state, const uint64_t *__restrict__ prefix,
-                          uint8_t *__restrict__ valid) {
+                          uint8_t *__restrict__ valid, int and_into) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const bool first = !state[2];  // tls13 first call: record 0 sets the mask
   const uint64_t mask = first ? be64(nonces + 4) : state[1];
   const uint64_t c = be64(nonces + 12 * i + 4) ^ mask;
-  valid[i] = ((first && i == 0) || (c != kMax && c >= prefix[i])) ? 1 : 0;
+  const uint8_t ok = ((first && i == 0) || (c != kMax && c >= prefix[i])) ? 1 : 0;
+  valid[i] = and_into ? (uint8_t)(valid[i] & ok) : ok;
 }
 
 __global__ void tls_final(const uint8_t *__restrict__ nonces, uint64_t n,
@@ -72,7 +73,7 @@ struct MaxOp {
 }  // namespace
 
 int tls_nonce_scan(const uint8_t *nonces, uint64_t n, int tls, uint64_t *min_next,
-                   uint64_t *mask, uint8_t *valid, void *stream) {
+                   uint64_t *mask, uint8_t *valid, int and_into, void *stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (n == 0) return 0;
   // tls13 before its first call: min_next_nonce == 0, mask unknown.
@@ -102,7 +103,8 @@ int tls_nonce_scan(const uint8_t *nonces, uint64_t n, int tls, uint64_t *min_nex
       rc = 1;
   }
   if (!rc) {
-    hipLaunchKernelGGL(tls_valid, dim3(grid), dim3(256), 0, s, nonces, n, d_state, prefix, valid);
+    hipLaunchKernelGGL(tls_valid, dim3(grid), dim3(256), 0, s, nonces, n, d_state, prefix, valid,
+                       and_into);
     hipLaunchKernelGGL(tls_final, dim3(1), dim3(1), 0, s, nonces, n, prefix, x, d_state);
     uint64_t out[3];
     // The context's nonce state lives on the host (as the reference's lives in

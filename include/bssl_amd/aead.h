@@ -167,6 +167,7 @@ BSSL_AMD_EXPORT void ERR_clear_error(void);
 #define CIPHER_R_BUFFER_TOO_SMALL 103
 #define CIPHER_R_CTRL_NOT_IMPLEMENTED 104
 #define CIPHER_R_INVALID_NONCE_SIZE 111
+#define CIPHER_R_INVALID_OPERATION 112  /* cipher.h:804 */
 #define CIPHER_R_NO_DIRECTION_SET 124
 #define CIPHER_R_OUTPUT_ALIASES_INPUT 115
 #define CIPHER_R_TAG_TOO_LARGE 116

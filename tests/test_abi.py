@@ -10,11 +10,11 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "bssl_amd", "aead.h")
+HEADERS = [os.path.join(ROOT, "include", "bssl_amd", h) for h in ("aead.h", "tls.h")]
 
 
 def header_functions():
-    text = open(HEADER).read()
+    text = "\n".join(open(h).read() for h in HEADERS)
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     text = "\n".join(l for l in text.splitlines() if not l.lstrip().startswith("#"))
     names = re.findall(r"BSSL_AMD_EXPORT[^;(]*?\b(\w+)\s*\(", text, flags=re.S)

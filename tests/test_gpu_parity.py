@@ -567,3 +567,121 @@ def test_tls_batch_rejections():
     with pytest.raises(ba.AEADError) as e:
         ctx.seal_batch_device(ba.make_batch(1, d, d, d, d, 8, d, record_len=16, record_stride=16))
     assert e.value.reason == ba.CIPHER_R_UNSUPPORTED_NONCE_SIZE
+
+
+# ---------------------------------------------------------------------------
+# TLS record layer (include/bssl_amd/tls.h) against a restatement of the
+# reference's do_seal_record (ssl/tls_record.cc:266-317) and
+# SSLAEADContext::SealScatter / GetAdditionalData (ssl/ssl_aead_ctx.cc:207-380)
+# on top of the oracle's AEAD.
+
+def _tls_seal_oracle(version, aead, key, fixed_iv, seq0, records, types):
+    tls13 = version == ba.TLS1_3_VERSION
+    chacha = aead == "chacha20-poly1305"
+    aid = o.CHACHA20_POLY1305 if chacha else o.AES_GCM
+    out = []
+    for i, (pt, typ) in enumerate(zip(records, types)):
+        seq = (seq0 + i).to_bytes(8, "big")
+        if tls13 or chacha:  # ssl_aead_ctx.cc:96-103, 326-336, 367-373
+            nonce, explicit = bytes(a ^ b for a, b in zip(fixed_iv, bytes(4) + seq)), b""
+        else:                # fixed IV || explicit nonce in the record (:104-110, 355-365)
+            nonce, explicit = fixed_iv + seq, seq
+        extra = bytes([typ]) if tls13 else b""  # tls_record.cc:272-276
+        ctlen = len(explicit) + len(pt) + len(extra) + 16
+        hdr = bytes([23 if tls13 else typ, 3, 3, ctlen >> 8, ctlen & 0xff])  # :287-298
+        ad = hdr if tls13 else seq + bytes([typ, 3, 3]) + len(pt).to_bytes(2, "big")  # :207-224
+        if len(pt) > 16384:
+            out.append(None)
+            continue
+        ok, ct, tag = o.seal(aid, key, nonce, pt + extra, ad)
+        assert ok
+        out.append((hdr + explicit, ct[:len(pt)], ct[len(pt):] + tag))
+    return out
+
+
+@pytest.mark.parametrize("version,aead", [(0x0303, "aes-128-gcm"), (0x0303, "aes-256-gcm"),
+                                          (0x0303, "chacha20-poly1305"), (0x0304, "aes-128-gcm"),
+                                          (0x0304, "aes-256-gcm"),
+                                          (0x0304, "chacha20-poly1305")])
+def test_tls_record_layer(version, aead):
+    rng = random.Random(version * 31 + len(aead))
+    key = bytes(rng.getrandbits(8) for _ in range(16 if "128" in aead else 32))
+    xor = version == 0x0304 or aead == "chacha20-poly1305"
+    fixed_iv = bytes(rng.getrandbits(8) for _ in range(12 if xor else 4))
+    # TLS 1.3 traffic keys start at sequence number 0 (RFC 8446 5.3); the tls13
+    # AEAD's nonce check takes the first nonce as the mask on that basis
+    # (e_aes.cc.inc:1181-1185), so only TLS 1.2 starts mid-stream here.
+    seq0 = 0 if version == 0x0304 else rng.getrandbits(40)
+    n = 300
+    lens = [rng.choice([0, 1, 15, 16, 17, 31, 64, 100, 1350, 4096, 16384]) for _ in range(n)]
+    lens[7] = 16385  # over SSL3_RT_MAX_PLAIN_LENGTH: that record fails
+    records = [bytes(rng.getrandbits(8) for _ in range(L)) for L in lens]
+    types = [rng.choice([21, 22, 23]) for _ in range(n)]
+    expect = _tls_seal_oracle(version, aead, key, fixed_iv, seq0, records, types)
+
+    sealer = ba.TlsAead(ba.evp_aead_seal, version, aead, key, fixed_iv, seq0)
+    pl, sl = sealer.prefix_len, sealer.suffix_len
+    assert pl == (5 if xor else 13) and sl == (17 if version == 0x0304 else 16)
+    inbuf, offs = _pack(records)
+    d_in = _t(inbuf)
+    d_body = torch.full_like(d_in, 0x5a)
+    d_pre = torch.full((n * pl,), 0x5a, dtype=torch.uint8, device=DEV)
+    d_suf = torch.full((n * sl,), 0x5a, dtype=torch.uint8, device=DEV)
+    d_types = _t(np.array(types, np.uint8))
+    d_st = torch.full((n,), 7, dtype=torch.uint8, device=DEV)
+    d_offs, d_lens = _t(offs.astype(np.int64)), _t(np.array(lens, np.int64))
+    # Two batches on one context: the sequence number carries over.
+    h = n // 2
+    for lo, hi in ((0, h), (h, n)):
+        r = ba.make_tls_records(hi - lo, d_in, d_body, d_pre[lo * pl:], d_suf[lo * sl:],
+                                offsets=d_offs[lo:], lengths=d_lens[lo:], types=d_types[lo:],
+                                status=d_st[lo:])
+        sealer.seal_records_device(r)
+    torch.cuda.synchronize()
+    assert sealer.sequence == seq0 + n
+    body, pre, suf = d_body.cpu().numpy(), d_pre.cpu().numpy(), d_suf.cpu().numpy()
+    st = d_st.cpu().numpy()
+    for i in range(n):
+        b = body[int(offs[i]):int(offs[i]) + lens[i]].tobytes()
+        if expect[i] is None:
+            assert st[i] == 0 and b == bytes(lens[i]), i
+            continue
+        e_pre, e_body, e_suf = expect[i]
+        assert st[i] == 1, i
+        assert pre[i * pl:(i + 1) * pl].tobytes() == e_pre, i
+        assert b == e_body, i
+        assert suf[i * sl:(i + 1) * sl].tobytes() == e_suf, i
+
+    # Open the wire records (in place) with a reader at the same sequence.
+    d_suf_bad = d_suf.clone()
+    d_suf_bad[3 * sl] ^= 1  # record 3: corrupted (TLS 1.3: its sealed inner type)
+    opener = ba.TlsAead(ba.evp_aead_open, version, aead, key, fixed_iv, seq0)
+    d_otypes = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    d_st2 = torch.full((n,), 7, dtype=torch.uint8, device=DEV)
+    r = ba.make_tls_records(n, d_body, d_body, d_pre, d_suf_bad, offsets=d_offs, lengths=d_lens,
+                            types=d_otypes, status=d_st2)
+    opener.open_records_device(r)
+    torch.cuda.synchronize()
+    body2, st2, ot = d_body.cpu().numpy(), d_st2.cpu().numpy(), d_otypes.cpu().numpy()
+    for i in range(n):
+        b = body2[int(offs[i]):int(offs[i]) + lens[i]].tobytes()
+        if expect[i] is None or i == 3:
+            assert st2[i] == 0 and b == bytes(lens[i]), i
+            continue
+        assert st2[i] == 1 and b == records[i] and ot[i] == types[i], i
+
+
+def test_tls_record_layer_errors():
+    key, iv = bytes(16), bytes(12)
+    with pytest.raises(ba.AEADError) as e:  # TLS 1.2 AES-GCM wants a 4-byte fixed IV
+        ba.TlsAead(ba.evp_aead_seal, 0x0303, "aes-128-gcm", key, iv)
+    assert e.value.reason == ba.CIPHER_R_INVALID_NONCE_SIZE
+    t = ba.TlsAead(ba.evp_aead_seal, 0x0304, "aes-128-gcm", key, iv, seq=(1 << 64) - 2)
+    d = torch.zeros(64, dtype=torch.uint8, device=DEV)
+    r = ba.make_tls_records(2, d, d, d, d, record_len=0, record_stride=16)
+    with pytest.raises(ba.AEADError):  # the sequence number would wrap (tls_record.cc:305)
+        t.seal_records_device(r)
+    assert t.sequence == (1 << 64) - 2
+    with pytest.raises(ba.AEADError) as e:
+        t.open_records_device(r)
+    assert e.value.reason == ba.CIPHER_R_INVALID_OPERATION
