@@ -4,7 +4,8 @@ buffers): pinned host buffers -> hipMemcpyAsync H2D -> batch seal ->
 hipMemcpyAsync D2H, pipelined over NSTREAMS streams in chunks.  Reported in
 DESIGN.md; never the bench `value` (which is device-resident).
 
-Usage: python tools/e2e_bench.py [--records 262144] [--chunk 16384] [--streams 3]
+Usage: python tools/e2e_bench.py [--records 262144] [--chunk 4096] [--streams 4]
+(--streams = ring slots; uploads, seals and downloads each have one stream).
 """
 import argparse
 import json
@@ -25,8 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="config2")
     ap.add_argument("--records", type=int, default=262144)
-    ap.add_argument("--chunk", type=int, default=16384)
-    ap.add_argument("--streams", type=int, default=3)
+    ap.add_argument("--chunk", type=int, default=4096)
+    ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -54,9 +55,14 @@ def main():
         h_ad[s0 * 13:(s0 + m) * 13].copy_(da)
     torch.cuda.synchronize()
     ctx = ba.AEADCtx(aead, bench.synth_key(0, key_len), 16)
-    streams = [torch.cuda.Stream() for _ in range(args.streams)]
+    # Three engines, one stream each: uploads, seals, downloads.  A ring of
+    # `slots` device buffers; chunk i uses slot i % slots, so its upload waits
+    # for the download of chunk i - slots (event), the seal for its upload and
+    # the download for its seal.  Both DMA directions stay busy.
+    nslots = max(2, args.streams)
+    s_up, s_seal, s_down = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
     slots = []
-    for _ in range(args.streams):
+    for _ in range(nslots):
         slots.append(dict(pt=torch.empty(c * stride, dtype=torch.uint8, device=dev),
                           ct=torch.empty(c * stride, dtype=torch.uint8, device=dev),
                           tags=torch.empty(c * 16, dtype=torch.uint8, device=dev),
@@ -64,18 +70,34 @@ def main():
                           ad=torch.empty(c * 13, dtype=torch.uint8, device=dev)))
 
     def run():
-        for i, s0 in enumerate(range(0, n, c)):
+        chunks = list(range(0, n, c))
+        freed = [None] * nslots
+        for i, s0 in enumerate(chunks):
             m = min(c, n - s0)
-            st, sl = streams[i % len(streams)], slots[i % len(streams)]
-            with torch.cuda.stream(st):
+            k = i % nslots
+            sl = slots[k]
+            with torch.cuda.stream(s_up):
+                if freed[k] is not None:
+                    s_up.wait_event(freed[k])
                 sl["pt"][:m * stride].copy_(h_pt[s0 * stride:(s0 + m) * stride], non_blocking=True)
                 sl["nonce"][:m * 12].copy_(h_nonce[s0 * 12:(s0 + m) * 12], non_blocking=True)
                 sl["ad"][:m * 13].copy_(h_ad[s0 * 13:(s0 + m) * 13], non_blocking=True)
+                up = torch.cuda.Event()
+                up.record(s_up)
+            with torch.cuda.stream(s_seal):
+                s_seal.wait_event(up)
                 b = ba.make_batch(m, sl["pt"], sl["ct"], sl["tags"], sl["nonce"], 12, sl["ad"],
                                   record_stride=stride, record_len=length, ad_stride=13, ad_len=13)
-                ctx.seal_batch_device(b, st)
+                ctx.seal_batch_device(b, s_seal)
+                sealed = torch.cuda.Event()
+                sealed.record(s_seal)
+            with torch.cuda.stream(s_down):
+                s_down.wait_event(sealed)
                 h_ct[s0 * stride:(s0 + m) * stride].copy_(sl["ct"][:m * stride], non_blocking=True)
                 h_tags[s0 * 16:(s0 + m) * 16].copy_(sl["tags"][:m * 16], non_blocking=True)
+                done = torch.cuda.Event()
+                done.record(s_down)
+                freed[k] = done
         torch.cuda.synchronize()
 
     run()
@@ -90,11 +112,24 @@ def main():
     h2d = n * stride / (time.perf_counter() - t0) / 2**30
     t0 = time.perf_counter(); h_ct.copy_(d_big, non_blocking=True); torch.cuda.synchronize()
     d2h = n * stride / (time.perf_counter() - t0) / 2**30
+    # Both directions at once on two streams (the ceiling for the pipeline:
+    # each record crosses PCIe twice).
+    s_in, s_out = torch.cuda.Stream(), torch.cuda.Stream()
+    d_big2 = torch.empty(n * stride, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(s_in):
+        d_big2.copy_(h_pt, non_blocking=True)
+    with torch.cuda.stream(s_out):
+        h_ct.copy_(d_big, non_blocking=True)
+    torch.cuda.synchronize()
+    duplex = n * stride / (time.perf_counter() - t0) / 2**30  # per direction
     best = min(times)
     print(json.dumps({"e2e_gib_per_s": round(n * length / best / 2**30, 2),
                       "records": n, "record_bytes": length, "chunk_records": c,
                       "streams": args.streams, "h2d_gib_per_s": round(h2d, 2),
-                      "d2h_gib_per_s": round(d2h, 2), "times_s": [round(t, 4) for t in times]}))
+                      "d2h_gib_per_s": round(d2h, 2),
+                      "duplex_per_direction_gib_per_s": round(duplex, 2), "times_s": [round(t, 4) for t in times]}))
 
 
 if __name__ == "__main__":
