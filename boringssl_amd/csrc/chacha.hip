@@ -312,9 +312,10 @@ __device__ __forceinline__ void crypt_block_x(const uint8_t *src, uint8_t *dst, 
 #else
 #define CSTAMP(i)
 #endif
+// One wave group: records pos = grp * (64 / L) + lane / L.
 template <bool OPEN, int L, bool XT>
-__global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
-    const ChaChaKeyDev *__restrict__ keys, BatchDesc b) {
+__device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ keys,
+                                             const BatchDesc &b, uint64_t grp) {
 #if BSSL_AMD_CHACHA_STAMPS
   uint64_t ts[5] = {0, 0, 0, 0, 0};
 #endif
@@ -323,7 +324,7 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
   constexpr int kLog = L == 2 ? 1 : L == 4 ? 2 : L == 8 ? 3 : 4;
   const int lane = threadIdx.x & 63;
   const int q = lane & (L - 1);
-  const uint64_t pos = ((uint64_t)blockIdx.x * kThreads + threadIdx.x) / L;
+  const uint64_t pos = grp * (64 / L) + lane / L;
   const bool active = pos < b.num_records;
   const uint64_t rec = active && b.order ? b.order[pos] : pos;  // sched.hip order
   RecordMeta m = {0, 0, 0, 0};
@@ -347,7 +348,23 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
     for (int i = 0; i < 8; i++) key[i] = kp->k[i];
     const uint8_t *np = b.nonces + (live ? rec * 12 : 0);
 #pragma unroll
-    for (int i = 0; i < 3; i++) nonce[i] = load_le32_bytes(np + 4 * i, live ? 4 : 0);
+    for (int i = 0; i < 3; i++)
+      nonce[i] = live && (reinterpret_cast<uintptr_t>(np) & 3) == 0
+                     ? reinterpret_cast<const uint32_t *>(np)[i]
+                     : load_le32_bytes(np + 4 * i, live ? 4 : 0);
+  }
+  // The lane's first AD block (block q), loaded now so its latency hides
+  // under the first ChaCha block instead of stalling the Poly1305 setup.
+  uint32_t adw[4] = {0, 0, 0, 0};
+  {
+    const uint8_t *ad = b.ad + (live ? m.ad_off : 0);
+    const uint64_t k = (uint64_t)q;
+    if (live && 16 * k < m.ad_len) {
+      const uint64_t avail = m.ad_len - 16 * k;
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        adw[i] = load_le32_bytes(ad + 16 * k + 4 * i, avail > 4u * i ? avail - 4u * i : 0);
+    }
   }
   // Message = the record's `in` bytes then b.extra_len extra bytes
   // (BatchDesc::extra, the TLS 1.3 inner type), whose ciphertext goes to
@@ -494,10 +511,12 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
                     load_le32_bytes(p + 12, avail > 12 ? avail - 12 : 0));
     };
     if (wmax <= 1) {
-      if (nab == 1) ya = ad_block(0);
+      if (nab == 1) ya = pblock(adw[0], adw[1], adw[2], adw[3]);  // block 0 (lane 0's)
     } else {
       P acc = pzero();
-      for (uint64_t k = q; k < nab; k += L) acc = padd(pmul(acc, pwr(kLog)), ad_block(k));
+      for (uint64_t k = q; k < nab; k += L)
+        acc = padd(pmul(acc, pwr(kLog)),
+                   k == (uint64_t)q ? pblock(adw[0], adw[1], adw[2], adw[3]) : ad_block(k));
       P a = pshfl(acc, (q + (int)(nab % L)) & (L - 1), L);
 #pragma unroll
       for (int t = 0; t < kLog; t++) {
@@ -616,6 +635,13 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
            (unsigned long long)(ts[3] - ts[2]), (unsigned long long)(ts[4] - ts[3]),
            (unsigned long long)(ts[4] - ts[0]));
 #endif
+}
+
+// One wave group per wave.
+template <bool OPEN, int L, bool XT>
+__global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
+    const ChaChaKeyDev *__restrict__ keys, BatchDesc b) {
+  chacha_group<OPEN, L, XT>(keys, b, (uint64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6));
 }
 
 }  // namespace
