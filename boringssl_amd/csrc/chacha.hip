@@ -59,7 +59,12 @@ __device__ __forceinline__ void chacha_block(const uint32_t key[8], uint32_t ctr
   asm volatile("" : "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7), "+v"(x8), "+v"(x9), "+v"(x10),
                "+v"(x11));
   uint32_t x12 = ctr, x13 = nonce[0], x14 = nonce[1], x15 = nonce[2];
-#pragma unroll
+#ifndef BSSL_AMD_CHACHA_UNROLL
+#define BSSL_AMD_CHACHA_UNROLL 10
+#endif
+#define CHACHA_PRAGMA_(x) _Pragma(#x)
+#define CHACHA_PRAGMA(x) CHACHA_PRAGMA_(x)
+  CHACHA_PRAGMA(unroll BSSL_AMD_CHACHA_UNROLL)
   for (int i = 0; i < 10; i++) {
     QR(x0, x4, x8, x12) QR(x1, x5, x9, x13) QR(x2, x6, x10, x14) QR(x3, x7, x11, x15)
     QR(x0, x5, x10, x15) QR(x1, x6, x11, x12) QR(x2, x7, x8, x13) QR(x3, x4, x9, x14)
@@ -307,6 +312,12 @@ __device__ __forceinline__ void crypt_block_x(const uint8_t *src, uint8_t *dst, 
 #ifndef BSSL_AMD_CHACHA_STAMPS
 #define BSSL_AMD_CHACHA_STAMPS 0
 #endif
+// Diagnostic ablations (wrong output; selected builds only): 1 = no input
+// loads in the block loop, 2 = no Poly1305 absorb in the loop, 3 = no ChaCha
+// rounds in the loop, 4 = no stores in the loop.
+#ifndef BSSL_AMD_CHACHA_ABLATE
+#define BSSL_AMD_CHACHA_ABLATE 0
+#endif
 #if BSSL_AMD_CHACHA_STAMPS  // diagnostic build: per-phase cycles of sample waves
 #define CSTAMP(i) ts[i] = __builtin_amdgcn_s_memtime()
 #else
@@ -389,6 +400,13 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   auto prefetch = [&](uint64_t u, uint4 pre[4]) {
     const uint64_t d = u - 1;
     if (u >= 1 && u <= nblk && aligned && m.len >= 64 * d + 64) {
+#if BSSL_AMD_CHACHA_ABLATE == 1
+      if (u >= (uint64_t)L) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) pre[i] = make_uint4((uint32_t)u, i, 3, 4);
+        return;
+      }
+#endif
       const uint4 *sp = reinterpret_cast<const uint4 *>(src + 64 * d);
 #pragma unroll
       for (int i = 0; i < 4; i++) pre[i] = sp[i];
@@ -407,6 +425,9 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
       }
 #pragma unroll
       for (int i = 0; i < 16; i++) y[i] = x[i] ^ ks[i];
+#if BSSL_AMD_CHACHA_ABLATE == 4
+      if (u < (uint64_t)L || y[0] == 0x12345678u)
+#endif
 #pragma unroll
       for (int i = 0; i < 4; i++)
         dp[i] = make_uint4(y[4 * i], y[4 * i + 1], y[4 * i + 2], y[4 * i + 3]);
@@ -567,10 +588,18 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   for (int it = 1; it < iters; it++) {
     const uint64_t u = (uint64_t)it * L + q;
     prefetch(u, pre);
+#if BSSL_AMD_CHACHA_ABLATE == 3
+#pragma unroll
+    for (int i = 0; i < 16; i++) ks[i] = key[i & 7] ^ (uint32_t)u ^ nonce[i % 3];
+#else
     chacha_block(key, (uint32_t)u, nonce, ks);
+#endif
     if (u <= nblk) {
       uint32_t c[16];
       crypt_block(u, ks, pre, c);
+#if BSSL_AMD_CHACHA_ABLATE == 2
+      if (c[0] == 0x12345678u)
+#endif
       absorb(u, c);
     }
   }
