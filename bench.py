@@ -41,6 +41,10 @@ CONFIGS = {
                 "config2: AES-128-GCM seal, 1M x 16 KiB records per GPU, single key"),
     "config3": ("chacha20-poly1305", 32, 1 << 20, 1350,
                 "config3: ChaCha20-Poly1305 seal, 1M x 1350 B records per GPU"),
+    # XChaCha20-Poly1305: config 3's records with 24-byte
+    # nonces (oracle/ref/ref_tool.cc make_nonce).
+    "config3x": ("xchacha20-poly1305", 32, 1 << 20, 1350,
+                 "config3x: XChaCha20-Poly1305 seal, 1M x 1350 B records per GPU"),
     "config4": ("aes-256-gcm", 32, 1 << 22, "mixed",
                 "config4: AES-256-GCM seal, 4M records of 64 B-16 KiB (mixed) per GPU"),
     # 64K keys x 64 records over 8 GPUs: per GPU 8192 keys x 64 records of
@@ -77,6 +81,7 @@ def mixed_lengths(first, n):
 METRICS = {
     "config2": METRIC,
     "config3": "GiB/s device-resident AEAD seal (ChaCha20-Poly1305, 1350 B records)",
+    "config3x": "GiB/s device-resident AEAD seal (XChaCha20-Poly1305, 1350 B records)",
     "config4": "GiB/s device-resident AEAD seal (AES-256-GCM, mixed 64 B-16 KiB records)",
     "config5": "GiB/s device-resident AEAD seal (AES-128-GCM, 16 KiB records, 64 records per key)",
 }
@@ -214,6 +219,12 @@ def main():
     d_tags = torch.empty(16 * nrec, dtype=torch.uint8, device=dev)
     d_status = torch.zeros(nrec, dtype=torch.uint8, device=dev)
     ba.synth_fill_device(first, nrec, d_offs, d_lens, d_pt, d_nonce, d_ad)
+    nonce_len = 12
+    if aead == "xchacha20-poly1305":  # 24-byte nonces (ref_tool.cc make_nonce)
+        a = d_nonce.view(-1, 12)
+        b = a.clone()
+        b[:, 4:] ^= 0xff
+        d_nonce, nonce_len = torch.cat([a, b], dim=1).contiguous().view(-1), 24
     uniform = length != "mixed"
     rpk = RECORDS_PER_KEY.get(args.config)
     d_kidx = None
@@ -226,7 +237,7 @@ def main():
         d_kidx = torch.from_numpy((np.arange(nrec) // rpk).astype(np.int32)).to(dev)
     else:
         ctx = ba.AEADCtx(aead, synth_key(0, key_len), 16)
-    batch = ba.make_batch(nrec, d_pt, d_ct, d_tags, d_nonce, 12, d_ad,
+    batch = ba.make_batch(nrec, d_pt, d_ct, d_tags, d_nonce, nonce_len, d_ad,
                           offsets=None if uniform else d_offs,
                           lengths=None if uniform else d_lens,
                           record_stride=int(padded[0]) if uniform else 0,
@@ -240,7 +251,7 @@ def main():
         # (tags verified every step).
         ctx.seal_batch_device(batch, stream)
         d_back = torch.empty_like(d_pt)
-        batch = ba.make_batch(nrec, d_ct, d_back, d_tags, d_nonce, 12, d_ad,
+        batch = ba.make_batch(nrec, d_ct, d_back, d_tags, d_nonce, nonce_len, d_ad,
                               offsets=None if uniform else d_offs,
                               lengths=None if uniform else d_lens,
                               record_stride=int(padded[0]) if uniform else 0,
@@ -282,7 +293,7 @@ def main():
     ms_per_step = elapsed * 1000.0 / args.steps
     total_bytes = reduce_sum(float(pt_bytes), world)  # all ranks' records
     value = total_bytes * args.steps / elapsed / 2**30
-    algo_bytes = 2 * pt_bytes + 41 * nrec  # PT in + CT out + tag + nonce + AD
+    algo_bytes = 2 * pt_bytes + (29 + nonce_len) * nrec  # PT in + CT out + tag + nonce + AD
     achieved = algo_bytes / (avg_kernel_ms / 1000.0) / 1e9
     traffic = load_traffic(kname)
 

@@ -56,7 +56,7 @@ evp_aead_seal = 1
 # Every symbol include/bssl_amd/*.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = [
     "EVP_aead_aes_128_gcm", "EVP_aead_aes_192_gcm", "EVP_aead_aes_256_gcm",
-    "EVP_aead_chacha20_poly1305", "EVP_aead_aes_128_gcm_tls12", "EVP_aead_aes_256_gcm_tls12",
+    "EVP_aead_chacha20_poly1305", "EVP_aead_xchacha20_poly1305", "EVP_aead_aes_128_gcm_tls12", "EVP_aead_aes_256_gcm_tls12",
     "EVP_aead_aes_128_gcm_tls13", "EVP_aead_aes_256_gcm_tls13",
     "EVP_AEAD_key_length", "EVP_AEAD_nonce_length", "EVP_AEAD_max_overhead",
     "EVP_AEAD_max_tag_len", "EVP_AEAD_CTX_zero", "EVP_AEAD_CTX_new", "EVP_AEAD_CTX_free",
@@ -66,6 +66,7 @@ EXPORTED_SYMBOLS = [
     "EVP_AEAD_CTX_openv_detached", "EVP_AEAD_CTX_tag_len", "EVP_AEAD_CTX_get_iv",
     "ERR_get_error", "ERR_peek_error", "ERR_peek_last_error", "ERR_clear_error",
     "EVP_AEAD_CTX_seal_batch_device", "EVP_AEAD_CTX_open_batch_device",
+    "EVP_AEAD_CTX_sealv_batch_device", "EVP_AEAD_CTX_openv_detached_batch_device",
     "BSSL_AMD_KEYSET_new", "BSSL_AMD_KEYSET_free", "BSSL_AMD_KEYSET_num_keys",
     "BSSL_AMD_KEYSET_seal_batch_device", "BSSL_AMD_KEYSET_open_batch_device",
     "BSSL_AMD_set_device", "BSSL_AMD_device_count", "BSSL_AMD_synth_fill_device",
@@ -100,6 +101,13 @@ class BSSL_AMD_BATCH(ctypes.Structure):
         ("nonces", _P), ("nonce_len", _S), ("ad", _P), ("ad_offsets", _P), ("ad_lengths", _P),
         ("ad_stride", ctypes.c_uint64), ("ad_len", ctypes.c_uint64), ("tags", _P),
         ("status", _P), ("key_index", _P),
+    ]
+
+
+class BSSL_AMD_IOV_BATCH(ctypes.Structure):
+    _fields_ = [
+        ("num_records", _S), ("iovecs", _P), ("iovec_start", _P), ("aadvecs", _P),
+        ("aadvec_start", _P), ("nonces", _P), ("nonce_len", _S), ("tags", _P), ("status", _P),
     ]
 
 
@@ -139,6 +147,9 @@ _SIGS = {
     "ERR_clear_error": (None, []),
     "EVP_AEAD_CTX_seal_batch_device": (_I, [_CTXP, ctypes.POINTER(BSSL_AMD_BATCH), _P]),
     "EVP_AEAD_CTX_open_batch_device": (_I, [_CTXP, ctypes.POINTER(BSSL_AMD_BATCH), _P]),
+    "EVP_AEAD_CTX_sealv_batch_device": (_I, [_CTXP, ctypes.POINTER(BSSL_AMD_IOV_BATCH), _P]),
+    "EVP_AEAD_CTX_openv_detached_batch_device": (_I, [_CTXP, ctypes.POINTER(BSSL_AMD_IOV_BATCH),
+                                                      _P]),
     "BSSL_AMD_KEYSET_new": (_P, [_P, _P, _S, _S]),
     "BSSL_AMD_KEYSET_free": (None, [_P]),
     "BSSL_AMD_KEYSET_num_keys": (_S, [_P]),
@@ -173,6 +184,7 @@ AEADS = {
     "aes-192-gcm": _lib.EVP_aead_aes_192_gcm,
     "aes-256-gcm": _lib.EVP_aead_aes_256_gcm,
     "chacha20-poly1305": _lib.EVP_aead_chacha20_poly1305,
+    "xchacha20-poly1305": _lib.EVP_aead_xchacha20_poly1305,
     "aes-128-gcm-tls12": _lib.EVP_aead_aes_128_gcm_tls12,
     "aes-256-gcm-tls12": _lib.EVP_aead_aes_256_gcm_tls12,
     "aes-128-gcm-tls13": _lib.EVP_aead_aes_128_gcm_tls13,
@@ -274,6 +286,17 @@ class AEADCtx:
         if not _lib.EVP_AEAD_CTX_open_batch_device(ctypes.byref(self.ctx), ctypes.byref(batch),
                                                    _stream_ptr(stream)):
             _fail("EVP_AEAD_CTX_open_batch_device")
+
+    def sealv_batch_device(self, batch, stream=None):
+        """N sealv calls over device iovec records (BSSL_AMD_IOV_BATCH)."""
+        if not _lib.EVP_AEAD_CTX_sealv_batch_device(ctypes.byref(self.ctx), ctypes.byref(batch),
+                                                    _stream_ptr(stream)):
+            _fail("EVP_AEAD_CTX_sealv_batch_device")
+
+    def openv_detached_batch_device(self, batch, stream=None):
+        if not _lib.EVP_AEAD_CTX_openv_detached_batch_device(
+                ctypes.byref(self.ctx), ctypes.byref(batch), _stream_ptr(stream)):
+            _fail("EVP_AEAD_CTX_openv_detached_batch_device")
 
 
 class Keyset:
@@ -409,6 +432,25 @@ def make_batch(num_records, inp, out, tags, nonces, nonce_len, ad=None, *, offse
     b.key_index = _dptr(key_index)
     b._refs = (inp, out, tags, nonces, ad, offsets, lengths, ad_offsets, ad_lengths, status,
                key_index)
+    return b
+
+
+def make_iov_batch(num_records, iovecs, iovec_start, tags, nonces, nonce_len, *, aadvecs=None,
+                   aadvec_start=None, status=None):
+    """Builds a BSSL_AMD_IOV_BATCH.  `iovecs`: device int64 tensor [m, 3] of
+    CRYPTO_IOVEC {out, in, len} (device addresses); `aadvecs`: [k, 2] of
+    CRYPTO_IVEC {in, len}; `*_start`: device int64 [num_records + 1]."""
+    b = BSSL_AMD_IOV_BATCH()
+    b.num_records = num_records
+    b.iovecs = _dptr(iovecs)
+    b.iovec_start = _dptr(iovec_start)
+    b.aadvecs = _dptr(aadvecs)
+    b.aadvec_start = _dptr(aadvec_start)
+    b.nonces = _dptr(nonces)
+    b.nonce_len = nonce_len
+    b.tags = _dptr(tags)
+    b.status = _dptr(status)
+    b._refs = (iovecs, iovec_start, aadvecs, aadvec_start, nonces, tags, status)
     return b
 
 

@@ -78,6 +78,7 @@ const evp_aead_st kAes128Gcm = {16, 12, 16, 16, kAeadAesGcm, 0};
 const evp_aead_st kAes192Gcm = {24, 12, 16, 16, kAeadAesGcm, 0};
 const evp_aead_st kAes256Gcm = {32, 12, 16, 16, kAeadAesGcm, 0};
 const evp_aead_st kChaChaPoly = {32, 12, 16, 16, kAeadChaChaPoly, 0};
+const evp_aead_st kXChaChaPoly = {32, 24, 16, 16, kAeadXChaChaPoly, 0};  // e_chacha20poly1305.cc:385-399
 const evp_aead_st kAes128GcmTls12 = {16, 12, 16, 16, kAeadAesGcm, 12};
 const evp_aead_st kAes256GcmTls12 = {32, 12, 16, 16, kAeadAesGcm, 12};
 const evp_aead_st kAes128GcmTls13 = {16, 12, 16, 16, kAeadAesGcm, 13};
@@ -182,6 +183,22 @@ const KernelEvents *timing_pair() {
   return &t_timing.pending.back();
 }
 
+// Launch the bulk kernels of the AEAD over a filled-in descriptor.  Returns 0
+// or a HIP error code.
+int launch_desc(const KeyMaterial *km, const BatchDesc &d, bool open, void *stream) {
+  int rc;
+  const KernelEvents *ev = timing_pair();
+  if (km->aead->kind == kAeadAesGcm) {
+    rc = launch_gcm(static_cast<const GcmKeyDev *>(km->dev), d, open, km->nr, stream, ev);
+    t_timing.last_name = "gcm_kernel";
+  } else {
+    rc = launch_chacha(static_cast<const ChaChaKeyDev *>(km->dev), d, open,
+                       km->aead->kind == kAeadXChaChaPoly, stream, ev);
+    t_timing.last_name = "chacha_poly_kernel";
+  }
+  return rc;
+}
+
 // Launch a batch over device buffers.  Returns 1 on success.
 int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch, bool open,
               bool use_key_index, void *stream, const uint8_t *valid = nullptr) {
@@ -210,16 +227,7 @@ int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch
   d.extra = nullptr;
   d.extra_out = nullptr;
   d.extra_len = d.extra_stride = d.extra_out_stride = d.tag_stride = 0;
-  int rc;
-  const KernelEvents *ev = timing_pair();
-  if (km->aead->kind == kAeadAesGcm) {
-    rc = launch_gcm(static_cast<const GcmKeyDev *>(km->dev), d, open, km->nr, stream, ev);
-    t_timing.last_name = "gcm_kernel";
-  } else {
-    rc = launch_chacha(static_cast<const ChaChaKeyDev *>(km->dev), d, open, stream, ev);
-    t_timing.last_name = "chacha_poly_kernel";
-  }
-  if (rc != 0) {
+  if (launch_desc(km, d, open, stream) != 0) {
     PUT_ERROR(ERR_R_INTERNAL_ERROR);
     return 0;
   }
@@ -241,7 +249,7 @@ bool check_batch(const EVP_AEAD *aead, const BSSL_AMD_BATCH *b) {
       PUT_ERROR(CIPHER_R_INVALID_NONCE_SIZE);
       return false;
     }
-  } else if (b->nonce_len != 12) {  // e_chacha20poly1305.cc:127-130
+  } else if (b->nonce_len != aead->nonce_len) {  // e_chacha20poly1305.cc:127-130, 241-244
     PUT_ERROR(CIPHER_R_UNSUPPORTED_NONCE_SIZE);
     return false;
   }
@@ -466,7 +474,7 @@ bool aead_record_checks(const EVP_AEAD_CTX *ctx, size_t nonce_len, size_t in_len
       return false;
     }
   } else {
-    if (nonce_len != 12) {
+    if (nonce_len != aead->nonce_len) {  // 12, or 24 for XChaCha (e_chacha20poly1305.cc:241)
       PUT_ERROR(CIPHER_R_UNSUPPORTED_NONCE_SIZE);
       return false;
     }
@@ -488,6 +496,7 @@ const EVP_AEAD *EVP_aead_aes_128_gcm(void) { return &kAes128Gcm; }
 const EVP_AEAD *EVP_aead_aes_192_gcm(void) { return &kAes192Gcm; }
 const EVP_AEAD *EVP_aead_aes_256_gcm(void) { return &kAes256Gcm; }
 const EVP_AEAD *EVP_aead_chacha20_poly1305(void) { return &kChaChaPoly; }
+const EVP_AEAD *EVP_aead_xchacha20_poly1305(void) { return &kXChaChaPoly; }
 const EVP_AEAD *EVP_aead_aes_128_gcm_tls12(void) { return &kAes128GcmTls12; }
 const EVP_AEAD *EVP_aead_aes_256_gcm_tls12(void) { return &kAes256GcmTls12; }
 const EVP_AEAD *EVP_aead_aes_128_gcm_tls13(void) { return &kAes128GcmTls13; }
@@ -924,6 +933,114 @@ int EVP_AEAD_CTX_open_batch_device(const EVP_AEAD_CTX *ctx, const BSSL_AMD_BATCH
   return run_batch(state_of(ctx)->km, ctx->tag_len, batch, true, false, hip_stream);
 }
 
+namespace {
+
+// The bulk kernels of `km` over the gathered records of an iovec batch.
+struct KeyRunner : IovRunner {
+  const KeyMaterial *km;
+  size_t tag_len;
+  bool open;
+  void *stream;
+  const uint8_t *valid;
+  KeyRunner(const KeyMaterial *k, size_t t, bool o, void *s, const uint8_t *v)
+      : km(k), tag_len(t), open(o), stream(s), valid(v) {}
+  int operator()(BatchDesc &d) const override {
+    d.tag_len = (uint32_t)tag_len;
+    d.num_keys = (uint32_t)km->num_keys;
+    d.valid = valid;
+    return launch_desc(km, d, open, stream);
+  }
+};
+
+bool check_iov_batch(const EVP_AEAD *aead, const BSSL_AMD_IOV_BATCH *b) {
+  if (!b) {
+    PUT_ERROR(ERR_R_SHOULD_NOT_HAVE_BEEN_CALLED);
+    return false;
+  }
+  if (b->num_records == 0) return true;
+  if (!b->iovecs || !b->iovec_start || !b->nonces || !b->tags ||
+      (b->aadvecs && !b->aadvec_start)) {
+    PUT_ERROR(ERR_R_SHOULD_NOT_HAVE_BEEN_CALLED);
+    return false;
+  }
+  BSSL_AMD_BATCH probe = {};
+  probe.num_records = b->num_records;
+  probe.in = probe.out = reinterpret_cast<uint8_t *>(1);
+  probe.nonces = b->nonces;
+  probe.nonce_len = b->nonce_len;
+  probe.tags = b->tags;
+  return check_batch(aead, &probe);  // nonce-length rules of the AEAD
+}
+
+IovBatchDesc iov_desc(const BSSL_AMD_IOV_BATCH *b) {
+  static_assert(sizeof(IovecDev) == sizeof(CRYPTO_IOVEC), "CRYPTO_IOVEC layout");
+  static_assert(sizeof(IvecDev) == sizeof(CRYPTO_IVEC), "CRYPTO_IVEC layout");
+  IovBatchDesc d;
+  d.num_records = b->num_records;
+  d.iovecs = reinterpret_cast<const IovecDev *>(b->iovecs);
+  d.iovec_start = b->iovec_start;
+  d.aadvecs = reinterpret_cast<const IvecDev *>(b->aadvecs);
+  d.aadvec_start = b->aadvec_start;
+  d.nonces = b->nonces;
+  d.nonce_len = b->nonce_len;
+  d.tags = b->tags;
+  d.status = b->status;
+  return d;
+}
+
+}  // namespace
+
+// aead.cc.inc:316-361 (sealv) for a batch of device records.
+int EVP_AEAD_CTX_sealv_batch_device(const EVP_AEAD_CTX *ctx, const BSSL_AMD_IOV_BATCH *batch,
+                                    void *hip_stream) {
+  if (!ctx || !ctx->aead || !check_iov_batch(ctx->aead, batch)) return 0;
+  if (batch->num_records == 0) return 1;
+  CtxState *st = state_of(ctx);
+  hipStream_t s = reinterpret_cast<hipStream_t>(hip_stream);
+  uint8_t *valid = nullptr;
+  if (ctx->aead->tls) {  // the monotonic-nonce check, as for contiguous batches
+    if (batch->nonce_len != 12) {
+      PUT_ERROR(CIPHER_R_UNSUPPORTED_NONCE_SIZE);
+      return 0;
+    }
+    if (hipMallocAsync(reinterpret_cast<void **>(&valid), batch->num_records, s) != hipSuccess) {
+      PUT_ERROR(ERR_R_MALLOC_FAILURE);
+      return 0;
+    }
+    if (tls_nonce_scan(batch->nonces, batch->num_records, ctx->aead->tls, &st->min_next_nonce,
+                       &st->mask, valid, 0, hip_stream) != 0) {
+      hipFreeAsync(valid, s);
+      PUT_ERROR(ERR_R_INTERNAL_ERROR);
+      return 0;
+    }
+  }
+  const int rc = iov_batch_run(iov_desc(batch),
+                               KeyRunner(st->km, ctx->tag_len, false, hip_stream, valid),
+                               hip_stream);
+  if (valid) hipFreeAsync(valid, s);
+  if (rc != 0) {
+    PUT_ERROR(ERR_R_INTERNAL_ERROR);
+    return 0;
+  }
+  return 1;
+}
+
+// aead.cc.inc:531-584 (openv_detached) for a batch of device records; the
+// tags (tag_len bytes each) are read at tags + i*tag_len.
+int EVP_AEAD_CTX_openv_detached_batch_device(const EVP_AEAD_CTX *ctx,
+                                             const BSSL_AMD_IOV_BATCH *batch, void *hip_stream) {
+  if (!ctx || !ctx->aead || !check_iov_batch(ctx->aead, batch)) return 0;
+  if (batch->num_records == 0) return 1;
+  const int rc = iov_batch_run(
+      iov_desc(batch), KeyRunner(state_of(ctx)->km, ctx->tag_len, true, hip_stream, nullptr),
+      hip_stream);
+  if (rc != 0) {
+    PUT_ERROR(ERR_R_INTERNAL_ERROR);
+    return 0;
+  }
+  return 1;
+}
+
 struct bssl_amd_keyset_st {
   KeyMaterial *km;
   size_t tag_len;
@@ -1141,7 +1258,7 @@ int tls_records(BSSL_AMD_TLS_AEAD *t, const BSSL_AMD_TLS_RECORDS *r, void *strea
                        ? launch_gcm(static_cast<const GcmKeyDev *>(st->km->dev), d, !t->seal,
                                     st->km->nr, stream, ev)
                        : launch_chacha(static_cast<const ChaChaKeyDev *>(st->km->dev), d,
-                                       !t->seal, stream, ev);
+                                       !t->seal, false, stream, ev);
     t_timing.last_name = ctx->aead->kind == kAeadAesGcm ? "gcm_kernel" : "chacha_poly_kernel";
     ok = rc == 0;
     // TLS 1.2 open reports the header type (tls_record.cc:197-235).

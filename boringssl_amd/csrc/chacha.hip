@@ -33,6 +33,14 @@ namespace bssl_amd {
 namespace {
 
 constexpr int kThreads = 256;
+#ifndef BSSL_AMD_CHACHA_L
+#define BSSL_AMD_CHACHA_L 4
+#endif
+#ifndef BSSL_AMD_CHACHA_UNROLL
+#define BSSL_AMD_CHACHA_UNROLL 10
+#endif
+#define CHACHA_PRAGMA_(x) _Pragma(#x)
+#define CHACHA_PRAGMA(x) CHACHA_PRAGMA_(x)
 constexpr uint32_t kM26 = 0x3ffffff;
 
 __device__ __forceinline__ uint32_t rotl(uint32_t v, int n) {
@@ -59,11 +67,6 @@ __device__ __forceinline__ void chacha_block(const uint32_t key[8], uint32_t ctr
   asm volatile("" : "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7), "+v"(x8), "+v"(x9), "+v"(x10),
                "+v"(x11));
   uint32_t x12 = ctr, x13 = nonce[0], x14 = nonce[1], x15 = nonce[2];
-#ifndef BSSL_AMD_CHACHA_UNROLL
-#define BSSL_AMD_CHACHA_UNROLL 10
-#endif
-#define CHACHA_PRAGMA_(x) _Pragma(#x)
-#define CHACHA_PRAGMA(x) CHACHA_PRAGMA_(x)
   CHACHA_PRAGMA(unroll BSSL_AMD_CHACHA_UNROLL)
   for (int i = 0; i < 10; i++) {
     QR(x0, x4, x8, x12) QR(x1, x5, x9, x13) QR(x2, x6, x10, x14) QR(x3, x7, x11, x15)
@@ -85,6 +88,23 @@ __device__ __forceinline__ void chacha_block(const uint32_t key[8], uint32_t ctr
   out[13] = x13 + nonce[0];
   out[14] = x14 + nonce[1];
   out[15] = x15 + nonce[2];
+}
+
+// HChaCha20 (CRYPTO_hchacha20, crypto/chacha/chacha.cc:43-63): the state of
+// (key, 16-byte nonce) after 20 rounds, words 0-3 and 12-15 -- the
+// XChaCha20-Poly1305 subkey (e_chacha20poly1305.cc:248-252).
+__device__ __forceinline__ void hchacha20(uint32_t key[8], const uint32_t n[4]) {
+  uint32_t x0 = 0x61707865, x1 = 0x3320646e, x2 = 0x79622d32, x3 = 0x6b206574;
+  uint32_t x4 = key[0], x5 = key[1], x6 = key[2], x7 = key[3];
+  uint32_t x8 = key[4], x9 = key[5], x10 = key[6], x11 = key[7];
+  uint32_t x12 = n[0], x13 = n[1], x14 = n[2], x15 = n[3];
+  CHACHA_PRAGMA(unroll BSSL_AMD_CHACHA_UNROLL)
+  for (int i = 0; i < 10; i++) {
+    QR(x0, x4, x8, x12) QR(x1, x5, x9, x13) QR(x2, x6, x10, x14) QR(x3, x7, x11, x15)
+    QR(x0, x5, x10, x15) QR(x1, x6, x11, x12) QR(x2, x7, x8, x13) QR(x3, x4, x9, x14)
+  }
+  key[0] = x0; key[1] = x1; key[2] = x2; key[3] = x3;
+  key[4] = x12; key[5] = x13; key[6] = x14; key[7] = x15;
 }
 
 // ---------------------------------------------------------------------------
@@ -324,7 +344,7 @@ __device__ __forceinline__ void crypt_block_x(const uint8_t *src, uint8_t *dst, 
 #define CSTAMP(i)
 #endif
 // One wave group: records pos = grp * (64 / L) + lane / L.
-template <bool OPEN, int L, bool XT>
+template <bool OPEN, int L, bool XT, bool XC>
 __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ keys,
                                              const BatchDesc &b, uint64_t grp) {
 #if BSSL_AMD_CHACHA_STAMPS
@@ -347,8 +367,10 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     m.ad_len = b.ad_lengths ? b.ad_lengths[rec] : b.ad_len;
     kidx = b.key_index ? b.key_index[rec] : 0u;
   }
-  // e_chacha20poly1305.cc:127-142: 12-byte nonce, < 2^32 - 1 blocks.
-  const bool bad = active && (kidx >= b.num_keys || b.nonce_len != 12 ||
+  // e_chacha20poly1305.cc:127-142: 12-byte nonce, < 2^32 - 1 blocks
+  // (XChaCha20-Poly1305: 24-byte nonce, :241-244).
+  constexpr uint32_t kNonceLen = XC ? 24 : 12;
+  const bool bad = active && (kidx >= b.num_keys || b.nonce_len != kNonceLen ||
                               m.len + b.extra_len >= (uint64_t(1) << 32) * 64 - 64 ||
                               (b.valid && !b.valid[rec]));
   const bool live = active && !bad;
@@ -357,12 +379,25 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     const ChaChaKeyDev *kp = keys + (live ? kidx : 0u);
 #pragma unroll
     for (int i = 0; i < 8; i++) key[i] = kp->k[i];
-    const uint8_t *np = b.nonces + (live ? rec * 12 : 0);
+    const uint8_t *np = b.nonces + (live ? rec * kNonceLen : 0);
+    constexpr int kWords = kNonceLen / 4;
+    uint32_t nw[kWords];
 #pragma unroll
-    for (int i = 0; i < 3; i++)
-      nonce[i] = live && (reinterpret_cast<uintptr_t>(np) & 3) == 0
-                     ? reinterpret_cast<const uint32_t *>(np)[i]
-                     : load_le32_bytes(np + 4 * i, live ? 4 : 0);
+    for (int i = 0; i < kWords; i++)
+      nw[i] = live && (reinterpret_cast<uintptr_t>(np) & 3) == 0
+                  ? reinterpret_cast<const uint32_t *>(np)[i]
+                  : load_le32_bytes(np + 4 * i, live ? 4 : 0);
+    if constexpr (XC) {
+      // key' = HChaCha20(key, nonce[0:16]), nonce' = 0^4 || nonce[16:24]
+      // (e_chacha20poly1305.cc:248-252).
+      hchacha20(key, nw);
+      nonce[0] = 0;
+      nonce[1] = nw[4];
+      nonce[2] = nw[5];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 3; i++) nonce[i] = nw[i];
+    }
   }
   // The lane's first AD block (block q), loaded now so its latency hides
   // under the first ChaCha block instead of stalling the Poly1305 setup.
@@ -667,21 +702,26 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
 }
 
 // One wave group per wave.
-template <bool OPEN, int L, bool XT>
+template <bool OPEN, int L, bool XT, bool XC>
 __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
     const ChaChaKeyDev *__restrict__ keys, BatchDesc b) {
-  chacha_group<OPEN, L, XT>(keys, b, (uint64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6));
+  chacha_group<OPEN, L, XT, XC>(keys, b,
+                                (uint64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6));
+}
+
+template <bool OPEN, bool XT, bool XC>
+void launch_one(const ChaChaKeyDev *keys, const BatchDesc &b, uint64_t blocks, hipStream_t s) {
+  constexpr int L = BSSL_AMD_CHACHA_L;
+  hipLaunchKernelGGL((chacha_poly_kernel<OPEN, L, XT, XC>), dim3((unsigned)blocks),
+                     dim3(kThreads), 0, s, keys, b);
 }
 
 }  // namespace
 
-int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, void *stream,
-                  const KernelEvents *ev) {
+int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, bool xchacha,
+                  void *stream, const KernelEvents *ev) {
   if (b.num_records == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-#ifndef BSSL_AMD_CHACHA_L
-#define BSSL_AMD_CHACHA_L 4
-#endif
   constexpr int L = BSSL_AMD_CHACHA_L;  // lanes per record (see chacha_poly_kernel)
   const uint64_t blocks = (b.num_records * L + kThreads - 1) / kThreads;
   if (blocks > 0x7fffffffu) return 1;
@@ -699,18 +739,21 @@ int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, void 
     bo.order = order;
   }
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
-  if (open && b.extra_len)
-    hipLaunchKernelGGL((chacha_poly_kernel<true, L, true>), dim3((unsigned)blocks),
-                       dim3(kThreads), 0, s, keys, bo);
-  else if (open)
-    hipLaunchKernelGGL((chacha_poly_kernel<true, L, false>), dim3((unsigned)blocks),
-                       dim3(kThreads), 0, s, keys, bo);
-  else if (b.extra_len)
-    hipLaunchKernelGGL((chacha_poly_kernel<false, L, true>), dim3((unsigned)blocks),
-                       dim3(kThreads), 0, s, keys, bo);
-  else
-    hipLaunchKernelGGL((chacha_poly_kernel<false, L, false>), dim3((unsigned)blocks),
-                       dim3(kThreads), 0, s, keys, bo);
+  const bool xt = b.extra_len != 0;
+  if (xchacha) {
+    if (open)
+      xt ? launch_one<true, true, true>(keys, bo, blocks, s)
+         : launch_one<true, false, true>(keys, bo, blocks, s);
+    else
+      xt ? launch_one<false, true, true>(keys, bo, blocks, s)
+         : launch_one<false, false, true>(keys, bo, blocks, s);
+  } else if (open) {
+    xt ? launch_one<true, true, false>(keys, bo, blocks, s)
+       : launch_one<true, false, false>(keys, bo, blocks, s);
+  } else {
+    xt ? launch_one<false, true, false>(keys, bo, blocks, s)
+       : launch_one<false, false, false>(keys, bo, blocks, s);
+  }
   const int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
   if (order) hipFreeAsync(order, s);

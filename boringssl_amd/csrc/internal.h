@@ -43,7 +43,7 @@ struct alignas(16) ChaChaKeyDev {
   uint32_t k[8];
 };
 
-enum AeadKind : int { kAeadAesGcm = 0, kAeadChaChaPoly = 1 };
+enum AeadKind : int { kAeadAesGcm = 0, kAeadChaChaPoly = 1, kAeadXChaChaPoly = 2 };
 
 // Record-batch descriptor (device pointers), see BSSL_AMD_BATCH.
 struct BatchDesc {
@@ -117,7 +117,8 @@ int build_length_order(const uint64_t *lengths, uint64_t n, uint32_t *order, uin
 inline bool wants_length_order(const BatchDesc &b) {
   return b.lengths && b.num_records >= 4096 && b.num_records < (uint64_t(1) << 32);
 }
-int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open,
+// xchacha: XChaCha20-Poly1305 (24-byte nonces, per-record HChaCha20 subkey).
+int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, bool xchacha,
                   void *stream, const KernelEvents *ev);
 // tls12 / tls13 nonce checks over a batch of seal calls (tls_scan.hip):
 // writes valid[i] (device) and advances the context's nonce state in place
@@ -147,6 +148,35 @@ struct TlsPrepare {
   uint8_t *nonces, *prefix, *ad, *extra, *valid;
 };
 int launch_tls_prepare(const TlsPrepare &p, void *stream);
+// Batches of non-contiguous records (iovec.hip): CRYPTO_IOVEC / CRYPTO_IVEC
+// layouts (reference include/openssl/aead.h:400-414) on the device.
+struct IovecDev {
+  uint8_t *out;
+  const uint8_t *in;
+  uint64_t len;
+};
+struct IvecDev {
+  const uint8_t *in;
+  uint64_t len;
+};
+struct IovBatchDesc {
+  uint64_t num_records;
+  const IovecDev *iovecs;
+  const uint64_t *iovec_start;   // num_records + 1 entries
+  const IvecDev *aadvecs;        // or null (no AD)
+  const uint64_t *aadvec_start;  // num_records + 1 entries
+  const uint8_t *nonces;
+  uint64_t nonce_len;
+  uint8_t *tags;
+  uint8_t *status;
+};
+// Runs the bulk kernels over the gathered records (a contiguous BatchDesc
+// whose tag_len / key fields the runner fills in).  Returns 0 or an error.
+struct IovRunner {
+  virtual int operator()(BatchDesc &d) const = 0;
+};
+// Gather -> run -> scatter; synchronises `stream` once (staging size).
+int iov_batch_run(const IovBatchDesc &b, const IovRunner &run, void *stream);
 int launch_synth(uint64_t first, size_t n, const uint64_t *offsets,
                  const uint64_t *lengths, uint8_t *pt, uint8_t *nonces,
                  uint8_t *ads, void *stream);

@@ -1,0 +1,180 @@
+// iovec.hip -- EVP_AEAD_CTX_sealv / _openv_detached over device batches of
+// non-contiguous records.
+//
+// Reference: EVP_AEAD_CTX_sealv / _openv_detached (crypto/fipsmodule/cipher/
+// aead.cc.inc:316-361, 531-584) take one record as an array of CRYPTO_IOVEC
+// {out, in, len} chunks and its AD as an array of CRYPTO_IVEC {in, len}
+// (include/openssl/aead.h:400-414); the AEADs walk the chunks with
+// bssl::iovec::ForEachBlockRange (crypto/cipher/internal.h), i.e. the record
+// is the concatenation of its chunks.  Here a batch of such records is
+// gathered into one contiguous device staging area (records 16-byte aligned,
+// so the bulk kernels take their aligned fast path), sealed or opened in place
+// by the same bulk kernels as any batch, and scattered back to the chunks'
+// `out` pointers.  A failed record is zero-filled in the staging area by the
+// bulk kernel, so the scatter zeroes its chunks (clear_iovec,
+// aead.cc.inc:310-314, 325-333).
+//
+// Copies: one workgroup per record walks its chunks in order; each chunk is
+// copied in 16-byte destination words assembled from byte-aligned source
+// reads (chunks have arbitrary lengths, so a record's later chunks start at
+// arbitrary alignments), with a byte loop for the head and tail.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "internal.h"
+
+namespace bssl_amd {
+namespace {
+
+constexpr int kCopyThreads = 256;
+
+// dst[0, n) = src[0, n) for one chunk, all threads of the workgroup.
+__device__ __forceinline__ void copy_bytes(uint8_t *dst, const uint8_t *src, uint64_t n) {
+  // Head: bytes until dst is 16-byte aligned.
+  const uint64_t head = min<uint64_t>(n, (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15);
+  for (uint64_t i = threadIdx.x; i < head; i += blockDim.x) dst[i] = src[i];
+  const uint64_t words = (n - head) / 16;
+  uint8_t *d = dst + head;
+  const uint8_t *s = src + head;
+  if ((reinterpret_cast<uintptr_t>(s) & 15) == 0) {
+    for (uint64_t w = threadIdx.x; w < words; w += blockDim.x)
+      reinterpret_cast<uint4 *>(d)[w] = reinterpret_cast<const uint4 *>(s)[w];
+  } else if ((reinterpret_cast<uintptr_t>(s) & 3) == 0) {
+    for (uint64_t w = threadIdx.x; w < words; w += blockDim.x) {
+      const uint32_t *sp = reinterpret_cast<const uint32_t *>(s + 16 * w);
+      reinterpret_cast<uint4 *>(d)[w] = make_uint4(sp[0], sp[1], sp[2], sp[3]);
+    }
+  } else {
+    for (uint64_t w = threadIdx.x; w < words; w += blockDim.x) {
+      const uint8_t *sp = s + 16 * w;
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        v[k] = (uint32_t)sp[4 * k] | ((uint32_t)sp[4 * k + 1] << 8) |
+               ((uint32_t)sp[4 * k + 2] << 16) | ((uint32_t)sp[4 * k + 3] << 24);
+      reinterpret_cast<uint4 *>(d)[w] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  }
+  for (uint64_t i = head + 16 * words + threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+
+// Per record: message and AD lengths, and their 16-byte padded sizes for the
+// staging layout.
+__global__ void iov_lengths(const IovBatchDesc b, uint64_t *__restrict__ len,
+                            uint64_t *__restrict__ padded, uint64_t *__restrict__ ad_len,
+                            uint64_t *__restrict__ ad_padded) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= b.num_records) return;
+  uint64_t t = 0, a = 0;
+  for (uint64_t c = b.iovec_start[i]; c < b.iovec_start[i + 1]; c++) t += b.iovecs[c].len;
+  if (b.aadvecs)
+    for (uint64_t c = b.aadvec_start[i]; c < b.aadvec_start[i + 1]; c++) a += b.aadvecs[c].len;
+  len[i] = t;
+  padded[i] = (t + 15) & ~uint64_t(15);
+  ad_len[i] = a;
+  ad_padded[i] = (a + 15) & ~uint64_t(15);
+}
+
+// Gather (TO_STAGE) or scatter (!TO_STAGE) the chunks of records
+// blockIdx.x, blockIdx.x + gridDim.x, ...
+template <bool TO_STAGE>
+__global__ __launch_bounds__(kCopyThreads) void iov_copy(const IovBatchDesc b,
+                                                         uint8_t *__restrict__ stage,
+                                                         const uint64_t *__restrict__ off,
+                                                         uint8_t *__restrict__ ad_stage,
+                                                         const uint64_t *__restrict__ ad_off) {
+  for (uint64_t i = blockIdx.x; i < b.num_records; i += gridDim.x) {
+    uint64_t pos = off[i];
+    for (uint64_t c = b.iovec_start[i]; c < b.iovec_start[i + 1]; c++) {
+      const IovecDev v = b.iovecs[c];
+      if (TO_STAGE)
+        copy_bytes(stage + pos, v.in, v.len);
+      else
+        copy_bytes(v.out, stage + pos, v.len);
+      pos += v.len;
+    }
+    if (TO_STAGE && b.aadvecs) {
+      uint64_t apos = ad_off[i];
+      for (uint64_t c = b.aadvec_start[i]; c < b.aadvec_start[i + 1]; c++) {
+        const IvecDev v = b.aadvecs[c];
+        copy_bytes(ad_stage + apos, v.in, v.len);
+        apos += v.len;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+int iov_batch_run(const IovBatchDesc &b, const IovRunner &run, void *stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint64_t n = b.num_records;
+  if (n == 0) return 0;
+  size_t temp = 0;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, temp, (const uint64_t *)nullptr,
+                                       (uint64_t *)nullptr, n + 1, s) != hipSuccess)
+    return 1;
+  // len, padded (n+1, last = 0), off (n+1), ad_len, ad_padded (n+1), ad_off (n+1)
+  const size_t words = 6 * (n + 1) + 2;
+  uint8_t *meta = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void **>(&meta), words * 8 + temp, s) != hipSuccess) return 2;
+  uint64_t *len = reinterpret_cast<uint64_t *>(meta);
+  uint64_t *padded = len + (n + 1);
+  uint64_t *off = padded + (n + 1);
+  uint64_t *ad_len = off + (n + 1);
+  uint64_t *ad_padded = ad_len + (n + 1);
+  uint64_t *ad_off = ad_padded + (n + 1);
+  void *d_temp = meta + words * 8;
+  int rc = 0;
+  if (hipMemsetAsync(padded + n, 0, 8, s) != hipSuccess ||
+      hipMemsetAsync(ad_padded + n, 0, 8, s) != hipSuccess)
+    rc = 1;
+  if (!rc) {
+    hipLaunchKernelGGL(iov_lengths, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b, len,
+                       padded, ad_len, ad_padded);
+    if (hipcub::DeviceScan::ExclusiveSum(d_temp, temp, padded, off, n + 1, s) != hipSuccess ||
+        hipcub::DeviceScan::ExclusiveSum(d_temp, temp, ad_padded, ad_off, n + 1, s) !=
+            hipSuccess)
+      rc = 1;
+  }
+  // The staging size is known only on the device: read the two totals back
+  // (this synchronises the stream once per batch).
+  uint64_t totals[2] = {0, 0};
+  if (!rc && (hipMemcpyAsync(&totals[0], off + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+              hipMemcpyAsync(&totals[1], ad_off + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+              hipStreamSynchronize(s) != hipSuccess))
+    rc = 1;
+  uint8_t *stage = nullptr;
+  if (!rc && hipMallocAsync(reinterpret_cast<void **>(&stage), totals[0] + totals[1] + 16, s) !=
+                 hipSuccess)
+    rc = 2;
+  if (!rc) {
+    uint8_t *ad_stage = stage + totals[0];
+    const unsigned grid = (unsigned)(n < 65536 ? n : 65536);
+    hipLaunchKernelGGL(iov_copy<true>, dim3(grid), dim3(kCopyThreads), 0, s, b, stage, off,
+                       ad_stage, ad_off);
+    BatchDesc d = {};
+    d.in = stage;
+    d.out = stage;
+    d.offsets = off;
+    d.lengths = len;
+    d.nonces = b.nonces;
+    d.nonce_len = b.nonce_len;
+    d.ad = ad_stage;
+    d.ad_offsets = ad_off;
+    d.ad_lengths = ad_len;
+    d.tags = b.tags;
+    d.status = b.status;
+    d.num_records = n;
+    rc = run(d);
+    if (!rc)
+      hipLaunchKernelGGL(iov_copy<false>, dim3(grid), dim3(kCopyThreads), 0, s, b, stage, off,
+                         ad_stage, ad_off);
+    hipFreeAsync(stage, s);
+  }
+  hipFreeAsync(meta, s);
+  if (!rc && hipGetLastError() != hipSuccess) rc = 1;
+  return rc;
+}
+
+}  // namespace bssl_amd

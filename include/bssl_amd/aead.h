@@ -74,6 +74,7 @@ BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_aes_128_gcm(void);        /* aead.h:100
 BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_aes_192_gcm(void);        /* aead.h:113 */
 BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_aes_256_gcm(void);        /* aead.h:122 */
 BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_chacha20_poly1305(void);  /* aead.h:126 */
+BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_xchacha20_poly1305(void); /* aead.h:130 */
 BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_aes_128_gcm_tls12(void);  /* aead.h:583 */
 BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_aes_256_gcm_tls12(void);  /* aead.h:584 */
 BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_aes_128_gcm_tls13(void);  /* aead.h:585 */
@@ -231,6 +232,40 @@ BSSL_AMD_EXPORT int EVP_AEAD_CTX_seal_batch_device(const EVP_AEAD_CTX *ctx,
 BSSL_AMD_EXPORT int EVP_AEAD_CTX_open_batch_device(const EVP_AEAD_CTX *ctx,
                                                    const BSSL_AMD_BATCH *batch,
                                                    void *hip_stream);
+
+/* A batch of non-contiguous records: the device form of N
+ * EVP_AEAD_CTX_sealv / _openv_detached calls (aead.cc.inc:316-361, 531-584).
+ * Every pointer is a DEVICE pointer, including the ones inside the CRYPTO_IOVEC
+ * / CRYPTO_IVEC arrays.  Record i is the concatenation of
+ * iovecs[iovec_start[i] .. iovec_start[i+1]) (each chunk's output goes to its
+ * `out`, which may equal its `in`), its AD the concatenation of
+ * aadvecs[aadvec_start[i] .. aadvec_start[i+1]) (aadvecs NULL = no AD);
+ * nonce at nonces + i*nonce_len; tag at tags + i*tag_len (written by seal,
+ * read by open).  status[i] (optional) as for BSSL_AMD_BATCH; a failed
+ * record's chunks (and, for seal, tag) are zero-filled (clear_iovec,
+ * aead.cc.inc:310-333).  The records are gathered into a device staging area,
+ * run through the same kernels as BSSL_AMD_BATCH and scattered back; the call
+ * synchronises `hip_stream` once (to size the staging area).  Chunks of one
+ * batch must not partially overlap (aead.cc.inc:281-308; not checked on the
+ * device). */
+typedef struct bssl_amd_iov_batch_st {
+  size_t num_records;
+  const CRYPTO_IOVEC *iovecs;
+  const uint64_t *iovec_start;  /* num_records + 1 entries */
+  const CRYPTO_IVEC *aadvecs;
+  const uint64_t *aadvec_start; /* num_records + 1 entries */
+  const uint8_t *nonces;
+  size_t nonce_len;
+  uint8_t *tags;
+  uint8_t *status;
+} BSSL_AMD_IOV_BATCH;
+
+BSSL_AMD_EXPORT int EVP_AEAD_CTX_sealv_batch_device(const EVP_AEAD_CTX *ctx,
+                                                    const BSSL_AMD_IOV_BATCH *batch,
+                                                    void *hip_stream);
+BSSL_AMD_EXPORT int EVP_AEAD_CTX_openv_detached_batch_device(const EVP_AEAD_CTX *ctx,
+                                                             const BSSL_AMD_IOV_BATCH *batch,
+                                                             void *hip_stream);
 
 /* Many keys of one AEAD (the multi-session case): key material for all keys
  * is expanded once and kept resident in device memory. */

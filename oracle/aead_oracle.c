@@ -489,6 +489,70 @@ int oracle_chacha20_poly1305_open(const uint8_t key[32], const uint8_t *nonce,
   return 1;
 }
 
+/* HChaCha20 (draft-irtf-cfrg-xchacha-03 section 2.2); reference
+ * CRYPTO_hchacha20, crypto/chacha/chacha.cc:43-63: the ChaCha20 state of
+ * (key, 16-byte nonce) after 20 rounds, words 0-3 and 12-15, no feed-forward. */
+void oracle_hchacha20(uint8_t out[32], const uint8_t key[32],
+                      const uint8_t nonce[16]) {
+  uint32_t x[16];
+  x[0] = 0x61707865; x[1] = 0x3320646e; x[2] = 0x79622d32; x[3] = 0x6b206574;
+  for (int i = 0; i < 8; i++) x[4 + i] = load_le32(key + 4 * i);
+  for (int i = 0; i < 4; i++) x[12 + i] = load_le32(nonce + 4 * i);
+  for (int i = 0; i < 10; i++) {
+    QR(x[0], x[4], x[8], x[12]) QR(x[1], x[5], x[9], x[13])
+    QR(x[2], x[6], x[10], x[14]) QR(x[3], x[7], x[11], x[15])
+    QR(x[0], x[5], x[10], x[15]) QR(x[1], x[6], x[11], x[12])
+    QR(x[2], x[7], x[8], x[13]) QR(x[3], x[4], x[9], x[14])
+  }
+  for (int i = 0; i < 8; i++) {
+    const uint32_t v = x[i < 4 ? i : i + 8];
+    out[4 * i] = (uint8_t)v;
+    out[4 * i + 1] = (uint8_t)(v >> 8);
+    out[4 * i + 2] = (uint8_t)(v >> 16);
+    out[4 * i + 3] = (uint8_t)(v >> 24);
+  }
+}
+
+/* XChaCha20-Poly1305 (crypto/cipher/e_chacha20poly1305.cc:233-256, 310-330):
+ * 24-byte nonce, key' = HChaCha20(key, nonce[0:16]), nonce' = 0^4 || nonce[16:24],
+ * then ChaCha20-Poly1305 under (key', nonce'). */
+static int xchacha_derive(const uint8_t key[32], const uint8_t *nonce,
+                          size_t nonce_len, uint8_t dkey[32], uint8_t dnonce[12]) {
+  if (nonce_len != 24) return 0; /* e_chacha20poly1305.cc:241-244 */
+  oracle_hchacha20(dkey, key, nonce);
+  memset(dnonce, 0, 4);
+  memcpy(dnonce + 4, nonce + 16, 8);
+  return 1;
+}
+
+int oracle_xchacha20_poly1305_seal(const uint8_t key[32], const uint8_t *nonce,
+                                   size_t nonce_len, const uint8_t *in,
+                                   size_t in_len, const uint8_t *ad,
+                                   size_t ad_len, uint8_t *out, uint8_t *tag,
+                                   size_t tag_len) {
+  uint8_t dkey[32], dnonce[12];
+  if (!xchacha_derive(key, nonce, nonce_len, dkey, dnonce)) {
+    if (in_len) memset(out, 0, in_len);
+    return 0;
+  }
+  return oracle_chacha20_poly1305_seal(dkey, dnonce, 12, in, in_len, ad, ad_len,
+                                       out, tag, tag_len);
+}
+
+int oracle_xchacha20_poly1305_open(const uint8_t key[32], const uint8_t *nonce,
+                                   size_t nonce_len, const uint8_t *in,
+                                   size_t in_len, const uint8_t *ad,
+                                   size_t ad_len, const uint8_t *tag,
+                                   size_t tag_len, uint8_t *out) {
+  uint8_t dkey[32], dnonce[12];
+  if (!xchacha_derive(key, nonce, nonce_len, dkey, dnonce)) {
+    if (in_len) memset(out, 0, in_len);
+    return 0;
+  }
+  return oracle_chacha20_poly1305_open(dkey, dnonce, 12, in, in_len, ad, ad_len,
+                                       tag, tag_len, out);
+}
+
 /* ------------------------------------------------------------------------- */
 
 size_t oracle_batch(int aead, int seal, const uint8_t *keys, size_t key_len,
@@ -517,6 +581,15 @@ size_t oracle_batch(int aead, int seal, const uint8_t *keys, size_t key_len,
                                       lens[i], ai, ad_lens[i],
                                       tags + (size_t)i * tag_len, tag_len,
                                       out + offsets[i]);
+    } else if (aead == ORACLE_XCHACHA20_POLY1305) {
+      ok = seal ? oracle_xchacha20_poly1305_seal(
+                      k, ni, nonce_len, in + offsets[i], lens[i], ai,
+                      ad_lens[i], out + offsets[i], tags + (size_t)i * tag_len,
+                      tag_len)
+                : oracle_xchacha20_poly1305_open(
+                      k, ni, nonce_len, in + offsets[i], lens[i], ai,
+                      ad_lens[i], tags + (size_t)i * tag_len, tag_len,
+                      out + offsets[i]);
     } else {
       ok = seal ? oracle_chacha20_poly1305_seal(
                       k, ni, nonce_len, in + offsets[i], lens[i], ai,

@@ -33,6 +33,7 @@ const EVP_AEAD *aead_by_name(const std::string &n, size_t *key_len) {
   if (n == "aes-192-gcm") { *key_len = 24; return EVP_aead_aes_192_gcm(); }
   if (n == "aes-256-gcm") { *key_len = 32; return EVP_aead_aes_256_gcm(); }
   if (n == "chacha20-poly1305") { *key_len = 32; return EVP_aead_chacha20_poly1305(); }
+  if (n == "xchacha20-poly1305") { *key_len = 32; return EVP_aead_xchacha20_poly1305(); }
   fprintf(stderr, "unknown aead %s\n", n.c_str());
   exit(2);
 }
@@ -111,6 +112,18 @@ int cmd_edge() {
 //   tags_sha256 = SHA-256(tag_0 || tag_1 || ... )
 //   ct_sha256   = SHA-256(SHA-256(ct of records [0,1024)) || SHA-256(ct of
 //                 records [1024,2048)) || ...)   ("checksum of checksums")
+// Synthetic nonce of record i: synth_nonce(i) (12 bytes) and, for 24-byte
+// (XChaCha20-Poly1305) nonces, synth_nonce(i) again with bytes 4..11 XOR 0xff
+// (= synth_nonce(~i)).
+size_t make_nonce(uint64_t i, size_t nonce_len, uint8_t *out) {
+  synth_nonce(i, out);
+  if (nonce_len == 24) {
+    memcpy(out + 12, out, 12);
+    for (int b = 4; b < 12; b++) out[12 + b] ^= 0xff;
+  }
+  return nonce_len;
+}
+
 int cmd_digest(int argc, char **argv) {
   if (argc < 6) return 2;
   size_t key_len;
@@ -150,12 +163,12 @@ int cmd_digest(int argc, char **argv) {
         pt.resize(len + 1);
         ct.resize(len + 1);
         synth_pt(i, len, pt.data());
-        uint8_t nonce[12], ad[13];
-        synth_nonce(i, nonce);
+        uint8_t nonce[24], ad[13];
+        const size_t nl = make_nonce(i, EVP_AEAD_nonce_length(aead), nonce);
         synth_ad(i, len, ad);
         size_t tag_out = 0;
         if (!EVP_AEAD_CTX_seal_scatter(ctx.get(), ct.data(), &tags[16 * i], &tag_out, 16, nonce,
-                                       12, pt.data(), len, nullptr, 0, ad, 13))
+                                       nl, pt.data(), len, nullptr, 0, ad, 13))
           abort();
         SHA256_Update(&sha, ct.data(), len);
         total_bytes += len;
@@ -186,10 +199,11 @@ int cmd_bench(int argc, char **argv) {
   double secs = atof(argv[6]);
   const uint64_t stride = (len + 63) / 64 * 64;
   std::vector<uint8_t> pt(nrec * stride), ct(nrec * stride), tags(nrec * 16);
-  std::vector<uint8_t> nonces(nrec * 12), ads(nrec * 13);
+  const size_t nl = EVP_AEAD_nonce_length(aead);
+  std::vector<uint8_t> nonces(nrec * nl), ads(nrec * 13);
   for (uint64_t i = 0; i < nrec; i++) {
     synth_pt(i, len, &pt[i * stride]);
-    synth_nonce(i, &nonces[12 * i]);
+    make_nonce(i, nl, &nonces[nl * i]);
     synth_ad(i, len, &ads[13 * i]);
   }
   std::vector<uint8_t> key(key_len);
@@ -210,7 +224,7 @@ int cmd_bench(int argc, char **argv) {
       for (uint64_t i = lo; i < hi; i++) {
         size_t tag_out;
         if (!EVP_AEAD_CTX_seal_scatter(ctx.get(), &ct[i * stride], &tags[16 * i], &tag_out, 16,
-                                       &nonces[12 * i], 12, &pt[i * stride], len, nullptr, 0,
+                                       &nonces[nl * i], nl, &pt[i * stride], len, nullptr, 0,
                                        &ads[13 * i], 13))
           abort();
         count++;

@@ -14,6 +14,7 @@ _LIB_PATH = os.path.join(ROOT, "oracle", "liboracle.so")
 
 AES_GCM = 0
 CHACHA20_POLY1305 = 1
+XCHACHA20_POLY1305 = 2
 
 _P = ctypes.c_void_p
 _S = ctypes.c_size_t
@@ -32,6 +33,9 @@ def _load():
         "oracle_poly1305": (None, [_P, _P, _S, _P]),
         "oracle_chacha20_poly1305_seal": (ctypes.c_int, [_P, _P, _S, _P, _S, _P, _S, _P, _P, _S]),
         "oracle_chacha20_poly1305_open": (ctypes.c_int, [_P, _P, _S, _P, _S, _P, _S, _P, _S, _P]),
+        "oracle_hchacha20": (None, [_P, _P, _P]),
+        "oracle_xchacha20_poly1305_seal": (ctypes.c_int, [_P, _P, _S, _P, _S, _P, _S, _P, _P, _S]),
+        "oracle_xchacha20_poly1305_open": (ctypes.c_int, [_P, _P, _S, _P, _S, _P, _S, _P, _S, _P]),
         "oracle_batch": (_S, [ctypes.c_int, ctypes.c_int, _P, _S, _P, _S, _P, _P, _P, _P, _P, _S,
                               _P, _P, _P, _P, _S, _P, ctypes.c_int]),
         "synth_key": (None, [ctypes.c_uint64, _S, _P]),
@@ -85,6 +89,9 @@ def seal(aead, key, nonce, pt, ad, tag_len=16):
     if aead == AES_GCM:
         ok = lib().oracle_aes_gcm_seal(bytes(key), len(key), bytes(nonce), len(nonce), bytes(pt),
                                        len(pt), bytes(ad), len(ad), out, tag, tag_len)
+    elif aead == XCHACHA20_POLY1305:
+        ok = lib().oracle_xchacha20_poly1305_seal(bytes(key), bytes(nonce), len(nonce), bytes(pt),
+                                                  len(pt), bytes(ad), len(ad), out, tag, tag_len)
     else:
         ok = lib().oracle_chacha20_poly1305_seal(bytes(key), bytes(nonce), len(nonce), bytes(pt),
                                                  len(pt), bytes(ad), len(ad), out, tag, tag_len)
@@ -97,6 +104,10 @@ def open_(aead, key, nonce, ct, ad, tag):
     if aead == AES_GCM:
         ok = lib().oracle_aes_gcm_open(bytes(key), len(key), bytes(nonce), len(nonce), bytes(ct),
                                        len(ct), bytes(ad), len(ad), bytes(tag), len(tag), out)
+    elif aead == XCHACHA20_POLY1305:
+        ok = lib().oracle_xchacha20_poly1305_open(bytes(key), bytes(nonce), len(nonce), bytes(ct),
+                                                  len(ct), bytes(ad), len(ad), bytes(tag), len(tag),
+                                                  out)
     else:
         ok = lib().oracle_chacha20_poly1305_open(bytes(key), bytes(nonce), len(nonce), bytes(ct),
                                                  len(ct), bytes(ad), len(ad), bytes(tag), len(tag), out)
@@ -107,6 +118,12 @@ def chacha20(key, nonce, counter, data):
     out = ctypes.create_string_buffer(max(1, len(data)))
     lib().oracle_chacha20(out, bytes(data), len(data), bytes(key), bytes(nonce), counter)
     return out.raw[:len(data)]
+
+
+def hchacha20(key, nonce16):
+    out = ctypes.create_string_buffer(32)
+    lib().oracle_hchacha20(out, bytes(key), bytes(nonce16))
+    return out.raw
 
 
 def poly1305(key, msg):
@@ -160,3 +177,12 @@ def synth_batch(first, lens, align=16, threads=8):
     lib().synth_fill(first, len(lens), _ptr(offsets), _ptr(lens), _ptr(pt), _ptr(nonces),
                      _ptr(ads), threads)
     return pt, offsets, nonces, ads
+
+
+def xchacha_nonces(nonces12):
+    """24-byte synthetic nonces (ref_tool.cc make_nonce): synth_nonce(i) then
+    synth_nonce(i) with bytes 4..11 XOR 0xff (= synth_nonce(~i))."""
+    a = np.asarray(nonces12, dtype=np.uint8).reshape(-1, 12)
+    b = a.copy()
+    b[:, 4:] ^= 0xff
+    return np.ascontiguousarray(np.concatenate([a, b], axis=1)).reshape(-1)

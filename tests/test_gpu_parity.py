@@ -24,7 +24,12 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
 ORACLE_ID = {"aes-128-gcm": o.AES_GCM, "aes-192-gcm": o.AES_GCM, "aes-256-gcm": o.AES_GCM,
-             "chacha20-poly1305": o.CHACHA20_POLY1305}
+             "chacha20-poly1305": o.CHACHA20_POLY1305, "xchacha20-poly1305": o.XCHACHA20_POLY1305}
+
+
+def _nl(aead):
+    """Nonce length of the AEAD (EVP_AEAD_nonce_length)."""
+    return 24 if aead == "xchacha20-poly1305" else 12
 
 
 def _h(s):
@@ -108,7 +113,8 @@ def run_batch(aead, keys, key_index, ins, nonces, ads, tag_len, open_=False, tag
 # ---------------------------------------------------------------------------
 # reference known-answer files through the single-record host API
 
-@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-192-gcm", "aes-256-gcm", "chacha20-poly1305"])
+@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-192-gcm", "aes-256-gcm", "chacha20-poly1305",
+                                  "xchacha20-poly1305"])
 def test_kat_single_record(aead):
     cases = [c for c in load("kat_aead.json") if c["aead"] == aead]
     ctxs = {}
@@ -157,7 +163,7 @@ def test_batch_multikey_vectors(source):
     """Every record with its own key (keyset + key_index), seal then open."""
     cases = [c for c in load(source) if c.get("valid", True)]
     for (aead, nl, tag_len), grp in _groups(cases).items():
-        if aead == "chacha20-poly1305" and nl != 12:
+        if "chacha" in aead and nl != _nl(aead):
             continue
         if nl == 0:
             continue
@@ -175,7 +181,8 @@ def test_batch_multikey_vectors(source):
         assert back == ins
 
 
-@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm", "chacha20-poly1305"])
+@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm", "chacha20-poly1305",
+                                  "xchacha20-poly1305"])
 @pytest.mark.parametrize("layout", ["aligned", "unaligned", "inplace"])
 def test_batch_ragged_vs_oracle(aead, layout):
     rng = random.Random(hash((aead, layout)) & 0xffff)
@@ -184,7 +191,7 @@ def test_batch_ragged_vs_oracle(aead, layout):
     lens = [rng.choice([0, 1, 15, 16, 17, 63, 64, 65, 255, 256, 1000, 1350, 4097, 16384])
             for _ in range(n)]
     ins = [bytes(rng.getrandbits(8) for _ in range(l)) for l in lens]
-    nonces = [bytes(rng.getrandbits(8) for _ in range(12)) for _ in range(n)]
+    nonces = [bytes(rng.getrandbits(8) for _ in range(_nl(aead))) for _ in range(n)]
     ads = [bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 5, 13, 16, 40, 300])))
            for _ in range(n)]
     outs, tags, st = run_batch(aead, [key], None, ins, nonces, ads, 16,
@@ -196,7 +203,8 @@ def test_batch_ragged_vs_oracle(aead, layout):
         assert ok and outs[i] == ct and tags[i] == tag, (i, lens[i], len(ads[i]))
 
 
-@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm", "chacha20-poly1305"])
+@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm", "chacha20-poly1305",
+                                  "xchacha20-poly1305"])
 @pytest.mark.parametrize("multikey", [False, True])
 def test_batch_large_ragged_reordered(aead, multikey):
     """>= 4096 ragged records: the launcher processes them in length-class
@@ -205,7 +213,7 @@ def test_batch_large_ragged_reordered(aead, multikey):
     n = 5000
     lens = rng.choice([0, 1, 16, 17, 200, 1350, 4096, 9000, 16384, 16400], size=n).tolist()
     ins = [rng.integers(0, 256, size=l, dtype=np.uint8).tobytes() for l in lens]
-    nonces = [rng.integers(0, 256, size=12, dtype=np.uint8).tobytes() for _ in range(n)]
+    nonces = [rng.integers(0, 256, size=_nl(aead), dtype=np.uint8).tobytes() for _ in range(n)]
     ads = [rng.integers(0, 256, size=13, dtype=np.uint8).tobytes() for _ in range(n)]
     nkeys = 7 if multikey else 1
     keys = [rng.integers(0, 256, size=AEAD_KEYLEN[aead], dtype=np.uint8).tobytes()
@@ -271,13 +279,14 @@ def test_batch_gcm_nonce_lengths_and_truncated_tags():
                 assert outs[i] == ct and tags[i] == tag, (nl, tag_len, i)
 
 
-@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm", "chacha20-poly1305"])
+@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm", "chacha20-poly1305",
+                                  "xchacha20-poly1305"])
 def test_open_rejects_tampering_and_zeroes_output(aead):
     rng = random.Random(11)
     key = bytes(rng.getrandbits(8) for _ in range(AEAD_KEYLEN[aead]))
     n = 64
     ins = [bytes(rng.getrandbits(8) for _ in range(rng.randrange(1, 3000))) for _ in range(n)]
-    nonces = [bytes(rng.getrandbits(8) for _ in range(12)) for _ in range(n)]
+    nonces = [bytes(rng.getrandbits(8) for _ in range(_nl(aead))) for _ in range(n)]
     ads = [bytes(rng.getrandbits(8) for _ in range(13)) for _ in range(n)]
     cts, tags, st = run_batch(aead, [key], None, ins, nonces, ads, 16)
     assert st.all()
@@ -356,6 +365,13 @@ def _device_digests(d_out, offs, lens, d_tags, chunk=1024):
     return hashlib.sha256(tags).hexdigest(), hashlib.sha256(b"".join(parts)).hexdigest()
 
 
+def xchacha_nonces_device(d_n12):
+    a = d_n12.view(-1, 12)
+    b = a.clone()
+    b[:, 4:] ^= 0xff
+    return torch.cat([a, b], dim=1).contiguous().view(-1)
+
+
 def _run_synth_digest(name):
     g = load("ref_digests.json")[name]
     aead, nkeys, rpk, length = g["aead"], g["nkeys"], g["records_per_key"], g["len"]
@@ -365,7 +381,10 @@ def _run_synth_digest(name):
     d_tags = torch.zeros(16 * n, dtype=torch.uint8, device=DEV)
     d_st = torch.zeros(n, dtype=torch.uint8, device=DEV)
     keys = [o.synth_key(k, AEAD_KEYLEN[aead]) for k in range(nkeys)]
-    b = ba.make_batch(n, d_pt, d_out, d_tags, d_n, 12, d_a, offsets=d_offs, lengths=d_lens,
+    nl = _nl(aead)
+    if nl == 24:  # ref_tool.cc make_nonce: n_i || (n_i with bytes 4..11 XOR 0xff)
+        d_n = xchacha_nonces_device(d_n)
+    b = ba.make_batch(n, d_pt, d_out, d_tags, d_n, nl, d_a, offsets=d_offs, lengths=d_lens,
                       ad_stride=13, ad_len=13, status=d_st,
                       key_index=_t((np.arange(n) // rpk).astype(np.int32)) if nkeys > 1 else None)
     if nkeys > 1:
@@ -380,7 +399,7 @@ def _run_synth_digest(name):
     assert ct_d == g["ct_sha256"], name
     # open(seal(x)) == x, in place, all tags verify
     d_st.zero_()
-    b2 = ba.make_batch(n, d_out, d_out, d_tags, d_n, 12, d_a, offsets=d_offs, lengths=d_lens,
+    b2 = ba.make_batch(n, d_out, d_out, d_tags, d_n, nl, d_a, offsets=d_offs, lengths=d_lens,
                        ad_stride=13, ad_len=13, status=d_st, key_index=b._refs[-1])
     obj.open_batch_device(b2)
     torch.cuda.synchronize()
@@ -389,12 +408,13 @@ def _run_synth_digest(name):
 
 
 @pytest.mark.parametrize("name", ["parity_aes128_16k", "parity_aes256_mixed", "parity_chacha_1350",
-                                  "parity_multikey_aes128"])
+                                  "parity_multikey_aes128", "parity_xchacha_1350"])
 def test_synth_parity_digest(name):
     _run_synth_digest(name)
 
 
-@pytest.mark.parametrize("name", ["config2_aes128_16k", "config3_chacha_1350"])
+@pytest.mark.parametrize("name", ["config2_aes128_16k", "config3_chacha_1350",
+                                  "config3x_xchacha_1350"])
 def test_baseline_config_digest(name):
     """BASELINE.json configs 2 and 3 at full size (16 GiB / 1.3 GiB)."""
     _run_synth_digest(name)
@@ -685,3 +705,105 @@ def test_tls_record_layer_errors():
     with pytest.raises(ba.AEADError) as e:
         t.open_records_device(r)
     assert e.value.reason == ba.CIPHER_R_INVALID_OPERATION
+
+
+# ---------------------------------------------------------------------------
+# iovec batches: N EVP_AEAD_CTX_sealv / _openv_detached calls over device
+# chunks (aead.cc.inc:316-361, 531-584).
+
+def _split(rng, data, max_parts):
+    k = rng.randint(1, max_parts)
+    cuts = sorted(rng.randint(0, len(data)) for _ in range(k - 1))
+    parts, prev = [], 0
+    for c in cuts + [len(data)]:
+        parts.append(data[prev:c])
+        prev = c
+    return parts
+
+
+@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm", "chacha20-poly1305",
+                                  "xchacha20-poly1305"])
+def test_iovec_batch_vs_oracle(aead):
+    rng = random.Random(hash(aead) & 0xffff)
+    key = bytes(rng.getrandbits(8) for _ in range(AEAD_KEYLEN[aead]))
+    nl = _nl(aead)
+    n = 150
+    pts = [bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 1, 15, 16, 17, 100, 1350,
+                                                                   5000, 16384])))
+           for _ in range(n)]
+    ads = [bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 5, 13, 40]))) for _ in range(n)]
+    nonces = [bytes(rng.getrandbits(8) for _ in range(nl)) for _ in range(n)]
+    inplace = [rng.random() < 0.3 for _ in range(n)]
+    # Chunks at random (often odd) offsets of one input arena; outputs at the
+    # same offsets of an output arena, or in place.
+    chunks, starts, ad_chunks, ad_starts = [], [0], [], [0]
+    pos, apos = 0, 0
+    for i in range(n):
+        for part in _split(rng, pts[i], 5):
+            pos += rng.randint(0, 7)
+            chunks.append((pos, part, inplace[i]))
+            pos += len(part)
+        starts.append(len(chunks))
+        for part in _split(rng, ads[i], 3):
+            apos += rng.randint(0, 3)
+            ad_chunks.append((apos, part))
+            apos += len(part)
+        ad_starts.append(len(ad_chunks))
+    src = np.zeros(pos + 16, dtype=np.uint8)
+    for off, part, _ in chunks:
+        src[off:off + len(part)] = np.frombuffer(part, dtype=np.uint8)
+    adbuf = np.zeros(apos + 16, dtype=np.uint8)
+    for off, part in ad_chunks:
+        adbuf[off:off + len(part)] = np.frombuffer(part, dtype=np.uint8)
+    d_src, d_ad = _t(src), _t(adbuf)
+    d_dst = torch.zeros_like(d_src)
+    sb, db, ab = d_src.data_ptr(), d_dst.data_ptr(), d_ad.data_ptr()
+    iov = np.array([(sb + off if ip else db + off, sb + off, len(part)) for off, part, ip in chunks],
+                   dtype=np.int64).reshape(-1, 3)
+    aiv = np.array([(ab + off, len(part)) for off, part in ad_chunks], dtype=np.int64).reshape(-1, 2)
+    d_iov, d_aiv = _t(iov), _t(aiv)
+    d_starts, d_astarts = _t(np.array(starts, np.int64)), _t(np.array(ad_starts, np.int64))
+    d_nonce = _t(np.frombuffer(b"".join(nonces), dtype=np.uint8).copy())
+    d_tags = torch.zeros(16 * n, dtype=torch.uint8, device=DEV)
+    d_st = torch.full((n,), 7, dtype=torch.uint8, device=DEV)
+    ctx = ba.AEADCtx(aead, key, 16)
+    b = ba.make_iov_batch(n, d_iov, d_starts, d_tags, d_nonce, nl, aadvecs=d_aiv,
+                          aadvec_start=d_astarts, status=d_st)
+    ctx.sealv_batch_device(b)
+    torch.cuda.synchronize()
+    assert d_st.cpu().tolist() == [1] * n
+    out_src, out_dst, tags = d_src.cpu().numpy(), d_dst.cpu().numpy(), d_tags.cpu().numpy()
+
+    def gather(i, a, b_):
+        return b"".join((a if chunks[c][2] else b_)[chunks[c][0]:chunks[c][0] + len(chunks[c][1])]
+                        .tobytes() for c in range(starts[i], starts[i + 1]))
+
+    cts = []
+    for i in range(n):
+        ok, ct, tag = o.seal(ORACLE_ID[aead], key, nonces[i], pts[i], ads[i])
+        got = gather(i, out_src, out_dst)
+        assert ok and got == ct and tags[16 * i:16 * i + 16].tobytes() == tag, (i, len(pts[i]))
+        cts.append(ct)
+    # Open the ciphertext chunks (where the seal left them) into a third arena;
+    # corrupt every 7th tag: those records fail and their chunks are zeroed.
+    d_back = torch.full_like(d_src, 0xAA)
+    kb = d_back.data_ptr()
+    iov2 = np.array([(kb + off, (sb if ip else db) + off, len(part)) for off, part, ip in chunks],
+                    dtype=np.int64).reshape(-1, 3)
+    bad = set(range(0, n, 7))
+    tg = tags.copy()
+    for i in bad:
+        tg[16 * i] ^= 1
+    d_st.fill_(7)
+    b2 = ba.make_iov_batch(n, _t(iov2), d_starts, _t(tg), d_nonce, nl, aadvecs=d_aiv,
+                           aadvec_start=d_astarts, status=d_st)
+    ctx.openv_detached_batch_device(b2)
+    torch.cuda.synchronize()
+    st, back = d_st.cpu().numpy(), d_back.cpu().numpy()
+    for i in range(n):
+        got = b"".join(back[chunks[c][0]:chunks[c][0] + len(chunks[c][1])].tobytes()
+                       for c in range(starts[i], starts[i + 1]))
+        if i in bad:
+            assert st[i] == 0 and got == bytes(len(pts[i])), i
+        else:
+            assert st[i] == 1 and got == pts[i], i

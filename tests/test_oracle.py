@@ -12,7 +12,7 @@ import oracle_lib as o
 from golden_util import AEAD_KEYLEN, batch_digests, load
 
 AEAD_ID = {"aes-128-gcm": o.AES_GCM, "aes-192-gcm": o.AES_GCM, "aes-256-gcm": o.AES_GCM,
-           "chacha20-poly1305": o.CHACHA20_POLY1305}
+           "chacha20-poly1305": o.CHACHA20_POLY1305, "xchacha20-poly1305": o.XCHACHA20_POLY1305}
 
 
 def _h(s):
@@ -34,7 +34,8 @@ def test_poly1305_kat():
         assert o.poly1305(_h(c["key"]), _h(c["input"])).hex() == c["mac"], c["source"]
 
 
-@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-192-gcm", "aes-256-gcm", "chacha20-poly1305"])
+@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-192-gcm", "aes-256-gcm", "chacha20-poly1305",
+                                  "xchacha20-poly1305"])
 def test_aead_kat_files(aead):
     cases = [c for c in load("kat_aead.json") if c["aead"] == aead]
     assert cases
@@ -60,6 +61,15 @@ def test_aead_kat_files(aead):
             assert not ok, c["source"]
 
 
+def test_hchacha20_kat():
+    # draft-irtf-cfrg-xchacha-03 section 2.2.1 test vector (the construction of
+    # CRYPTO_hchacha20, crypto/chacha/chacha.cc:43-63).
+    key = bytes(range(32))
+    nonce = bytes.fromhex("000000090000004a0000000031415927")
+    assert o.hchacha20(key, nonce).hex() == (
+        "82413b4227b27bfed30e42508a877d73a0f9e4d58a74a853c12ec41326d3ecdc")
+
+
 def test_ref_edge_cases():
     cases = load("ref_edge.json")
     assert len(cases) > 200
@@ -82,7 +92,7 @@ def _parity_batch(aead, nkeys, rpk, length):
 
 
 @pytest.mark.parametrize("name", ["parity_aes128_16k", "parity_aes256_mixed", "parity_chacha_1350",
-                                  "parity_multikey_aes128"])
+                                  "parity_multikey_aes128", "parity_xchacha_1350"])
 def test_oracle_batch_matches_reference_digest(name):
     g = load("ref_digests.json")[name]
     aead = g["aead"]
@@ -93,7 +103,10 @@ def test_oracle_batch_matches_reference_digest(name):
     tags = np.zeros(16 * n, dtype=np.uint8)
     ad_off = (np.arange(n, dtype=np.uint64) * np.uint64(13))
     ad_len = np.full(n, 13, dtype=np.uint64)
-    failed = o.batch(AEAD_ID[aead], 1, keys, key_len, key_index, pt, out, offsets, lens, nonces, 12,
+    nl = 12
+    if aead == "xchacha20-poly1305":
+        nonces, nl = o.xchacha_nonces(nonces), 24
+    failed = o.batch(AEAD_ID[aead], 1, keys, key_len, key_index, pt, out, offsets, lens, nonces, nl,
                      ads, ad_off, ad_len, tags, 16)
     assert failed == 0
     tags_d, ct_d = batch_digests(out, offsets, lens, tags)
@@ -103,6 +116,6 @@ def test_oracle_batch_matches_reference_digest(name):
     back = np.zeros_like(pt)
     status = np.zeros(n, dtype=np.uint8)
     failed = o.batch(AEAD_ID[aead], 0, keys, key_len, key_index, out, back, offsets, lens, nonces,
-                     12, ads, ad_off, ad_len, tags, 16, status)
+                     nl, ads, ad_off, ad_len, tags, 16, status)
     assert failed == 0 and status.all()
     assert np.array_equal(back, pt)
