@@ -489,6 +489,154 @@ int oracle_chacha20_poly1305_open(const uint8_t key[32], const uint8_t *nonce,
   return 1;
 }
 
+/* ------------------------------------------------------------------------- */
+/* AES-GCM-SIV (RFC 8452); reference crypto/cipher/e_aesgcmsiv.cc:533-867
+ * (the portable path).  POLYVAL is evaluated through GHASH exactly as the
+ * reference does (:604-682): H' = mulX_GHASH(ByteReverse(H)), blocks
+ * byte-reversed, result byte-reversed. */
+
+static void siv_byte_reverse(uint8_t b[16]) { /* e_aesgcmsiv.cc:624-629 */
+  for (int i = 0; i < 8; i++) {
+    uint8_t t = b[i];
+    b[i] = b[15 - i];
+    b[15 - i] = t;
+  }
+}
+
+/* e_aesgcmsiv.cc:634-645: b as a little-endian 128-bit integer V; V >>= 1,
+ * 0xe1 into the top byte if bit 0 was set; written back big-endian. */
+static void siv_reverse_and_mulX_ghash(uint8_t b[16]) {
+  uint8_t v[16];
+  const int carry = b[0] & 1;
+  for (int i = 0; i < 16; i++)
+    v[i] = (uint8_t)((b[i] >> 1) | (i < 15 ? (uint8_t)(b[i + 1] << 7) : 0));
+  if (carry) v[15] ^= 0xe1;
+  for (int i = 0; i < 16; i++) b[i] = v[15 - i];
+}
+
+typedef struct {
+  uint8_t h[16]; /* mulX_GHASH(ByteReverse(auth key)) */
+  uint8_t s[16]; /* GHASH-order accumulator */
+} siv_polyval;
+
+static void siv_polyval_init(siv_polyval *p, const uint8_t key[16]) {
+  memcpy(p->h, key, 16);
+  siv_reverse_and_mulX_ghash(p->h);
+  memset(p->s, 0, 16);
+}
+
+/* Zero-padded 16-byte blocks of `in` (e_aesgcmsiv.cc:697-711). */
+static void siv_polyval_update(siv_polyval *p, const uint8_t *in, size_t len) {
+  for (size_t o = 0; o < len; o += 16) {
+    uint8_t blk[16] = {0};
+    memcpy(blk, in + o, len - o < 16 ? len - o : 16);
+    siv_byte_reverse(blk);
+    for (int i = 0; i < 16; i++) p->s[i] ^= blk[i];
+    oracle_gf128_mul(p->s, p->h);
+  }
+}
+
+/* gcm_siv_polyval (e_aesgcmsiv.cc:686-736): POLYVAL over AD || PT || lengths,
+ * XOR the nonce, clear the top bit. */
+static void siv_tag_input(const uint8_t auth_key[16], const uint8_t *ad, size_t ad_len,
+                          const uint8_t *pt, size_t pt_len, const uint8_t nonce[12],
+                          uint8_t out[16]) {
+  siv_polyval p;
+  siv_polyval_init(&p, auth_key);
+  siv_polyval_update(&p, ad, ad_len);
+  siv_polyval_update(&p, pt, pt_len);
+  uint8_t lens[16];
+  for (int i = 0; i < 8; i++) {
+    lens[i] = (uint8_t)(((uint64_t)ad_len * 8) >> (8 * i));
+    lens[8 + i] = (uint8_t)(((uint64_t)pt_len * 8) >> (8 * i));
+  }
+  siv_polyval_update(&p, lens, 16);
+  memcpy(out, p.s, 16);
+  siv_byte_reverse(out);
+  for (int i = 0; i < 12; i++) out[i] ^= nonce[i];
+  out[15] &= 0x7f;
+}
+
+/* gcm_siv_keys (e_aesgcmsiv.cc:750-780): AES_K(le32(i) || nonce)[0:8] for
+ * i = 0..3 (AES-128) or 0..5 (AES-256): 16-byte auth key, then the record's
+ * encryption key. */
+static void siv_record_keys(const uint8_t *key, size_t key_len, const uint8_t nonce[12],
+                            uint8_t auth_key[16], uint8_t enc_key[32]) {
+  uint8_t material[48];
+  const int blocks = key_len == 32 ? 6 : 4;
+  for (int i = 0; i < blocks; i++) {
+    uint8_t ctr[16] = {0}, ks[16];
+    ctr[0] = (uint8_t)i;
+    memcpy(ctr + 4, nonce, 12);
+    oracle_aes_encrypt_block(key, key_len, ctr, ks);
+    memcpy(material + 8 * i, ks, 8);
+  }
+  memcpy(auth_key, material, 16);
+  memcpy(enc_key, material + 16, key_len);
+}
+
+/* gcm_siv_crypt (e_aesgcmsiv.cc:571-601): CTR from the tag with byte 15 |=
+ * 0x80 and a little-endian 32-bit counter in bytes 0..3. */
+static void siv_ctr(const uint8_t *enc_key, size_t key_len, const uint8_t tag[16],
+                    const uint8_t *in, uint8_t *out, size_t len) {
+  uint8_t ctr[16], ks[16];
+  memcpy(ctr, tag, 16);
+  ctr[15] |= 0x80;
+  for (size_t o = 0; o < len; o += 16) {
+    oracle_aes_encrypt_block(enc_key, key_len, ctr, ks);
+    uint32_t c = (uint32_t)ctr[0] | ((uint32_t)ctr[1] << 8) | ((uint32_t)ctr[2] << 16) |
+                 ((uint32_t)ctr[3] << 24);
+    c++;
+    ctr[0] = (uint8_t)c; ctr[1] = (uint8_t)(c >> 8); ctr[2] = (uint8_t)(c >> 16);
+    ctr[3] = (uint8_t)(c >> 24);
+    for (size_t i = 0; i < 16 && o + i < len; i++) out[o + i] = in[o + i] ^ ks[i];
+  }
+}
+
+/* aead_aes_gcm_siv_sealv (e_aesgcmsiv.cc:782-823).  tag_len must be 16
+ * (aead_aes_gcm_siv_init, :542-548). */
+int oracle_aes_gcm_siv_seal(const uint8_t *key, size_t key_len, const uint8_t *nonce,
+                            size_t nonce_len, const uint8_t *in, size_t in_len,
+                            const uint8_t *ad, size_t ad_len, uint8_t *out, uint8_t *tag,
+                            size_t tag_len) {
+  if ((key_len != 16 && key_len != 32) || tag_len != 16 || nonce_len != 12 ||
+      (uint64_t)in_len > (UINT64_C(1) << 36) || (uint64_t)ad_len >= (UINT64_C(1) << 61)) {
+    if (in_len) memset(out, 0, in_len);
+    return 0;
+  }
+  uint8_t auth_key[16], enc_key[32], t[16];
+  siv_record_keys(key, key_len, nonce, auth_key, enc_key);
+  siv_tag_input(auth_key, ad, ad_len, in, in_len, nonce, t);
+  oracle_aes_encrypt_block(enc_key, key_len, t, t);
+  siv_ctr(enc_key, key_len, t, in, out, in_len);
+  memcpy(tag, t, 16);
+  return 1;
+}
+
+/* aead_aes_gcm_siv_openv_detached (e_aesgcmsiv.cc:825-867). */
+int oracle_aes_gcm_siv_open(const uint8_t *key, size_t key_len, const uint8_t *nonce,
+                            size_t nonce_len, const uint8_t *in, size_t in_len,
+                            const uint8_t *ad, size_t ad_len, const uint8_t *tag,
+                            size_t tag_len, uint8_t *out) {
+  if ((key_len != 16 && key_len != 32) || tag_len != 16 || nonce_len != 12 ||
+      (uint64_t)in_len > (UINT64_C(1) << 36) || (uint64_t)ad_len >= (UINT64_C(1) << 61)) {
+    if (in_len) memset(out, 0, in_len);
+    return 0;
+  }
+  uint8_t auth_key[16], enc_key[32], t[16];
+  siv_record_keys(key, key_len, nonce, auth_key, enc_key);
+  siv_ctr(enc_key, key_len, tag, in, out, in_len);
+  siv_tag_input(auth_key, ad, ad_len, out, in_len, nonce, t);
+  oracle_aes_encrypt_block(enc_key, key_len, t, t);
+  uint8_t diff = 0;
+  for (int i = 0; i < 16; i++) diff |= t[i] ^ tag[i];
+  if (diff) {
+    if (in_len) memset(out, 0, in_len);
+    return 0;
+  }
+  return 1;
+}
+
 /* HChaCha20 (draft-irtf-cfrg-xchacha-03 section 2.2); reference
  * CRYPTO_hchacha20, crypto/chacha/chacha.cc:43-63: the ChaCha20 state of
  * (key, 16-byte nonce) after 20 rounds, words 0-3 and 12-15, no feed-forward. */
@@ -581,6 +729,13 @@ size_t oracle_batch(int aead, int seal, const uint8_t *keys, size_t key_len,
                                       lens[i], ai, ad_lens[i],
                                       tags + (size_t)i * tag_len, tag_len,
                                       out + offsets[i]);
+    } else if (aead == ORACLE_AES_GCM_SIV) {
+      ok = seal ? oracle_aes_gcm_siv_seal(k, key_len, ni, nonce_len, in + offsets[i], lens[i],
+                                          ai, ad_lens[i], out + offsets[i],
+                                          tags + (size_t)i * tag_len, tag_len)
+                : oracle_aes_gcm_siv_open(k, key_len, ni, nonce_len, in + offsets[i], lens[i],
+                                          ai, ad_lens[i], tags + (size_t)i * tag_len, tag_len,
+                                          out + offsets[i]);
     } else if (aead == ORACLE_XCHACHA20_POLY1305) {
       ok = seal ? oracle_xchacha20_poly1305_seal(
                       k, ni, nonce_len, in + offsets[i], lens[i], ai,

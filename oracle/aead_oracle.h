@@ -24,7 +24,8 @@ extern "C" {
 enum {
   ORACLE_AES_GCM = 0,          /* key 16/24/32 bytes */
   ORACLE_CHACHA20_POLY1305 = 1, /* key 32 bytes, nonce 12 bytes */
-  ORACLE_XCHACHA20_POLY1305 = 2 /* key 32 bytes, nonce 24 bytes */
+  ORACLE_XCHACHA20_POLY1305 = 2, /* key 32 bytes, nonce 24 bytes */
+  ORACLE_AES_GCM_SIV = 3          /* key 16/32 bytes, nonce 12 bytes, tag 16 */
 };
 
 /* AES (FIPS-197) single block, key 16/24/32 bytes. */
@@ -66,6 +67,16 @@ int oracle_chacha20_poly1305_open(const uint8_t key[32], const uint8_t *nonce,
                                   size_t in_len, const uint8_t *ad,
                                   size_t ad_len, const uint8_t *tag,
                                   size_t tag_len, uint8_t *out);
+
+/* AES-GCM-SIV (RFC 8452; crypto/cipher/e_aesgcmsiv.cc:533-867). */
+int oracle_aes_gcm_siv_seal(const uint8_t *key, size_t key_len, const uint8_t *nonce,
+                            size_t nonce_len, const uint8_t *in, size_t in_len,
+                            const uint8_t *ad, size_t ad_len, uint8_t *out, uint8_t *tag,
+                            size_t tag_len);
+int oracle_aes_gcm_siv_open(const uint8_t *key, size_t key_len, const uint8_t *nonce,
+                            size_t nonce_len, const uint8_t *in, size_t in_len,
+                            const uint8_t *ad, size_t ad_len, const uint8_t *tag,
+                            size_t tag_len, uint8_t *out);
 
 /* HChaCha20 and XChaCha20-Poly1305 (crypto/chacha/chacha.cc:43-63,
  * crypto/cipher/e_chacha20poly1305.cc:233-256, 310-330). */

@@ -34,6 +34,8 @@ const EVP_AEAD *aead_by_name(const std::string &n, size_t *key_len) {
   if (n == "aes-256-gcm") { *key_len = 32; return EVP_aead_aes_256_gcm(); }
   if (n == "chacha20-poly1305") { *key_len = 32; return EVP_aead_chacha20_poly1305(); }
   if (n == "xchacha20-poly1305") { *key_len = 32; return EVP_aead_xchacha20_poly1305(); }
+  if (n == "aes-128-gcm-siv") { *key_len = 16; return EVP_aead_aes_128_gcm_siv(); }
+  if (n == "aes-256-gcm-siv") { *key_len = 32; return EVP_aead_aes_256_gcm_siv(); }
   fprintf(stderr, "unknown aead %s\n", n.c_str());
   exit(2);
 }

@@ -9,9 +9,11 @@ reads the committed JSON.  Three kinds of fixture are produced:
                        crypto/cipher/test/aes_{128,192,256}_gcm_tests.txt
                        crypto/cipher/test/chacha20_poly1305_tests.txt
                        crypto/cipher/test/xchacha20_poly1305_tests.txt
+                       crypto/cipher/test/aes_{128,256}_gcm_siv_tests.txt
                        third_party/wycheproof_testvectors/aes_gcm_test.txt
                        third_party/wycheproof_testvectors/chacha20_poly1305_test.txt
                        third_party/wycheproof_testvectors/xchacha20_poly1305_test.txt
+                       third_party/wycheproof_testvectors/aes_gcm_siv_test.txt
                        crypto/fipsmodule/aes/aes_tests.txt
                        crypto/poly1305/poly1305_tests.txt
                      The field semantics follow crypto/cipher/aead_test.cc:188-281
@@ -87,6 +89,8 @@ def convert_aead():
         ("crypto/cipher/test/aes_256_gcm_tests.txt", "aes-256-gcm"),
         ("crypto/cipher/test/chacha20_poly1305_tests.txt", "chacha20-poly1305"),
         ("crypto/cipher/test/xchacha20_poly1305_tests.txt", "xchacha20-poly1305"),
+        ("crypto/cipher/test/aes_128_gcm_siv_tests.txt", "aes-128-gcm-siv"),
+        ("crypto/cipher/test/aes_256_gcm_siv_tests.txt", "aes-256-gcm-siv"),
     ]
     for rel, aead in files:
         for i, c in enumerate(parse_filetest(os.path.join(REF, rel))):
@@ -99,12 +103,17 @@ def convert_aead():
         ("third_party/wycheproof_testvectors/aes_gcm_test.txt", "gcm"),
         ("third_party/wycheproof_testvectors/chacha20_poly1305_test.txt", "chacha"),
         ("third_party/wycheproof_testvectors/xchacha20_poly1305_test.txt", "xchacha"),
+        ("third_party/wycheproof_testvectors/aes_gcm_siv_test.txt", "siv"),
     ]
     for rel, kind in wfiles:
         for c in parse_filetest(os.path.join(REF, rel)):
             ins = c["_instr"]
             if kind == "gcm":
                 aead = {"128": "aes-128-gcm", "192": "aes-192-gcm", "256": "aes-256-gcm"}[ins["keySize"]]
+            elif kind == "siv":
+                aead = {"128": "aes-128-gcm-siv", "256": "aes-256-gcm-siv"}.get(ins["keySize"])
+                if aead is None:
+                    continue  # 192-bit keys: no such EVP_AEAD
             elif kind == "chacha":
                 aead = "chacha20-poly1305"
             else:
@@ -152,9 +161,13 @@ DIGESTS = [
     ("parity_chacha_1350", "chacha20-poly1305", 1, 16384, "1350"),
     ("parity_multikey_aes128", "aes-128-gcm", 256, 16, "16384"),
     ("parity_xchacha_1350", "xchacha20-poly1305", 1, 16384, "1350"),
+    ("parity_siv128_1350", "aes-128-gcm-siv", 1, 16384, "1350"),
+    ("parity_siv256_mixed", "aes-256-gcm-siv", 1, 4096, "mixed"),
+    ("parity_siv128_multikey", "aes-128-gcm-siv", 64, 16, "16384"),
     ("config2_aes128_16k", "aes-128-gcm", 1, 1048576, "16384"),
     ("config3_chacha_1350", "chacha20-poly1305", 1, 1048576, "1350"),
     ("config3x_xchacha_1350", "xchacha20-poly1305", 1, 1048576, "1350"),
+    ("configs_siv128_16k", "aes-128-gcm-siv", 1, 262144, "16384"),
     ("config4_aes256_mixed", "aes-256-gcm", 1, 4194304, "mixed"),
     ("config5_multikey_aes128", "aes-128-gcm", 65536, 64, "16384"),
 ]
@@ -168,7 +181,8 @@ def main():
     # attach Wycheproof tcIds (comment lines precede each record in file order)
     for rel in ("third_party/wycheproof_testvectors/aes_gcm_test.txt",
                 "third_party/wycheproof_testvectors/chacha20_poly1305_test.txt",
-                "third_party/wycheproof_testvectors/xchacha20_poly1305_test.txt"):
+                "third_party/wycheproof_testvectors/xchacha20_poly1305_test.txt",
+                "third_party/wycheproof_testvectors/aes_gcm_siv_test.txt"):
         ids = _tcids(os.path.join(REF, rel))
         recs = [r for r in aead if r["source"].startswith(rel)]
         assert len(ids) == len(recs), (rel, len(ids), len(recs))

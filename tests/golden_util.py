@@ -12,7 +12,7 @@ import numpy as np
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 AEAD_KEYLEN = {"aes-128-gcm": 16, "aes-192-gcm": 24, "aes-256-gcm": 32, "chacha20-poly1305": 32,
-               "xchacha20-poly1305": 32}
+               "xchacha20-poly1305": 32, "aes-128-gcm-siv": 16, "aes-256-gcm-siv": 32}
 
 
 def load(name):

@@ -15,6 +15,7 @@ _LIB_PATH = os.path.join(ROOT, "oracle", "liboracle.so")
 AES_GCM = 0
 CHACHA20_POLY1305 = 1
 XCHACHA20_POLY1305 = 2
+AES_GCM_SIV = 3
 
 _P = ctypes.c_void_p
 _S = ctypes.c_size_t
@@ -34,6 +35,8 @@ def _load():
         "oracle_chacha20_poly1305_seal": (ctypes.c_int, [_P, _P, _S, _P, _S, _P, _S, _P, _P, _S]),
         "oracle_chacha20_poly1305_open": (ctypes.c_int, [_P, _P, _S, _P, _S, _P, _S, _P, _S, _P]),
         "oracle_hchacha20": (None, [_P, _P, _P]),
+        "oracle_aes_gcm_siv_seal": (ctypes.c_int, [_P, _S, _P, _S, _P, _S, _P, _S, _P, _P, _S]),
+        "oracle_aes_gcm_siv_open": (ctypes.c_int, [_P, _S, _P, _S, _P, _S, _P, _S, _P, _S, _P]),
         "oracle_xchacha20_poly1305_seal": (ctypes.c_int, [_P, _P, _S, _P, _S, _P, _S, _P, _P, _S]),
         "oracle_xchacha20_poly1305_open": (ctypes.c_int, [_P, _P, _S, _P, _S, _P, _S, _P, _S, _P]),
         "oracle_batch": (_S, [ctypes.c_int, ctypes.c_int, _P, _S, _P, _S, _P, _P, _P, _P, _P, _S,
@@ -89,6 +92,10 @@ def seal(aead, key, nonce, pt, ad, tag_len=16):
     if aead == AES_GCM:
         ok = lib().oracle_aes_gcm_seal(bytes(key), len(key), bytes(nonce), len(nonce), bytes(pt),
                                        len(pt), bytes(ad), len(ad), out, tag, tag_len)
+    elif aead == AES_GCM_SIV:
+        ok = lib().oracle_aes_gcm_siv_seal(bytes(key), len(key), bytes(nonce), len(nonce),
+                                           bytes(pt), len(pt), bytes(ad), len(ad), out, tag,
+                                           tag_len)
     elif aead == XCHACHA20_POLY1305:
         ok = lib().oracle_xchacha20_poly1305_seal(bytes(key), bytes(nonce), len(nonce), bytes(pt),
                                                   len(pt), bytes(ad), len(ad), out, tag, tag_len)
@@ -104,6 +111,10 @@ def open_(aead, key, nonce, ct, ad, tag):
     if aead == AES_GCM:
         ok = lib().oracle_aes_gcm_open(bytes(key), len(key), bytes(nonce), len(nonce), bytes(ct),
                                        len(ct), bytes(ad), len(ad), bytes(tag), len(tag), out)
+    elif aead == AES_GCM_SIV:
+        ok = lib().oracle_aes_gcm_siv_open(bytes(key), len(key), bytes(nonce), len(nonce),
+                                           bytes(ct), len(ct), bytes(ad), len(ad), bytes(tag),
+                                           len(tag), out)
     elif aead == XCHACHA20_POLY1305:
         ok = lib().oracle_xchacha20_poly1305_open(bytes(key), bytes(nonce), len(nonce), bytes(ct),
                                                   len(ct), bytes(ad), len(ad), bytes(tag), len(tag),

@@ -12,7 +12,8 @@ import oracle_lib as o
 from golden_util import AEAD_KEYLEN, batch_digests, load
 
 AEAD_ID = {"aes-128-gcm": o.AES_GCM, "aes-192-gcm": o.AES_GCM, "aes-256-gcm": o.AES_GCM,
-           "chacha20-poly1305": o.CHACHA20_POLY1305, "xchacha20-poly1305": o.XCHACHA20_POLY1305}
+           "chacha20-poly1305": o.CHACHA20_POLY1305, "xchacha20-poly1305": o.XCHACHA20_POLY1305,
+           "aes-128-gcm-siv": o.AES_GCM_SIV, "aes-256-gcm-siv": o.AES_GCM_SIV}
 
 
 def _h(s):
@@ -35,7 +36,7 @@ def test_poly1305_kat():
 
 
 @pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-192-gcm", "aes-256-gcm", "chacha20-poly1305",
-                                  "xchacha20-poly1305"])
+                                  "xchacha20-poly1305", "aes-128-gcm-siv", "aes-256-gcm-siv"])
 def test_aead_kat_files(aead):
     cases = [c for c in load("kat_aead.json") if c["aead"] == aead]
     assert cases
@@ -92,7 +93,9 @@ def _parity_batch(aead, nkeys, rpk, length):
 
 
 @pytest.mark.parametrize("name", ["parity_aes128_16k", "parity_aes256_mixed", "parity_chacha_1350",
-                                  "parity_multikey_aes128", "parity_xchacha_1350"])
+                                  "parity_multikey_aes128", "parity_xchacha_1350",
+                                  "parity_siv128_1350", "parity_siv256_mixed",
+                                  "parity_siv128_multikey"])
 def test_oracle_batch_matches_reference_digest(name):
     g = load("ref_digests.json")[name]
     aead = g["aead"]
