@@ -56,7 +56,8 @@ evp_aead_seal = 1
 # Every symbol include/bssl_amd/*.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = [
     "EVP_aead_aes_128_gcm", "EVP_aead_aes_192_gcm", "EVP_aead_aes_256_gcm",
-    "EVP_aead_chacha20_poly1305", "EVP_aead_xchacha20_poly1305", "EVP_aead_aes_128_gcm_tls12", "EVP_aead_aes_256_gcm_tls12",
+    "EVP_aead_chacha20_poly1305", "EVP_aead_xchacha20_poly1305",
+    "EVP_aead_aes_128_gcm_siv", "EVP_aead_aes_256_gcm_siv", "EVP_aead_aes_128_gcm_tls12", "EVP_aead_aes_256_gcm_tls12",
     "EVP_aead_aes_128_gcm_tls13", "EVP_aead_aes_256_gcm_tls13",
     "EVP_AEAD_key_length", "EVP_AEAD_nonce_length", "EVP_AEAD_max_overhead",
     "EVP_AEAD_max_tag_len", "EVP_AEAD_CTX_zero", "EVP_AEAD_CTX_new", "EVP_AEAD_CTX_free",
@@ -185,6 +186,8 @@ AEADS = {
     "aes-256-gcm": _lib.EVP_aead_aes_256_gcm,
     "chacha20-poly1305": _lib.EVP_aead_chacha20_poly1305,
     "xchacha20-poly1305": _lib.EVP_aead_xchacha20_poly1305,
+    "aes-128-gcm-siv": _lib.EVP_aead_aes_128_gcm_siv,
+    "aes-256-gcm-siv": _lib.EVP_aead_aes_256_gcm_siv,
     "aes-128-gcm-tls12": _lib.EVP_aead_aes_128_gcm_tls12,
     "aes-256-gcm-tls12": _lib.EVP_aead_aes_256_gcm_tls12,
     "aes-128-gcm-tls13": _lib.EVP_aead_aes_128_gcm_tls13,

@@ -79,6 +79,8 @@ const evp_aead_st kAes192Gcm = {24, 12, 16, 16, kAeadAesGcm, 0};
 const evp_aead_st kAes256Gcm = {32, 12, 16, 16, kAeadAesGcm, 0};
 const evp_aead_st kChaChaPoly = {32, 12, 16, 16, kAeadChaChaPoly, 0};
 const evp_aead_st kXChaChaPoly = {32, 24, 16, 16, kAeadXChaChaPoly, 0};  // e_chacha20poly1305.cc:385-399
+const evp_aead_st kAes128GcmSiv = {16, 12, 16, 16, kAeadAesGcmSiv, 0};  // e_aesgcmsiv.cc:869-899
+const evp_aead_st kAes256GcmSiv = {32, 12, 16, 16, kAeadAesGcmSiv, 0};
 const evp_aead_st kAes128GcmTls12 = {16, 12, 16, 16, kAeadAesGcm, 12};
 const evp_aead_st kAes256GcmTls12 = {32, 12, 16, 16, kAeadAesGcm, 12};
 const evp_aead_st kAes128GcmTls13 = {16, 12, 16, 16, kAeadAesGcm, 13};
@@ -112,7 +114,7 @@ KeyMaterial *make_keys(const EVP_AEAD *aead, const uint8_t *keys, size_t num_key
   if (!km) return nullptr;
   size_t bytes;
   std::vector<uint8_t> host;
-  if (aead->kind == kAeadAesGcm) {
+  if (aead->kind == kAeadAesGcm || aead->kind == kAeadAesGcmSiv) {
     bytes = num_keys * sizeof(GcmKeyDev);
     host.resize(bytes);
     GcmKeyDev *h = reinterpret_cast<GcmKeyDev *>(host.data());
@@ -191,6 +193,9 @@ int launch_desc(const KeyMaterial *km, const BatchDesc &d, bool open, void *stre
   if (km->aead->kind == kAeadAesGcm) {
     rc = launch_gcm(static_cast<const GcmKeyDev *>(km->dev), d, open, km->nr, stream, ev);
     t_timing.last_name = "gcm_kernel";
+  } else if (km->aead->kind == kAeadAesGcmSiv) {
+    rc = launch_gcm_siv(static_cast<const GcmKeyDev *>(km->dev), d, open, km->nr, stream, ev);
+    t_timing.last_name = "gcm_siv_kernel";
   } else {
     rc = launch_chacha(static_cast<const ChaChaKeyDev *>(km->dev), d, open,
                        km->aead->kind == kAeadXChaChaPoly, stream, ev);
@@ -473,6 +478,15 @@ bool aead_record_checks(const EVP_AEAD_CTX *ctx, size_t nonce_len, size_t in_len
       PUT_ERROR(CIPHER_R_INVALID_NONCE_SIZE);
       return false;
     }
+  } else if (aead->kind == kAeadAesGcmSiv) {
+    if (nonce_len != 12) {  // e_aesgcmsiv.cc:805-808, 843-846
+      PUT_ERROR(CIPHER_R_UNSUPPORTED_NONCE_SIZE);
+      return false;
+    }
+    if ((uint64_t)in_len > (UINT64_C(1) << 36)) {  // :794-798
+      PUT_ERROR(CIPHER_R_TOO_LARGE);
+      return false;
+    }
   } else {
     if (nonce_len != aead->nonce_len) {  // 12, or 24 for XChaCha (e_chacha20poly1305.cc:241)
       PUT_ERROR(CIPHER_R_UNSUPPORTED_NONCE_SIZE);
@@ -497,6 +511,8 @@ const EVP_AEAD *EVP_aead_aes_192_gcm(void) { return &kAes192Gcm; }
 const EVP_AEAD *EVP_aead_aes_256_gcm(void) { return &kAes256Gcm; }
 const EVP_AEAD *EVP_aead_chacha20_poly1305(void) { return &kChaChaPoly; }
 const EVP_AEAD *EVP_aead_xchacha20_poly1305(void) { return &kXChaChaPoly; }
+const EVP_AEAD *EVP_aead_aes_128_gcm_siv(void) { return &kAes128GcmSiv; }
+const EVP_AEAD *EVP_aead_aes_256_gcm_siv(void) { return &kAes256GcmSiv; }
 const EVP_AEAD *EVP_aead_aes_128_gcm_tls12(void) { return &kAes128GcmTls12; }
 const EVP_AEAD *EVP_aead_aes_256_gcm_tls12(void) { return &kAes256GcmTls12; }
 const EVP_AEAD *EVP_aead_aes_128_gcm_tls13(void) { return &kAes128GcmTls13; }
@@ -544,8 +560,10 @@ int EVP_AEAD_CTX_init_with_direction(EVP_AEAD_CTX *ctx, const EVP_AEAD *aead,
   }
   // e_aes.cc.inc:742-749 / e_chacha20poly1305.cc:51-57
   if (tag_len == EVP_AEAD_DEFAULT_TAG_LENGTH) tag_len = aead->max_tag_len;
-  if (tag_len > aead->max_tag_len) {
-    PUT_ERROR(aead->kind == kAeadAesGcm ? CIPHER_R_TAG_TOO_LARGE : CIPHER_R_TOO_LARGE);
+  if (tag_len > aead->max_tag_len ||
+      (aead->kind == kAeadAesGcmSiv && tag_len != 16)) {  // e_aesgcmsiv.cc:542-548
+    PUT_ERROR(aead->kind == kAeadAesGcm || aead->kind == kAeadAesGcmSiv ? CIPHER_R_TAG_TOO_LARGE
+                                                                       : CIPHER_R_TOO_LARGE);
     ctx->aead = nullptr;
     return 0;
   }

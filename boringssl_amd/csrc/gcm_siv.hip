@@ -1,0 +1,406 @@
+// gcm_siv.hip -- AES-GCM-SIV (RFC 8452) seal / open over device-resident
+// record batches.
+//
+// Replaces aead_aes_gcm_siv_sealv / _openv_detached
+// (crypto/cipher/e_aesgcmsiv.cc:782-867) and their helpers gcm_siv_keys
+// (:750-780), gcm_siv_polyval (:686-736) and gcm_siv_crypt (:571-601).
+// Design:
+// * 16 lanes per record, 16 records per 256-thread workgroup.
+// * Per-record keys: lanes 0..3 (0..5 for AES-256) of a record encrypt
+//   le32(i) || nonce under the master key (T-table AES, tables in LDS) and the
+//   halves are exchanged by shuffles; lane 0 expands the record's encryption
+//   key into the record's LDS slot.
+// * POLYVAL through GHASH, as the reference computes it (:604-682):
+//   H_g = mulX_GHASH(ByteReverse(H)) and every block byte-reversed -- which in
+//   big-endian words is the block's little-endian words in reverse order, so
+//   it costs nothing.  Products use Shoup's 4-bit method with one 16-entry
+//   table per power of H_g in LDS (M[v] = v(x) * H_g^k) and the 4-bit
+//   reduction computed arithmetically: 32 dependent nibble steps, no
+//   position-dependent tables (which would be 8 KiB per power per record).
+//   Lane q folds the elements j = q, q+16, ... of [AD blocks, message blocks,
+//   length block] with Horner's rule in H_g^16, multiplies its sum by
+//   H_g^(n - j_last) (tables H, H^2, H^4, H^8, H^16) and the 16 lanes are
+//   XOR-reduced.
+// * Seal: POLYVAL over the plaintext, tag = AES_K'(POLYVAL ^ nonce, bit 127
+//   cleared), then CTR from the tag (byte 15 |= 0x80, little-endian 32-bit
+//   counter in bytes 0..3): the plaintext is read twice, as SIV requires.
+//   Open: CTR and POLYVAL in one pass (the lane that decrypts a block folds
+//   it), then the tag compare; a failed record is zero-filled.
+#include <hip/hip_runtime.h>
+
+#include "internal.h"
+
+namespace bssl_amd {
+namespace {
+
+constexpr int kL = 16;                // lanes per record
+constexpr int kThreads = 256;
+constexpr int kRecs = kThreads / kL;  // records per workgroup
+constexpr int kPows = 5;              // H, H^2, H^4, H^8, H^16
+
+struct Tables {
+  uint32_t te0[256];
+};
+
+constexpr uint8_t cx_mul(uint8_t a, uint8_t b) {
+  uint8_t p = 0;
+  for (int i = 0; i < 8; i++) {
+    if (b & 1) p ^= a;
+    a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+    b >>= 1;
+  }
+  return p;
+}
+
+constexpr Tables make_tables() {
+  Tables t{};
+  for (int x = 0; x < 256; x++) {
+    uint8_t inv = 1, base = (uint8_t)x;  // x^254
+    for (int e = 254; e; e >>= 1) {
+      if (e & 1) inv = cx_mul(inv, base);
+      base = cx_mul(base, base);
+    }
+    if (!x) inv = 0;
+    uint8_t s = inv, r = inv;
+    for (int i = 0; i < 4; i++) {
+      r = (uint8_t)((r << 1) | (r >> 7));
+      s ^= r;
+    }
+    s ^= 0x63;
+    // bytes (2s, s, s, 3s): the MixColumns column of a row-0 byte
+    t.te0[x] = (uint32_t)cx_mul(s, 2) | ((uint32_t)s << 8) | ((uint32_t)s << 16) |
+               ((uint32_t)cx_mul(s, 3) << 24);
+  }
+  return t;
+}
+
+__constant__ Tables kSivTables = make_tables();
+
+struct Lds {
+  uint32_t t[4][256];          // T0..T3 (T_r = rotl(T0, 8r))
+  uint4 rk[kRecs][15];         // each record's encryption round keys
+  uint4 m[kRecs][kPows][16];   // each record's Shoup tables
+};
+
+__device__ __forceinline__ uint32_t rotl(uint32_t v, int n) {
+  return __builtin_amdgcn_alignbit(v, v, 32 - n);
+}
+
+__device__ __forceinline__ uint32_t sbox(const Lds &L, uint32_t x) {
+  return (L.t[0][x] >> 8) & 0xff;
+}
+
+// FIPS-197 cipher on little-endian column words; `rk` in LDS or global memory.
+template <int NR>
+__device__ __forceinline__ uint4 aes_enc(uint4 in, const uint4 *rk, const Lds &L) {
+  uint32_t s0 = in.x ^ rk[0].x, s1 = in.y ^ rk[0].y, s2 = in.z ^ rk[0].z, s3 = in.w ^ rk[0].w;
+#pragma unroll
+  for (int r = 1; r < NR; r++) {
+    const uint4 k = rk[r];
+    const uint32_t t0 = L.t[0][s0 & 0xff] ^ L.t[1][(s1 >> 8) & 0xff] ^
+                        L.t[2][(s2 >> 16) & 0xff] ^ L.t[3][s3 >> 24] ^ k.x;
+    const uint32_t t1 = L.t[0][s1 & 0xff] ^ L.t[1][(s2 >> 8) & 0xff] ^
+                        L.t[2][(s3 >> 16) & 0xff] ^ L.t[3][s0 >> 24] ^ k.y;
+    const uint32_t t2 = L.t[0][s2 & 0xff] ^ L.t[1][(s3 >> 8) & 0xff] ^
+                        L.t[2][(s0 >> 16) & 0xff] ^ L.t[3][s1 >> 24] ^ k.z;
+    const uint32_t t3 = L.t[0][s3 & 0xff] ^ L.t[1][(s0 >> 8) & 0xff] ^
+                        L.t[2][(s1 >> 16) & 0xff] ^ L.t[3][s2 >> 24] ^ k.w;
+    s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+  }
+  const uint4 k = rk[NR];
+  auto last = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return sbox(L, a & 0xff) | (sbox(L, (b >> 8) & 0xff) << 8) |
+           (sbox(L, (c >> 16) & 0xff) << 16) | (sbox(L, d >> 24) << 24);
+  };
+  return make_uint4(last(s0, s1, s2, s3) ^ k.x, last(s1, s2, s3, s0) ^ k.y,
+                    last(s2, s3, s0, s1) ^ k.z, last(s3, s0, s1, s2) ^ k.w);
+}
+
+// ---- GF(2^128) in GCM order, as big-endian words (w0 = bytes 0..3) --------
+
+__device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
+  return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
+}
+
+// * x (shift right by one, reduce by 0xe1 || 0^120).
+__device__ __forceinline__ uint4 mulx(uint4 v) {
+  const uint32_t red = (v.w & 1) ? 0xe1000000u : 0u;
+  return make_uint4((v.x >> 1) ^ red, (v.y >> 1) | (v.x << 31), (v.z >> 1) | (v.y << 31),
+                    (v.w >> 1) | (v.z << 31));
+}
+
+// The reduction of the 4 bits shifted out by Z * x^4, at bits 112..127:
+// clmul(r, 0x1c20) (crypto/fipsmodule/aes/gcm_nohw-style rem_4bit values).
+__device__ __forceinline__ uint32_t red4(uint32_t r) {
+  return ((r & 1) * 0x1c20u) ^ ((r & 2) * 0x1c20u) ^ ((r & 4) * 0x1c20u) ^ ((r & 8) * 0x1c20u);
+}
+
+// X * H^k with M = the 16-entry table of H^k (Shoup 4-bit, nibbles from the
+// highest-degree one down).
+__device__ __forceinline__ uint4 gmul(uint4 X, const uint4 *M) {
+  uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+  const uint32_t w[4] = {X.x, X.y, X.z, X.w};
+#pragma unroll
+  for (int k = 31; k >= 0; k--) {
+    const uint32_t nib = (w[k >> 3] >> (28 - 4 * (k & 7))) & 0xf;
+    const uint32_t r = z3 & 0xf;
+    z3 = __builtin_amdgcn_alignbit(z2, z3, 4);
+    z2 = __builtin_amdgcn_alignbit(z1, z2, 4);
+    z1 = __builtin_amdgcn_alignbit(z0, z1, 4);
+    z0 = (z0 >> 4) ^ (red4(r) << 16);
+    const uint4 m = M[nib];
+    z0 ^= m.x; z1 ^= m.y; z2 ^= m.z; z3 ^= m.w;
+    if ((k & 7) == 0) __builtin_amdgcn_sched_barrier(0);
+  }
+  return make_uint4(z0, z1, z2, z3);
+}
+
+__device__ __forceinline__ uint4 shfl_xor4(uint4 v, int o) {
+  return make_uint4(__shfl_xor(v.x, o, kL), __shfl_xor(v.y, o, kL), __shfl_xor(v.z, o, kL),
+                    __shfl_xor(v.w, o, kL));
+}
+
+// ---- record buffers ----------------------------------------------------------
+
+// Up to 16 bytes at p as little-endian words, zero-padded.
+__device__ __forceinline__ uint4 load_block(const uint8_t *p, uint64_t avail) {
+  if (avail >= 16 && (reinterpret_cast<uintptr_t>(p) & 15) == 0)
+    return *reinterpret_cast<const uint4 *>(p);
+  uint32_t w[4] = {0, 0, 0, 0};
+  const uint32_t n = avail < 16 ? (uint32_t)avail : 16u;
+  for (uint32_t i = 0; i < n; i++) w[i >> 2] |= (uint32_t)p[i] << (8 * (i & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void store_block(uint8_t *p, uint4 v, uint64_t avail) {
+  if (avail >= 16 && (reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+    *reinterpret_cast<uint4 *>(p) = v;
+    return;
+  }
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  const uint32_t n = avail < 16 ? (uint32_t)avail : 16u;
+  for (uint32_t i = 0; i < n; i++) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+}
+
+// Little-endian block words -> GCM-order big-endian words of the byte-reversed
+// block (POLYVAL's ByteReverse, e_aesgcmsiv.cc:624-629).
+__device__ __forceinline__ uint4 rev(uint4 x) { return make_uint4(x.w, x.z, x.y, x.x); }
+
+template <int NR, bool OPEN>
+__global__ __launch_bounds__(kThreads) void gcm_siv_kernel(const GcmKeyDev *__restrict__ keys,
+                                                           BatchDesc b) {
+  __shared__ Lds L;
+  for (int e = threadIdx.x; e < 256; e += kThreads) {
+    const uint32_t v = kSivTables.te0[e];
+    L.t[0][e] = v;
+    L.t[1][e] = rotl(v, 8);
+    L.t[2][e] = rotl(v, 16);
+    L.t[3][e] = rotl(v, 24);
+  }
+  __syncthreads();
+  const int q = threadIdx.x & (kL - 1);
+  const int slot = threadIdx.x / kL;
+  const uint64_t rec = (uint64_t)blockIdx.x * kRecs + slot;
+  const bool active = rec < b.num_records;
+  uint64_t off = 0, len = 0, ad_off = 0, ad_len = 0;
+  uint32_t kidx = 0;
+  if (active) {
+    off = b.offsets ? b.offsets[rec] : rec * b.record_stride;
+    len = b.lengths ? b.lengths[rec] : b.record_len;
+    ad_off = b.ad_offsets ? b.ad_offsets[rec] : rec * b.ad_stride;
+    ad_len = b.ad_lengths ? b.ad_lengths[rec] : b.ad_len;
+    kidx = b.key_index ? b.key_index[rec] : 0u;
+  }
+  // e_aesgcmsiv.cc:794-808, 830-846.
+  const bool live = active && kidx < b.num_keys && b.nonce_len == 12 && b.tag_len == 16 &&
+                    len <= (uint64_t(1) << 36) && ad_len < (uint64_t(1) << 61) &&
+                    (!b.valid || b.valid[rec]);
+  const uint8_t *np = b.nonces + (live ? rec * 12 : 0);
+  const uint4 nw = live ? load_block(np, 12) : make_uint4(0, 0, 0, 0);
+
+  // gcm_siv_keys (e_aesgcmsiv.cc:750-780): AES_K(le32(i) || nonce)[0:8].
+  constexpr int kKeyBlocks = NR == 14 ? 6 : 4;
+  uint4 km = make_uint4(0, 0, 0, 0);
+  if (live && q < kKeyBlocks)
+    km = aes_enc<NR>(make_uint4((uint32_t)q, nw.x, nw.y, nw.z),
+                     reinterpret_cast<const uint4 *>(keys[kidx].rk_plain), L);
+  uint32_t ek[8];
+#pragma unroll
+  for (int i = 0; i < kKeyBlocks - 2; i++) {
+    ek[2 * i] = __shfl(km.x, i + 2, kL);
+    ek[2 * i + 1] = __shfl(km.y, i + 2, kL);
+  }
+  const uint32_t a0 = __shfl(km.x, 0, kL), a1 = __shfl(km.y, 0, kL), a2 = __shfl(km.x, 1, kL),
+                 a3 = __shfl(km.y, 1, kL);
+  // FIPS-197 KeyExpansion of the record key, little-endian words, lane 0.
+  if (q == 0) {
+    constexpr int nk = NR - 6;
+    uint32_t win[nk];
+    uint32_t *out = reinterpret_cast<uint32_t *>(L.rk[slot]);
+#pragma unroll
+    for (int i = 0; i < nk; i++) {
+      win[i] = ek[i];
+      out[i] = ek[i];
+    }
+    uint32_t rcon = 1;
+#pragma unroll
+    for (int i = nk; i < 4 * (NR + 1); i++) {
+      uint32_t t = win[(i - 1) % nk];
+      if (i % nk == 0) {
+        t = (t >> 8) | (t << 24);  // RotWord
+        t = sbox(L, t & 0xff) | (sbox(L, (t >> 8) & 0xff) << 8) |
+            (sbox(L, (t >> 16) & 0xff) << 16) | (sbox(L, t >> 24) << 24);
+        t ^= rcon;
+        rcon = (rcon << 1) ^ ((rcon & 0x80) ? 0x11b : 0);
+      } else if (nk == 8 && i % nk == 4) {
+        t = sbox(L, t & 0xff) | (sbox(L, (t >> 8) & 0xff) << 8) |
+            (sbox(L, (t >> 16) & 0xff) << 16) | (sbox(L, t >> 24) << 24);
+      }
+      win[i % nk] ^= t;
+      out[i] = win[i % nk];
+    }
+  }
+  // Shoup tables of H_g^(2^p), p = 0..4.  H_g = mulX_GHASH(ByteReverse(H))
+  // (e_aesgcmsiv.cc:634-645): the little-endian integer of H shifted right
+  // by one, 0xe1 into its top byte if bit 0 was set, read big-endian.
+  uint4 hp = make_uint4(((a3 >> 1) ^ ((a0 & 1) ? 0xe1000000u : 0u)), (a2 >> 1) | (a3 << 31),
+                        (a1 >> 1) | (a2 << 31), (a0 >> 1) | (a1 << 31));
+#pragma unroll 1
+  for (int p = 0; p < kPows; p++) {
+    const uint4 b8 = hp, b4 = mulx(b8), b2 = mulx(b4), b1 = mulx(b2);
+    uint4 e = make_uint4(0, 0, 0, 0);
+    if (q & 8) e = xor4(e, b8);
+    if (q & 4) e = xor4(e, b4);
+    if (q & 2) e = xor4(e, b2);
+    if (q & 1) e = xor4(e, b1);
+    L.m[slot][p][q] = e;
+    __syncthreads();
+    if (p + 1 < kPows) hp = gmul(hp, L.m[slot][p]);
+  }
+  const uint4 *rk = L.rk[slot];
+
+  // POLYVAL sequence [AD blocks, message blocks, length block]; lane q takes
+  // elements j = q, q + 16, ...
+  const uint64_t nA = live ? (ad_len + 15) / 16 : 0, nP = live ? (len + 15) / 16 : 0;
+  const uint64_t n = live ? nA + nP + 1 : 0;
+  const uint8_t *ad = b.ad + ad_off;
+  const uint8_t *src = b.in + off;
+  uint8_t *dst = b.out + off;
+  uint4 ctr0 = make_uint4(0, 0, 0, 0);
+  if (OPEN && live) {
+    ctr0 = load_block(batch_tag(b, rec), 16);
+    ctr0.w |= 0x80000000u;  // counter[15] |= 0x80 (e_aesgcmsiv.cc:577)
+  }
+  const uint64_t abits = ad_len * 8, mbits = len * 8;
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  uint64_t jlast = 0;
+  bool any = false;
+  for (uint64_t j = q; j < n; j += kL) {
+    uint4 blk;
+    if (j < nA) {
+      blk = load_block(ad + 16 * j, ad_len - 16 * j);
+    } else if (j < nA + nP) {
+      const uint64_t p = j - nA;
+      const uint4 x = load_block(src + 16 * p, len - 16 * p);
+      if (OPEN) {
+        const uint4 ks = aes_enc<NR>(make_uint4(ctr0.x + (uint32_t)p, ctr0.y, ctr0.z, ctr0.w), rk, L);
+        uint4 y = xor4(x, ks);
+        store_block(dst + 16 * p, y, len - 16 * p);
+        const uint64_t rem = len - 16 * p;  // mask the padding of a partial block
+        if (rem < 16) {
+          uint32_t w[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const uint32_t lo = 4 * i;
+            w[i] &= rem >= lo + 4 ? 0xffffffffu : rem <= lo ? 0u : ((1u << (8 * (rem - lo))) - 1u);
+          }
+          y = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        blk = y;
+      } else {
+        blk = x;
+      }
+    } else {
+      blk = make_uint4((uint32_t)abits, (uint32_t)(abits >> 32), (uint32_t)mbits,
+                       (uint32_t)(mbits >> 32));
+    }
+    acc = any ? xor4(gmul(acc, L.m[slot][kPows - 1]), rev(blk)) : rev(blk);
+    any = true;
+    jlast = j;
+  }
+  // acc * H^(n - jlast), then the sum over the record's lanes.
+  if (any) {
+    const uint32_t e = (uint32_t)(n - jlast);  // 1..16
+    if (e == 16) {
+      acc = gmul(acc, L.m[slot][4]);
+    } else {
+#pragma unroll 1
+      for (int t = 0; t < 4; t++)
+        if (e & (1u << t)) acc = gmul(acc, L.m[slot][t]);
+    }
+  }
+#pragma unroll
+  for (int o = kL / 2; o >= 1; o >>= 1) acc = xor4(acc, shfl_xor4(acc, o));
+  // POLYVAL result (byte-reversed back), ^ nonce, bit 127 cleared, AES_K'.
+  uint4 s = rev(acc);
+  s.x ^= nw.x;
+  s.y ^= nw.y;
+  s.z ^= nw.z;
+  s.w &= 0x7fffffffu;
+  const uint4 tag = aes_enc<NR>(s, rk, L);
+
+  int ok = live;
+  if (OPEN && live) {
+    const uint4 t = load_block(batch_tag(b, rec), 16);  // CRYPTO_memcmp, :861-864
+    ok = ((t.x ^ tag.x) | (t.y ^ tag.y) | (t.z ^ tag.z) | (t.w ^ tag.w)) == 0;
+  }
+  if (!OPEN && live) {
+    // gcm_siv_crypt from the tag (e_aesgcmsiv.cc:817).
+    ctr0 = tag;
+    ctr0.w |= 0x80000000u;
+    for (uint64_t p = q; p < nP; p += kL) {
+      const uint4 x = load_block(src + 16 * p, len - 16 * p);
+      const uint4 ks = aes_enc<NR>(make_uint4(ctr0.x + (uint32_t)p, ctr0.y, ctr0.z, ctr0.w), rk, L);
+      store_block(dst + 16 * p, xor4(x, ks), len - 16 * p);
+    }
+  }
+  if (active && q == 0) {
+    if (!OPEN) store_block(batch_tag(b, rec), ok ? tag : make_uint4(0, 0, 0, 0), 16);
+    if (b.status) b.status[rec] = ok ? 1 : 0;
+  }
+  // Zero the output of a failed record (aead.cc.inc:132-139, 539-547).
+  if (active && !ok)
+    for (uint64_t p = q; 16 * p < len; p += kL)
+      store_block(dst + 16 * p, make_uint4(0, 0, 0, 0), len - 16 * p);
+}
+
+}  // namespace
+
+int launch_gcm_siv(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, void *stream,
+                   const KernelEvents *ev) {
+  if (b.num_records == 0) return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint64_t blocks = (b.num_records + kRecs - 1) / kRecs;
+  if (blocks > 0x7fffffffu) return 1;
+  if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
+  if (nr == 14) {
+    if (open)
+      hipLaunchKernelGGL((gcm_siv_kernel<14, true>), dim3((unsigned)blocks), dim3(kThreads), 0,
+                         s, keys, b);
+    else
+      hipLaunchKernelGGL((gcm_siv_kernel<14, false>), dim3((unsigned)blocks), dim3(kThreads), 0,
+                         s, keys, b);
+  } else {
+    if (open)
+      hipLaunchKernelGGL((gcm_siv_kernel<10, true>), dim3((unsigned)blocks), dim3(kThreads), 0,
+                         s, keys, b);
+    else
+      hipLaunchKernelGGL((gcm_siv_kernel<10, false>), dim3((unsigned)blocks), dim3(kThreads), 0,
+                         s, keys, b);
+  }
+  const int rc = (int)hipGetLastError();
+  if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
+  return rc;
+}
+
+}  // namespace bssl_amd

@@ -43,7 +43,12 @@ struct alignas(16) ChaChaKeyDev {
   uint32_t k[8];
 };
 
-enum AeadKind : int { kAeadAesGcm = 0, kAeadChaChaPoly = 1, kAeadXChaChaPoly = 2 };
+enum AeadKind : int {
+  kAeadAesGcm = 0,
+  kAeadChaChaPoly = 1,
+  kAeadXChaChaPoly = 2,
+  kAeadAesGcmSiv = 3
+};
 
 // Record-batch descriptor (device pointers), see BSSL_AMD_BATCH.
 struct BatchDesc {
@@ -117,6 +122,9 @@ int build_length_order(const uint64_t *lengths, uint64_t n, uint32_t *order, uin
 inline bool wants_length_order(const BatchDesc &b) {
   return b.lengths && b.num_records >= 4096 && b.num_records < (uint64_t(1) << 32);
 }
+// AES-GCM-SIV (gcm_siv.hip); uses GcmKeyDev::rk_plain of the master key.
+int launch_gcm_siv(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, void *stream,
+                   const KernelEvents *ev);
 // xchacha: XChaCha20-Poly1305 (24-byte nonces, per-record HChaCha20 subkey).
 int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, bool xchacha,
                   void *stream, const KernelEvents *ev);

@@ -75,6 +75,8 @@ BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_aes_192_gcm(void);        /* aead.h:113
 BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_aes_256_gcm(void);        /* aead.h:122 */
 BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_chacha20_poly1305(void);  /* aead.h:126 */
 BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_xchacha20_poly1305(void); /* aead.h:130 */
+BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_aes_128_gcm_siv(void);    /* aead.h:142 */
+BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_aes_256_gcm_siv(void);    /* aead.h:145 */
 BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_aes_128_gcm_tls12(void);  /* aead.h:583 */
 BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_aes_256_gcm_tls12(void);  /* aead.h:584 */
 BSSL_AMD_EXPORT const EVP_AEAD *EVP_aead_aes_128_gcm_tls13(void);  /* aead.h:585 */

@@ -24,7 +24,8 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
 ORACLE_ID = {"aes-128-gcm": o.AES_GCM, "aes-192-gcm": o.AES_GCM, "aes-256-gcm": o.AES_GCM,
-             "chacha20-poly1305": o.CHACHA20_POLY1305, "xchacha20-poly1305": o.XCHACHA20_POLY1305}
+             "chacha20-poly1305": o.CHACHA20_POLY1305, "xchacha20-poly1305": o.XCHACHA20_POLY1305,
+             "aes-128-gcm-siv": o.AES_GCM_SIV, "aes-256-gcm-siv": o.AES_GCM_SIV}
 
 
 def _nl(aead):
@@ -114,7 +115,7 @@ def run_batch(aead, keys, key_index, ins, nonces, ads, tag_len, open_=False, tag
 # reference known-answer files through the single-record host API
 
 @pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-192-gcm", "aes-256-gcm", "chacha20-poly1305",
-                                  "xchacha20-poly1305"])
+                                  "xchacha20-poly1305", "aes-128-gcm-siv", "aes-256-gcm-siv"])
 def test_kat_single_record(aead):
     cases = [c for c in load("kat_aead.json") if c["aead"] == aead]
     ctxs = {}
@@ -163,7 +164,7 @@ def test_batch_multikey_vectors(source):
     """Every record with its own key (keyset + key_index), seal then open."""
     cases = [c for c in load(source) if c.get("valid", True)]
     for (aead, nl, tag_len), grp in _groups(cases).items():
-        if "chacha" in aead and nl != _nl(aead):
+        if ("chacha" in aead or "siv" in aead) and nl != _nl(aead):
             continue
         if nl == 0:
             continue
@@ -182,7 +183,7 @@ def test_batch_multikey_vectors(source):
 
 
 @pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm", "chacha20-poly1305",
-                                  "xchacha20-poly1305"])
+                                  "xchacha20-poly1305", "aes-128-gcm-siv", "aes-256-gcm-siv"])
 @pytest.mark.parametrize("layout", ["aligned", "unaligned", "inplace"])
 def test_batch_ragged_vs_oracle(aead, layout):
     rng = random.Random(hash((aead, layout)) & 0xffff)
@@ -204,7 +205,7 @@ def test_batch_ragged_vs_oracle(aead, layout):
 
 
 @pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm", "chacha20-poly1305",
-                                  "xchacha20-poly1305"])
+                                  "xchacha20-poly1305", "aes-128-gcm-siv", "aes-256-gcm-siv"])
 @pytest.mark.parametrize("multikey", [False, True])
 def test_batch_large_ragged_reordered(aead, multikey):
     """>= 4096 ragged records: the launcher processes them in length-class
@@ -280,7 +281,7 @@ def test_batch_gcm_nonce_lengths_and_truncated_tags():
 
 
 @pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm", "chacha20-poly1305",
-                                  "xchacha20-poly1305"])
+                                  "xchacha20-poly1305", "aes-128-gcm-siv", "aes-256-gcm-siv"])
 def test_open_rejects_tampering_and_zeroes_output(aead):
     rng = random.Random(11)
     key = bytes(rng.getrandbits(8) for _ in range(AEAD_KEYLEN[aead]))
@@ -408,13 +409,15 @@ def _run_synth_digest(name):
 
 
 @pytest.mark.parametrize("name", ["parity_aes128_16k", "parity_aes256_mixed", "parity_chacha_1350",
-                                  "parity_multikey_aes128", "parity_xchacha_1350"])
+                                  "parity_multikey_aes128", "parity_xchacha_1350",
+                                  "parity_siv128_1350", "parity_siv256_mixed",
+                                  "parity_siv128_multikey"])
 def test_synth_parity_digest(name):
     _run_synth_digest(name)
 
 
 @pytest.mark.parametrize("name", ["config2_aes128_16k", "config3_chacha_1350",
-                                  "config3x_xchacha_1350"])
+                                  "config3x_xchacha_1350", "configs_siv128_16k"])
 def test_baseline_config_digest(name):
     """BASELINE.json configs 2 and 3 at full size (16 GiB / 1.3 GiB)."""
     _run_synth_digest(name)
@@ -722,7 +725,7 @@ def _split(rng, data, max_parts):
 
 
 @pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm", "chacha20-poly1305",
-                                  "xchacha20-poly1305"])
+                                  "xchacha20-poly1305", "aes-128-gcm-siv", "aes-256-gcm-siv"])
 def test_iovec_batch_vs_oracle(aead):
     rng = random.Random(hash(aead) & 0xffff)
     key = bytes(rng.getrandbits(8) for _ in range(AEAD_KEYLEN[aead]))
