@@ -45,6 +45,9 @@ CONFIGS = {
     # nonces (oracle/ref/ref_tool.cc make_nonce).
     "config3x": ("xchacha20-poly1305", 32, 1 << 20, 1350,
                  "config3x: XChaCha20-Poly1305 seal, 1M x 1350 B records per GPU"),
+    # AES-GCM-SIV: config 2's records.
+    "configS": ("aes-128-gcm-siv", 16, 1 << 20, 16384,
+                "configS: AES-128-GCM-SIV seal, 1M x 16 KiB records per GPU, single key"),
     "config4": ("aes-256-gcm", 32, 1 << 22, "mixed",
                 "config4: AES-256-GCM seal, 4M records of 64 B-16 KiB (mixed) per GPU"),
     # 64K keys x 64 records over 8 GPUs: per GPU 8192 keys x 64 records of
@@ -82,6 +85,7 @@ METRICS = {
     "config2": METRIC,
     "config3": "GiB/s device-resident AEAD seal (ChaCha20-Poly1305, 1350 B records)",
     "config3x": "GiB/s device-resident AEAD seal (XChaCha20-Poly1305, 1350 B records)",
+    "configS": "GiB/s device-resident AEAD seal (AES-128-GCM-SIV, 16 KiB records)",
     "config4": "GiB/s device-resident AEAD seal (AES-256-GCM, mixed 64 B-16 KiB records)",
     "config5": "GiB/s device-resident AEAD seal (AES-128-GCM, 16 KiB records, 64 records per key)",
 }
