@@ -14,10 +14,11 @@
 // bulk kernel, so the scatter zeroes its chunks (clear_iovec,
 // aead.cc.inc:310-314, 325-333).
 //
-// Copies: one workgroup per record walks its chunks in order; each chunk is
-// copied in 16-byte destination words assembled from byte-aligned source
-// reads (chunks have arbitrary lengths, so a record's later chunks start at
-// arbitrary alignments), with a byte loop for the head and tail.
+// Copies: one wave per record walks its chunks in order; each chunk is copied
+// in 16-byte destination words, assembled with v_alignbyte from aligned dword
+// loads when the source is not 4-byte aligned (chunks have arbitrary lengths,
+// so a record's later chunks start at arbitrary alignments), with a byte loop
+// for the head and tail.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -28,34 +29,34 @@ namespace {
 
 constexpr int kCopyThreads = 256;
 
-// dst[0, n) = src[0, n) for one chunk, all threads of the workgroup.
+// dst[0, n) = src[0, n) for one chunk, by the 64 lanes of one wave.
 __device__ __forceinline__ void copy_bytes(uint8_t *dst, const uint8_t *src, uint64_t n) {
+  const uint32_t lane = threadIdx.x & 63;
   // Head: bytes until dst is 16-byte aligned.
   const uint64_t head = min<uint64_t>(n, (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15);
-  for (uint64_t i = threadIdx.x; i < head; i += blockDim.x) dst[i] = src[i];
+  if (lane < head) dst[lane] = src[lane];
   const uint64_t words = (n - head) / 16;
-  uint8_t *d = dst + head;
+  uint4 *d = reinterpret_cast<uint4 *>(dst + head);
   const uint8_t *s = src + head;
+  const uint32_t m = reinterpret_cast<uintptr_t>(s) & 3;
   if ((reinterpret_cast<uintptr_t>(s) & 15) == 0) {
-    for (uint64_t w = threadIdx.x; w < words; w += blockDim.x)
-      reinterpret_cast<uint4 *>(d)[w] = reinterpret_cast<const uint4 *>(s)[w];
-  } else if ((reinterpret_cast<uintptr_t>(s) & 3) == 0) {
-    for (uint64_t w = threadIdx.x; w < words; w += blockDim.x) {
+    for (uint64_t w = lane; w < words; w += 64) d[w] = reinterpret_cast<const uint4 *>(s)[w];
+  } else if (m == 0) {
+    for (uint64_t w = lane; w < words; w += 64) {
       const uint32_t *sp = reinterpret_cast<const uint32_t *>(s + 16 * w);
-      reinterpret_cast<uint4 *>(d)[w] = make_uint4(sp[0], sp[1], sp[2], sp[3]);
+      d[w] = make_uint4(sp[0], sp[1], sp[2], sp[3]);
     }
   } else {
-    for (uint64_t w = threadIdx.x; w < words; w += blockDim.x) {
-      const uint8_t *sp = s + 16 * w;
-      uint32_t v[4];
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-        v[k] = (uint32_t)sp[4 * k] | ((uint32_t)sp[4 * k + 1] << 8) |
-               ((uint32_t)sp[4 * k + 2] << 16) | ((uint32_t)sp[4 * k + 3] << 24);
-      reinterpret_cast<uint4 *>(d)[w] = make_uint4(v[0], v[1], v[2], v[3]);
+    // Five aligned dwords cover the 16 source bytes (each holds at least one
+    // of them, so no load leaves the chunk's pages); v_alignbyte shifts.
+    for (uint64_t w = lane; w < words; w += 64) {
+      const uint32_t *sp = reinterpret_cast<const uint32_t *>(s + 16 * w - m);
+      const uint32_t d0 = sp[0], d1 = sp[1], d2 = sp[2], d3 = sp[3], d4 = sp[4];
+      d[w] = make_uint4(__builtin_amdgcn_alignbyte(d1, d0, m), __builtin_amdgcn_alignbyte(d2, d1, m),
+                        __builtin_amdgcn_alignbyte(d3, d2, m), __builtin_amdgcn_alignbyte(d4, d3, m));
     }
   }
-  for (uint64_t i = head + 16 * words + threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+  for (uint64_t i = head + 16 * words + lane; i < n; i += 64) dst[i] = src[i];
 }
 
 // Per record: message and AD lengths, and their 16-byte padded sizes for the
@@ -75,15 +76,17 @@ __global__ void iov_lengths(const IovBatchDesc b, uint64_t *__restrict__ len,
   ad_padded[i] = (a + 15) & ~uint64_t(15);
 }
 
-// Gather (TO_STAGE) or scatter (!TO_STAGE) the chunks of records
-// blockIdx.x, blockIdx.x + gridDim.x, ...
+// Gather (TO_STAGE) or scatter (!TO_STAGE) the chunks of records: one wave
+// per record, grid-stride over the batch.
 template <bool TO_STAGE>
 __global__ __launch_bounds__(kCopyThreads) void iov_copy(const IovBatchDesc b,
                                                          uint8_t *__restrict__ stage,
                                                          const uint64_t *__restrict__ off,
                                                          uint8_t *__restrict__ ad_stage,
                                                          const uint64_t *__restrict__ ad_off) {
-  for (uint64_t i = blockIdx.x; i < b.num_records; i += gridDim.x) {
+  constexpr uint32_t kWaves = kCopyThreads / 64;
+  for (uint64_t i = (uint64_t)blockIdx.x * kWaves + threadIdx.x / 64; i < b.num_records;
+       i += (uint64_t)gridDim.x * kWaves) {
     uint64_t pos = off[i];
     for (uint64_t c = b.iovec_start[i]; c < b.iovec_start[i + 1]; c++) {
       const IovecDev v = b.iovecs[c];
@@ -150,7 +153,8 @@ int iov_batch_run(const IovBatchDesc &b, const IovRunner &run, void *stream) {
     rc = 2;
   if (!rc) {
     uint8_t *ad_stage = stage + totals[0];
-    const unsigned grid = (unsigned)(n < 65536 ? n : 65536);
+    const uint64_t wgs = (n + 3) / 4;  // 4 records (waves) per workgroup
+    const unsigned grid = (unsigned)(wgs < 65536 ? wgs : 65536);
     hipLaunchKernelGGL(iov_copy<true>, dim3(grid), dim3(kCopyThreads), 0, s, b, stage, off,
                        ad_stage, ad_off);
     BatchDesc d = {};

@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Throughput of EVP_AEAD_CTX_sealv_batch_device (device iovec records,
+iovec.hip) next to the contiguous batch on the same records.
+
+Each record is split into three chunks as a socket layer would hand it over
+(a 5-byte piece, the middle, the rest), the chunks packed back to back at odd
+offsets in one arena (so most chunks are unaligned), outputs to a second
+arena; AD is one 13-byte chunk per record.  Prints one JSON line.
+
+  python tools/iov_bench.py [--aead aes-128-gcm] [--records N] [--len L] [--steps K]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import boringssl_amd as ba  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--aead", default="aes-128-gcm")
+    ap.add_argument("--records", type=int, default=1 << 18)
+    ap.add_argument("--len", type=int, default=16384)
+    ap.add_argument("--steps", type=int, default=10)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(0)
+    n, L = a.records, a.len
+    key_len = 16 if "128" in a.aead else 32
+    nl = 24 if a.aead.startswith("xchacha") else 12
+    g = torch.Generator(device=dev).manual_seed(1)
+    # chunk layout: record i occupies [base_i, base_i + L + 1) with a 1-byte
+    # gap, so record starts (and most chunk starts) are unaligned
+    stride = L + 1
+    src = torch.randint(0, 256, (n * stride + 64,), dtype=torch.uint8, device=dev, generator=g)
+    dst = torch.zeros_like(src)
+    base = torch.arange(n, dtype=torch.int64, device=dev) * stride
+    cut1 = torch.full((n,), min(5, L), dtype=torch.int64, device=dev)
+    cut2 = torch.full((n,), max(min(5, L), L // 2), dtype=torch.int64, device=dev)
+    offs = torch.stack([torch.zeros_like(cut1), cut1, cut2], 1)       # chunk start in record
+    lens = torch.stack([cut1, cut2 - cut1, L - cut2], 1)              # chunk length
+    iov = torch.stack([dst.data_ptr() + base[:, None] + offs,
+                       src.data_ptr() + base[:, None] + offs, lens], 2).reshape(-1, 3).contiguous()
+    starts = torch.arange(0, 3 * n + 1, 3, dtype=torch.int64, device=dev)
+    ad = torch.randint(0, 256, (13 * n,), dtype=torch.uint8, device=dev, generator=g)
+    aiv = torch.stack([ad.data_ptr() + 13 * torch.arange(n, dtype=torch.int64, device=dev),
+                       torch.full((n,), 13, dtype=torch.int64, device=dev)], 1).contiguous()
+    astarts = torch.arange(0, n + 1, dtype=torch.int64, device=dev)
+    nonces = torch.randint(0, 256, (nl * n,), dtype=torch.uint8, device=dev, generator=g)
+    tags = torch.zeros(16 * n, dtype=torch.uint8, device=dev)
+    status = torch.zeros(n, dtype=torch.uint8, device=dev)
+    ctx = ba.AEADCtx(a.aead, bytes(range(key_len)), 16)
+    b = ba.make_iov_batch(n, iov, starts, tags, nonces, nl, aadvecs=aiv, aadvec_start=astarts,
+                          status=status)
+    # The same records, contiguous and 16-byte aligned, for comparison.
+    cpt = torch.randint(0, 256, (n * ((L + 15) // 16 * 16) + 16,), dtype=torch.uint8, device=dev,
+                        generator=g)
+    cct = torch.zeros_like(cpt)
+    cb = ba.make_batch(n, cpt, cct, tags, nonces, nl, ad, record_stride=(L + 15) // 16 * 16,
+                       record_len=L, ad_stride=13, ad_len=13, status=status)
+    res = {}
+    for name, op, batch in (("iovec", ctx.sealv_batch_device, b),
+                            ("contiguous", ctx.seal_batch_device, cb)):
+        op(batch)
+        torch.cuda.synchronize()
+        assert bool(status.all()), name
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            op(batch)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / a.steps
+        res[name] = {"ms_per_batch": round(dt * 1e3, 3), "gib_per_s": round(n * L / dt / 2**30, 2)}
+    print(json.dumps({"aead": a.aead, "records": n, "record_bytes": L,
+                      "chunks_per_record": 3, **res}))
+
+
+if __name__ == "__main__":
+    main()
