@@ -17,7 +17,7 @@ step() {
   [ $rc -eq 0 ] || exit $rc
 }
 for cfg in ${CONFIGS:-config2 config3}; do
-  case $cfg in config3) K=chacha_poly_kernel ;; *) K=gcm_kernel ;; esac
+  case $cfg in config3|config3x) K=chacha_poly_kernel ;; configS) K=gcm_siv_kernel ;; *) K=gcm_kernel ;; esac
   step "stats_$cfg" 600 rocprofv3 --kernel-trace --stats -d "gpurun_out/prof_$cfg" -o run \
     --output-format csv -- python3 bench.py --config "$cfg" --steps 10 --warmup 2 --no-cpu-baseline
   B="python3 bench.py --config $cfg --steps 2 --warmup 1 --no-cpu-baseline"
