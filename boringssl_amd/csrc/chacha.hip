@@ -32,7 +32,18 @@
 namespace bssl_amd {
 namespace {
 
-constexpr int kThreads = 256;
+#ifndef BSSL_AMD_CHACHA_THREADS
+#define BSSL_AMD_CHACHA_THREADS 256
+#endif
+constexpr int kThreads = BSSL_AMD_CHACHA_THREADS;
+// Wave priority during a record group's start-up (loads, first ChaCha
+// block): waves that start mid-kernel otherwise lose every issue arbitration
+// to older waves and sit 60-100 K cycles before their first block (stamps,
+// DESIGN.md 4.3).  Priority 2 for that phase: +2-5 % on config 3 (40-step
+// runs, 1,061/1,072 -> 1,122/1,092 GiB/s); 0 = off.
+#ifndef BSSL_AMD_CHACHA_PRIO
+#define BSSL_AMD_CHACHA_PRIO 2
+#endif
 #ifndef BSSL_AMD_CHACHA_L
 #define BSSL_AMD_CHACHA_L 4
 #endif
@@ -351,6 +362,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   uint64_t ts[5] = {0, 0, 0, 0, 0};
 #endif
   CSTAMP(0);
+  if (BSSL_AMD_CHACHA_PRIO) __builtin_amdgcn_s_setprio(BSSL_AMD_CHACHA_PRIO);
   static_assert(L == 2 || L == 4 || L == 8 || L == 16, "lanes per record");
   constexpr int kLog = L == 2 ? 1 : L == 4 ? 2 : L == 8 ? 3 : 4;
   const int lane = threadIdx.x & 63;
@@ -497,6 +509,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   const bool have0 = q >= 1 && (uint64_t)q <= nblk;
   if (have0) crypt_block((uint64_t)q, ks, pre, c0);
   CSTAMP(1);
+  if (BSSL_AMD_CHACHA_PRIO) __builtin_amdgcn_s_setprio(0);
   uint32_t kw[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) kw[i] = __shfl(ks[i], 0, L);
