@@ -45,11 +45,14 @@ def test_library_exports_every_declared_symbol():
 def test_aead_parameters():
     import boringssl_amd as ba
     L = ba.lib
-    for name, key_len in [("aes-128-gcm", 16), ("aes-192-gcm", 24), ("aes-256-gcm", 32),
-                          ("chacha20-poly1305", 32), ("aes-128-gcm-tls13", 16)]:
+    for name, key_len, nonce_len in [
+            ("aes-128-gcm", 16, 12), ("aes-192-gcm", 24, 12), ("aes-256-gcm", 32, 12),
+            ("chacha20-poly1305", 32, 12), ("aes-128-gcm-tls13", 16, 12),
+            ("xchacha20-poly1305", 32, 24),  # e_chacha20poly1305.cc:385-399
+            ("aes-128-gcm-siv", 16, 12), ("aes-256-gcm-siv", 32, 12)]:  # e_aesgcmsiv.cc:869-899
         a = ba.EVP_aead(name)
         assert L.EVP_AEAD_key_length(a) == key_len
-        assert L.EVP_AEAD_nonce_length(a) == 12
+        assert L.EVP_AEAD_nonce_length(a) == nonce_len
         assert L.EVP_AEAD_max_overhead(a) == 16
         assert L.EVP_AEAD_max_tag_len(a) == 16
 
@@ -65,7 +68,52 @@ def test_init_rejects_bad_key_and_tag_length_without_gpu():
     with pytest.raises(ba.AEADError) as e:
         ba.AEADCtx("chacha20-poly1305", bytes(32), tag_len=17)
     assert e.value.reason == ba.CIPHER_R_TOO_LARGE
+    # GCM-SIV takes 16-byte tags only (e_aesgcmsiv.cc:542-548)
+    with pytest.raises(ba.AEADError) as e:
+        ba.AEADCtx("aes-128-gcm-siv", bytes(16), tag_len=12)
+    assert e.value.reason == ba.CIPHER_R_TAG_TOO_LARGE
+    with pytest.raises(ba.AEADError) as e:
+        ba.AEADCtx("xchacha20-poly1305", bytes(16))
+    assert e.value.reason == ba.CIPHER_R_UNSUPPORTED_KEY_SIZE
     assert ba.lib.ERR_get_error() == 0
+
+
+def test_struct_layouts_match_the_header(tmp_path):
+    """The ctypes mirror's structures have the C header's sizes and field
+    offsets (a C probe compiled against include/bssl_amd/*.h)."""
+    import boringssl_amd as ba
+    structs = {
+        "EVP_AEAD_CTX": (ba.EVP_AEAD_CTX, {"aead": "aead", "state": "state", "tag_len": "tag_len"}),
+        "CRYPTO_IOVEC": (ba.CRYPTO_IOVEC, {"out": "out", "in": "in_", "len": "len"}),
+        "CRYPTO_IVEC": (ba.CRYPTO_IVEC, {"in": "in_", "len": "len"}),
+        "BSSL_AMD_BATCH": (ba.BSSL_AMD_BATCH, {f: f for f in (
+            "num_records", "out", "offsets", "lengths", "record_stride", "record_len", "nonces",
+            "nonce_len", "ad", "ad_offsets", "ad_lengths", "ad_stride", "ad_len", "tags",
+            "status", "key_index")} | {"in": "in_"}),
+        "BSSL_AMD_IOV_BATCH": (ba.BSSL_AMD_IOV_BATCH, {f: f for f in (
+            "num_records", "iovecs", "iovec_start", "aadvecs", "aadvec_start", "nonces",
+            "nonce_len", "tags", "status")}),
+    }
+    lines = ["#include <stdio.h>", "#include <stddef.h>", "#include <bssl_amd/aead.h>",
+             "int main(void) {"]
+    for cname, (_, fields) in structs.items():
+        lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
+        for cf in fields:
+            lines.append(f'  printf("{cname} {cf} %zu\\n", offsetof({cname}, {cf}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src),
+                           "-o", str(exe)])
+    got = {}
+    for line in subprocess.check_output([str(exe)], text=True).splitlines():
+        name, key, val = line.split()
+        got[(name, key)] = int(val)
+    for cname, (cls, fields) in structs.items():
+        assert ctypes.sizeof(cls) == got[(cname, "size")], cname
+        for cf, pf in fields.items():
+            assert getattr(cls, pf).offset == got[(cname, cf)], (cname, cf)
 
 
 def test_error_queue_is_bounded_fifo():
