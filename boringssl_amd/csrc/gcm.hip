@@ -1002,6 +1002,26 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, gtab, mf0);
 }
 
+// Byte table of H^16 from the key's nibble tables (power 4): entry (e, p) =
+// T[2p][e >> 4] ^ T[2p+1][e & 15] (key_setup.cc layout), at kLdsG8 + e*256 +
+// p*16.  Thread tid writes entries tid + i*kThreads; since kThreads is a
+// multiple of 256 its p and (e & 15) are fixed and e >> 4 steps by
+// kThreads/256, so all of its global loads are issued before the first LDS
+// write (one memory latency per key change instead of one per entry).
+__device__ __forceinline__ void build_g8(uint8_t *smem, const uint4 *__restrict__ t16, int tid) {
+  static_assert(kThreads % 256 == 0 && 4096 % kThreads == 0, "table build split");
+  constexpr int kPer = 4096 / kThreads;
+  const uint32_t p = (uint32_t)tid & 15u, lo = ((uint32_t)tid >> 4) & 15u;
+  const uint32_t hi = (uint32_t)tid >> 8;
+  const uint4 b = t16[(2 * p + 1) * 16 + lo];
+  uint4 a[kPer];
+#pragma unroll
+  for (int i = 0; i < kPer; i++) a[i] = t16[(2 * p) * 16 + hi + (uint32_t)i * (kThreads / 256)];
+#pragma unroll
+  for (int i = 0; i < kPer; i++)
+    reinterpret_cast<uint4 *>(smem + kLdsG8)[tid + i * kThreads] = xor4(a[i], b);
+}
+
 template <int NR, bool OPEN, bool XT>
 __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restrict__ keys,
                                                       BatchDesc b,
@@ -1038,12 +1058,7 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
     // grid-wide counter, so waves that the SIMD arbiter favours (older
     // waves issue first) simply process more units instead of waiting at a
     // per-tile barrier for the slowest wave.
-    const uint4 *t16 = reinterpret_cast<const uint4 *>(keys[0].htab[4]);
-    for (uint32_t e = tid; e < 4096; e += kThreads) {
-      const uint32_t ev = e >> 4, p = e & 15;
-      reinterpret_cast<uint4 *>(smem + kLdsG8)[e] =
-          xor4(t16[(2 * p) * 16 + (ev >> 4)], t16[(2 * p + 1) * 16 + (ev & 15)]);
-    }
+    build_g8(smem, reinterpret_cast<const uint4 *>(keys[0].htab[4]), tid);
     __syncthreads();
     RoundKeys rk;
 #pragma unroll
@@ -1103,12 +1118,7 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
         __syncthreads();
         // Byte table of H^16 from the key's nibble tables (power 4): entry
         // (e, p) = T[2p][e >> 4] ^ T[2p+1][e & 15] (key_setup.cc layout).
-        const uint4 *t16 = reinterpret_cast<const uint4 *>(keys[k].htab[4]);
-        for (uint32_t e = tid; e < 4096; e += kThreads) {
-          const uint32_t ev = e >> 4, p = e & 15;
-          reinterpret_cast<uint4 *>(smem + kLdsG8)[e] =
-              xor4(t16[(2 * p) * 16 + (ev >> 4)], t16[(2 * p + 1) * 16 + (ev & 15)]);
-        }
+        build_g8(smem, reinterpret_cast<const uint4 *>(keys[k].htab[4]), tid);
         __syncthreads();
         loaded = k;
       }
