@@ -33,8 +33,27 @@
 namespace bssl_amd {
 namespace {
 
+// BSSL_AMD_SIV_REP = 1: T0/T1 replicated 32x in LDS (lane l reads bank l, as
+// gcm.hip) with T2/T3 = rot16(T0/T1); the 64 KiB table then takes one
+// 768-thread workgroup (48 records) per CU.  0 = four plain 1 KiB tables.
+// BSSL_AMD_SIV_SPLIT = 1: the per-block multiply by H^16 as four independent
+// Shoup chains (gmul4) instead of one 32-step chain.
+#ifndef BSSL_AMD_SIV_SPLIT
+#define BSSL_AMD_SIV_SPLIT 1
+#endif
+// BSSL_AMD_SIV_GROUP = 1: a record's 16 lanes are the 16 lanes of one
+// ds_read_b128 lane group ({0-3,12-15,20-27} / {4-11,16-19,28-31}, +32), so
+// the Shoup-table reads of a group all hit one record's 256-byte table:
+// distinct nibbles are distinct banks, equal ones the same address.  With
+// contiguous lanes a group mixes two records' tables and their reads collide.
+#ifndef BSSL_AMD_SIV_GROUP
+#define BSSL_AMD_SIV_GROUP 1
+#endif
+#ifndef BSSL_AMD_SIV_REP
+#define BSSL_AMD_SIV_REP 0
+#endif
 constexpr int kL = 16;                // lanes per record
-constexpr int kThreads = 256;
+constexpr int kThreads = BSSL_AMD_SIV_REP ? 768 : 256;
 constexpr int kRecs = kThreads / kL;  // records per workgroup
 constexpr int kPows = 5;              // H, H^2, H^4, H^8, H^16
 
@@ -77,18 +96,32 @@ constexpr Tables make_tables() {
 __constant__ Tables kSivTables = make_tables();
 
 struct Lds {
+#if BSSL_AMD_SIV_REP
+  uint32_t t[256][2][32];      // entry, T0 / T1 = rotl(T0, 8), replica (lane & 31)
+#else
   uint32_t t[4][256];          // T0..T3 (T_r = rotl(T0, 8r))
+#endif
   uint4 rk[kRecs][15];         // each record's encryption round keys
   uint4 m[kRecs][kPows][16];   // each record's Shoup tables
 };
+static_assert(sizeof(Lds) <= 160 * 1024, "LDS per workgroup");
 
 __device__ __forceinline__ uint32_t rotl(uint32_t v, int n) {
   return __builtin_amdgcn_alignbit(v, v, 32 - n);
 }
 
+#if BSSL_AMD_SIV_REP
+__device__ __forceinline__ uint32_t tlook(const Lds &L, int t, uint32_t x) {
+  return L.t[x][t][threadIdx.x & 31];
+}
+__device__ __forceinline__ uint32_t sbox(const Lds &L, uint32_t x) {
+  return (tlook(L, 0, x) >> 8) & 0xff;
+}
+#else
 __device__ __forceinline__ uint32_t sbox(const Lds &L, uint32_t x) {
   return (L.t[0][x] >> 8) & 0xff;
 }
+#endif
 
 // FIPS-197 cipher on little-endian column words; `rk` in LDS or global memory.
 template <int NR>
@@ -97,6 +130,15 @@ __device__ __forceinline__ uint4 aes_enc(uint4 in, const uint4 *rk, const Lds &L
 #pragma unroll
   for (int r = 1; r < NR; r++) {
     const uint4 k = rk[r];
+#if BSSL_AMD_SIV_REP
+    // T2[c] ^ T3[d] = rot16(T0[c] ^ T1[d])
+    auto col = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t kk) {
+      return tlook(L, 0, a & 0xff) ^ tlook(L, 1, (b >> 8) & 0xff) ^
+             rotl(tlook(L, 0, (c >> 16) & 0xff) ^ tlook(L, 1, d >> 24), 16) ^ kk;
+    };
+    const uint32_t t0 = col(s0, s1, s2, s3, k.x), t1 = col(s1, s2, s3, s0, k.y),
+                   t2 = col(s2, s3, s0, s1, k.z), t3 = col(s3, s0, s1, s2, k.w);
+#else
     const uint32_t t0 = L.t[0][s0 & 0xff] ^ L.t[1][(s1 >> 8) & 0xff] ^
                         L.t[2][(s2 >> 16) & 0xff] ^ L.t[3][s3 >> 24] ^ k.x;
     const uint32_t t1 = L.t[0][s1 & 0xff] ^ L.t[1][(s2 >> 8) & 0xff] ^
@@ -105,6 +147,7 @@ __device__ __forceinline__ uint4 aes_enc(uint4 in, const uint4 *rk, const Lds &L
                         L.t[2][(s0 >> 16) & 0xff] ^ L.t[3][s1 >> 24] ^ k.z;
     const uint32_t t3 = L.t[0][s3 & 0xff] ^ L.t[1][(s0 >> 8) & 0xff] ^
                         L.t[2][(s1 >> 16) & 0xff] ^ L.t[3][s2 >> 24] ^ k.w;
+#endif
     s0 = t0; s1 = t1; s2 = t2; s3 = t3;
   }
   const uint4 k = rk[NR];
@@ -155,9 +198,79 @@ __device__ __forceinline__ uint4 gmul(uint4 X, const uint4 *M) {
   return make_uint4(z0, z1, z2, z3);
 }
 
-__device__ __forceinline__ uint4 shfl_xor4(uint4 v, int o) {
-  return make_uint4(__shfl_xor(v.x, o, kL), __shfl_xor(v.y, o, kL), __shfl_xor(v.z, o, kL),
-                    __shfl_xor(v.w, o, kL));
+// X * x^32: one word down, the 32 bits shifted out of the top reduced by
+// x^128 = 1 + x + x^2 + x^7 (as mulx, 32 bits at once).
+__device__ __forceinline__ uint4 mulx32(uint4 z) {
+  const uint32_t s = z.w;
+  return make_uint4(s ^ (s >> 1) ^ (s >> 2) ^ (s >> 7), z.x ^ (s << 31) ^ (s << 30) ^ (s << 25),
+                    z.y, z.z);
+}
+
+// gmul as four independent 8-nibble Shoup chains, one per word of X
+// (X * H = sum_g x^(32 g) * (word g of X) * H), joined by Horner in x^32: the
+// same 32 table reads, a quarter of the dependent-latency chain.
+__device__ __forceinline__ uint4 gmul4(uint4 X, const uint4 *M) {
+  uint32_t z[4][4];
+  const uint32_t w[4] = {X.x, X.y, X.z, X.w};
+#pragma unroll
+  for (int g = 0; g < 4; g++) z[g][0] = z[g][1] = z[g][2] = z[g][3] = 0;
+#pragma unroll
+  for (int k = 7; k >= 0; k--) {
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+      const uint32_t nib = (w[g] >> (28 - 4 * k)) & 0xf;
+      const uint32_t r = z[g][3] & 0xf;
+      z[g][3] = __builtin_amdgcn_alignbit(z[g][2], z[g][3], 4);
+      z[g][2] = __builtin_amdgcn_alignbit(z[g][1], z[g][2], 4);
+      z[g][1] = __builtin_amdgcn_alignbit(z[g][0], z[g][1], 4);
+      z[g][0] = (z[g][0] >> 4) ^ (red4(r) << 16);
+      const uint4 m = M[nib];
+      z[g][0] ^= m.x; z[g][1] ^= m.y; z[g][2] ^= m.z; z[g][3] ^= m.w;
+    }
+  }
+  uint4 acc = make_uint4(z[3][0], z[3][1], z[3][2], z[3][3]);
+#pragma unroll
+  for (int g = 2; g >= 0; g--)
+    acc = xor4(mulx32(acc), make_uint4(z[g][0], z[g][1], z[g][2], z[g][3]));
+  return acc;
+}
+
+// Record lanes: lane q of the record in slot `slot` (BSSL_AMD_SIV_GROUP).
+// Lane within the 32-lane half of the record's q-th lane (set B = the
+// {4-11,16-19,28-31} group).
+__device__ __forceinline__ int group_lane(int setb, int q) {
+  return setb ? (q < 8 ? q + 4 : q < 12 ? q + 8 : q + 16) : (q < 4 ? q : q < 8 ? q + 8 : q + 12);
+}
+struct RecLanes {
+  int q, slot, setb, half;  // half = lane & 32
+  __device__ int src(int i) const {  // wave lane of the record's lane i
+    return BSSL_AMD_SIV_GROUP ? half + group_lane(setb, i) : (threadIdx.x & 63 & ~(kL - 1)) + i;
+  }
+};
+__device__ __forceinline__ RecLanes rec_lanes() {
+  RecLanes r;
+  const int t = threadIdx.x;
+  if (BSSL_AMD_SIV_GROUP) {
+    const int l = t & 31;
+    r.setb = (l >= 4 && l < 12) || (l >= 16 && l < 20) || l >= 28;
+    r.q = r.setb ? (l < 12 ? l - 4 : l < 20 ? l - 8 : l - 16)
+                 : (l < 4 ? l : l < 16 ? l - 8 : l - 12);
+    r.slot = 2 * (t >> 5) + r.setb;
+  } else {
+    r.setb = 0;
+    r.q = t & (kL - 1);
+    r.slot = t / kL;
+  }
+  r.half = t & 32;
+  return r;
+}
+__device__ __forceinline__ uint32_t rshfl(uint32_t v, const RecLanes &R, int i) {
+  return __shfl(v, R.src(i), 64);
+}
+__device__ __forceinline__ uint4 shfl_xor4(uint4 v, const RecLanes &R, int o) {
+  const int s = R.src(R.q ^ o);
+  return make_uint4(__shfl(v.x, s, 64), __shfl(v.y, s, 64), __shfl(v.z, s, 64),
+                    __shfl(v.w, s, 64));
 }
 
 // ---- record buffers ----------------------------------------------------------
@@ -198,6 +311,12 @@ template <int NR, bool OPEN>
 __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyDev *__restrict__ keys,
                                                            BatchDesc b) {
   __shared__ Lds L;
+#if BSSL_AMD_SIV_REP
+  for (int e = threadIdx.x; e < 256 * 64; e += kThreads) {
+    const uint32_t v = kSivTables.te0[e >> 6];
+    (&L.t[0][0][0])[e] = ((e >> 5) & 1) ? rotl(v, 8) : v;
+  }
+#else
   for (int e = threadIdx.x; e < 256; e += kThreads) {
     const uint32_t v = kSivTables.te0[e];
     L.t[0][e] = v;
@@ -205,9 +324,11 @@ __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyD
     L.t[2][e] = rotl(v, 16);
     L.t[3][e] = rotl(v, 24);
   }
+#endif
   __syncthreads();
-  const int q = threadIdx.x & (kL - 1);
-  const int slot = threadIdx.x / kL;
+  const RecLanes R = rec_lanes();
+  const int q = R.q;
+  const int slot = R.slot;
   const uint64_t rec = (uint64_t)blockIdx.x * kRecs + slot;
   const bool active = rec < b.num_records;
   uint64_t off = 0, len = 0, ad_off = 0, ad_len = 0;
@@ -235,11 +356,11 @@ __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyD
   uint32_t ek[8];
 #pragma unroll
   for (int i = 0; i < kKeyBlocks - 2; i++) {
-    ek[2 * i] = __shfl(km.x, i + 2, kL);
-    ek[2 * i + 1] = __shfl(km.y, i + 2, kL);
+    ek[2 * i] = rshfl(km.x, R, i + 2);
+    ek[2 * i + 1] = rshfl(km.y, R, i + 2);
   }
-  const uint32_t a0 = __shfl(km.x, 0, kL), a1 = __shfl(km.y, 0, kL), a2 = __shfl(km.x, 1, kL),
-                 a3 = __shfl(km.y, 1, kL);
+  const uint32_t a0 = rshfl(km.x, R, 0), a1 = rshfl(km.y, R, 0), a2 = rshfl(km.x, R, 1),
+                 a3 = rshfl(km.y, R, 1);
   // FIPS-197 KeyExpansion of the record key, little-endian words, lane 0.
   if (q == 0) {
     constexpr int nk = NR - 6;
@@ -332,7 +453,11 @@ __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyD
       blk = make_uint4((uint32_t)abits, (uint32_t)(abits >> 32), (uint32_t)mbits,
                        (uint32_t)(mbits >> 32));
     }
+#if BSSL_AMD_SIV_SPLIT
+    acc = any ? xor4(gmul4(acc, L.m[slot][kPows - 1]), rev(blk)) : rev(blk);
+#else
     acc = any ? xor4(gmul(acc, L.m[slot][kPows - 1]), rev(blk)) : rev(blk);
+#endif
     any = true;
     jlast = j;
   }
@@ -348,7 +473,7 @@ __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyD
     }
   }
 #pragma unroll
-  for (int o = kL / 2; o >= 1; o >>= 1) acc = xor4(acc, shfl_xor4(acc, o));
+  for (int o = kL / 2; o >= 1; o >>= 1) acc = xor4(acc, shfl_xor4(acc, R, o));
   // POLYVAL result (byte-reversed back), ^ nonce, bit 127 cleared, AES_K'.
   uint4 s = rev(acc);
   s.x ^= nw.x;
