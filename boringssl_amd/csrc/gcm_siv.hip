@@ -49,6 +49,13 @@ namespace {
 #ifndef BSSL_AMD_SIV_GROUP
 #define BSSL_AMD_SIV_GROUP 1
 #endif
+// BSSL_AMD_SIV_CTRCACHE = 1: counter-window caching of rounds 1-2 in the
+// seal keystream pass (CtrWindow).  Parity-tested; off because it measured
+// no faster (502-503 vs 505 GiB/s, configS): the keystream pass's lookups are
+// not what binds this kernel.
+#ifndef BSSL_AMD_SIV_CTRCACHE
+#define BSSL_AMD_SIV_CTRCACHE 0
+#endif
 #ifndef BSSL_AMD_SIV_REP
 #define BSSL_AMD_SIV_REP 0
 #endif
@@ -123,12 +130,22 @@ __device__ __forceinline__ uint32_t sbox(const Lds &L, uint32_t x) {
 }
 #endif
 
-// FIPS-197 cipher on little-endian column words; `rk` in LDS or global memory.
-template <int NR>
-__device__ __forceinline__ uint4 aes_enc(uint4 in, const uint4 *rk, const Lds &L) {
-  uint32_t s0 = in.x ^ rk[0].x, s1 = in.y ^ rk[0].y, s2 = in.z ^ rk[0].z, s3 = in.w ^ rk[0].w;
+// Table T_t[x] (T_t = rotl(T0, 8t)).
+__device__ __forceinline__ uint32_t tt(const Lds &L, int t, uint32_t x) {
+#if BSSL_AMD_SIV_REP
+  return t < 2 ? tlook(L, t, x) : rotl(tlook(L, t - 2, x), 16);
+#else
+  return L.t[t][x];
+#endif
+}
+
+// FIPS-197 cipher on little-endian column words, from round R0 on (s = the
+// state entering round R0); `rk` in LDS or global memory.
+template <int NR, int R0>
+__device__ __forceinline__ uint4 aes_enc_from(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+                                              const uint4 *rk, const Lds &L) {
 #pragma unroll
-  for (int r = 1; r < NR; r++) {
+  for (int r = R0; r < NR; r++) {
     const uint4 k = rk[r];
 #if BSSL_AMD_SIV_REP
     // T2[c] ^ T3[d] = rot16(T0[c] ^ T1[d])
@@ -158,6 +175,48 @@ __device__ __forceinline__ uint4 aes_enc(uint4 in, const uint4 *rk, const Lds &L
   return make_uint4(last(s0, s1, s2, s3) ^ k.x, last(s1, s2, s3, s0) ^ k.y,
                     last(s2, s3, s0, s1) ^ k.z, last(s3, s0, s1, s2) ^ k.w);
 }
+
+template <int NR>
+__device__ __forceinline__ uint4 aes_enc(uint4 in, const uint4 *rk, const Lds &L) {
+  return aes_enc_from<NR, 1>(in.x ^ rk[0].x, in.y ^ rk[0].y, in.z ^ rk[0].z, in.w ^ rk[0].w, rk,
+                             L);
+}
+
+// Counter-mode caching for the SIV keystream (Bernstein-Schwabe, as gcm.hip):
+// the counter is word 0 + p (little-endian, e_aesgcmsiv.cc:555-580), so within
+// a window of 256 counters only state byte 0 changes.  Round 1 then costs one
+// lookup (column 0's T0) and round 2 four (one per column, from round-1
+// column 0): 5 lookups instead of 32.  The window constants (27 lookups) are
+// rebuilt when the high 24 bits of state word 0 change.
+struct CtrWindow {
+  uint32_t hi = 0xffffffffu;  // (no 24-bit value equals it)
+  uint32_t k0, l0, l1, l2, l3;
+  __device__ __forceinline__ void update(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+                                         const uint4 *rk, const Lds &L) {
+    if ((s0 >> 8) == hi) return;
+    hi = s0 >> 8;
+    const uint4 a = rk[1], c = rk[2];
+    k0 = tt(L, 1, (s1 >> 8) & 0xff) ^ tt(L, 2, (s2 >> 16) & 0xff) ^ tt(L, 3, s3 >> 24) ^ a.x;
+    const uint32_t t1 = tt(L, 0, s1 & 0xff) ^ tt(L, 1, (s2 >> 8) & 0xff) ^
+                        tt(L, 2, (s3 >> 16) & 0xff) ^ tt(L, 3, s0 >> 24) ^ a.y;
+    const uint32_t t2 = tt(L, 0, s2 & 0xff) ^ tt(L, 1, (s3 >> 8) & 0xff) ^
+                        tt(L, 2, (s0 >> 16) & 0xff) ^ tt(L, 3, s1 >> 24) ^ a.z;
+    const uint32_t t3 = tt(L, 0, s3 & 0xff) ^ tt(L, 1, (s0 >> 8) & 0xff) ^
+                        tt(L, 2, (s1 >> 16) & 0xff) ^ tt(L, 3, s2 >> 24) ^ a.w;
+    l0 = tt(L, 1, (t1 >> 8) & 0xff) ^ tt(L, 2, (t2 >> 16) & 0xff) ^ tt(L, 3, t3 >> 24) ^ c.x;
+    l1 = tt(L, 0, t1 & 0xff) ^ tt(L, 1, (t2 >> 8) & 0xff) ^ tt(L, 2, (t3 >> 16) & 0xff) ^ c.y;
+    l2 = tt(L, 0, t2 & 0xff) ^ tt(L, 1, (t3 >> 8) & 0xff) ^ tt(L, 3, t1 >> 24) ^ c.z;
+    l3 = tt(L, 0, t3 & 0xff) ^ tt(L, 2, (t1 >> 16) & 0xff) ^ tt(L, 3, t2 >> 24) ^ c.w;
+  }
+  // Keystream block for state word 0 = s0 (in this window).
+  template <int NR>
+  __device__ __forceinline__ uint4 block(uint32_t s0, const uint4 *rk, const Lds &L) const {
+    const uint32_t t0 = k0 ^ tt(L, 0, s0 & 0xff);
+    return aes_enc_from<NR, 3>(l0 ^ tt(L, 0, t0 & 0xff), l1 ^ tt(L, 3, t0 >> 24),
+                               l2 ^ tt(L, 2, (t0 >> 16) & 0xff), l3 ^ tt(L, 1, (t0 >> 8) & 0xff),
+                               rk, L);
+  }
+};
 
 // ---- GF(2^128) in GCM order, as big-endian words (w0 = bytes 0..3) --------
 
@@ -491,9 +550,20 @@ __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyD
     // gcm_siv_crypt from the tag (e_aesgcmsiv.cc:817).
     ctr0 = tag;
     ctr0.w |= 0x80000000u;
+#if BSSL_AMD_SIV_CTRCACHE
+    const uint4 r0 = rk[0];
+    const uint32_t s1 = ctr0.y ^ r0.y, s2 = ctr0.z ^ r0.z, s3 = ctr0.w ^ r0.w;
+    CtrWindow wc;
+#endif
     for (uint64_t p = q; p < nP; p += kL) {
       const uint4 x = load_block(src + 16 * p, len - 16 * p);
+#if BSSL_AMD_SIV_CTRCACHE
+      const uint32_t s0 = (ctr0.x + (uint32_t)p) ^ r0.x;
+      wc.update(s0, s1, s2, s3, rk, L);
+      const uint4 ks = wc.block<NR>(s0, rk, L);
+#else
       const uint4 ks = aes_enc<NR>(make_uint4(ctr0.x + (uint32_t)p, ctr0.y, ctr0.z, ctr0.w), rk, L);
+#endif
       store_block(dst + 16 * p, xor4(x, ks), len - 16 * p);
     }
   }
