@@ -49,6 +49,11 @@ namespace {
 #ifndef BSSL_AMD_SIV_GROUP
 #define BSSL_AMD_SIV_GROUP 1
 #endif
+// BSSL_AMD_SIV_FASTRED = 1: the Shoup step's 4-bit reduction as shifts of
+// the top nibble (red4_hi) instead of four multiplies.
+#ifndef BSSL_AMD_SIV_FASTRED
+#define BSSL_AMD_SIV_FASTRED 1
+#endif
 // BSSL_AMD_SIV_CTRCACHE = 1: counter-window caching of rounds 1-2 in the
 // seal keystream pass (CtrWindow).  Parity-tested; off because it measured
 // no faster (502-503 vs 505 GiB/s, configS): the keystream pass's lookups are
@@ -236,6 +241,17 @@ __device__ __forceinline__ uint4 mulx(uint4 v) {
 __device__ __forceinline__ uint32_t red4(uint32_t r) {
   return ((r & 1) * 0x1c20u) ^ ((r & 2) * 0x1c20u) ^ ((r & 4) * 0x1c20u) ^ ((r & 8) * 0x1c20u);
 }
+// red4(z3 & 0xf) << 16 without the multiplies: with u = z3 << 28 (the four
+// bits at the top), clmul(r, 0x1c20) << 16 = r<<28 ^ r<<27 ^ r<<26 ^ r<<21
+// = u ^ u>>1 ^ u>>2 ^ u>>7 (0x1c20 = bits 5, 10, 11, 12).
+__device__ __forceinline__ uint32_t red4_hi(uint32_t z3) {
+#if BSSL_AMD_SIV_FASTRED
+  const uint32_t u = z3 << 28;
+  return u ^ (u >> 1) ^ (u >> 2) ^ (u >> 7);
+#else
+  return red4(z3 & 0xf) << 16;
+#endif
+}
 
 // X * H^k with M = the 16-entry table of H^k (Shoup 4-bit, nibbles from the
 // highest-degree one down).
@@ -245,11 +261,11 @@ __device__ __forceinline__ uint4 gmul(uint4 X, const uint4 *M) {
 #pragma unroll
   for (int k = 31; k >= 0; k--) {
     const uint32_t nib = (w[k >> 3] >> (28 - 4 * (k & 7))) & 0xf;
-    const uint32_t r = z3 & 0xf;
+    const uint32_t r = red4_hi(z3);
     z3 = __builtin_amdgcn_alignbit(z2, z3, 4);
     z2 = __builtin_amdgcn_alignbit(z1, z2, 4);
     z1 = __builtin_amdgcn_alignbit(z0, z1, 4);
-    z0 = (z0 >> 4) ^ (red4(r) << 16);
+    z0 = (z0 >> 4) ^ r;
     const uint4 m = M[nib];
     z0 ^= m.x; z1 ^= m.y; z2 ^= m.z; z3 ^= m.w;
     if ((k & 7) == 0) __builtin_amdgcn_sched_barrier(0);
@@ -278,11 +294,11 @@ __device__ __forceinline__ uint4 gmul4(uint4 X, const uint4 *M) {
 #pragma unroll
     for (int g = 0; g < 4; g++) {
       const uint32_t nib = (w[g] >> (28 - 4 * k)) & 0xf;
-      const uint32_t r = z[g][3] & 0xf;
+      const uint32_t r = red4_hi(z[g][3]);
       z[g][3] = __builtin_amdgcn_alignbit(z[g][2], z[g][3], 4);
       z[g][2] = __builtin_amdgcn_alignbit(z[g][1], z[g][2], 4);
       z[g][1] = __builtin_amdgcn_alignbit(z[g][0], z[g][1], 4);
-      z[g][0] = (z[g][0] >> 4) ^ (red4(r) << 16);
+      z[g][0] = (z[g][0] >> 4) ^ r;
       const uint4 m = M[nib];
       z[g][0] ^= m.x; z[g][1] ^= m.y; z[g][2] ^= m.z; z[g][3] ^= m.w;
     }
