@@ -49,6 +49,10 @@ namespace {
 #ifndef BSSL_AMD_SIV_GROUP
 #define BSSL_AMD_SIV_GROUP 1
 #endif
+// BSSL_AMD_SIV_DEFER = 1 (with SPLIT): gmul4d, one reduction per chain.
+#ifndef BSSL_AMD_SIV_DEFER
+#define BSSL_AMD_SIV_DEFER 1
+#endif
 // BSSL_AMD_SIV_FASTRED = 1: the Shoup step's 4-bit reduction as shifts of
 // the top nibble (red4_hi) instead of four multiplies.
 #ifndef BSSL_AMD_SIV_FASTRED
@@ -310,6 +314,43 @@ __device__ __forceinline__ uint4 gmul4(uint4 X, const uint4 *M) {
   return acc;
 }
 
+// gmul4 with the reduction deferred: each 8-step chain shifts its 32
+// spilled bits into a fifth word instead of reducing 4 bits per step, and
+// reduces them once at the end (x^128 = 1 + x + x^2 + x^7, as mulx32; the
+// reduced terms stay below degree 39 + 28, so no second reduction).  Per
+// step: 4 funnel shifts, 1 shift and 4 XORs.
+__device__ __forceinline__ uint4 gmul4d(uint4 X, const uint4 *M) {
+  uint32_t z[4][5];
+  const uint32_t w[4] = {X.x, X.y, X.z, X.w};
+#pragma unroll
+  for (int g = 0; g < 4; g++) z[g][0] = z[g][1] = z[g][2] = z[g][3] = z[g][4] = 0;
+#pragma unroll
+  for (int k = 7; k >= 0; k--) {
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+      const uint32_t nib = (w[g] >> (28 - 4 * k)) & 0xf;
+      z[g][4] = __builtin_amdgcn_alignbit(z[g][3], z[g][4], 4);
+      z[g][3] = __builtin_amdgcn_alignbit(z[g][2], z[g][3], 4);
+      z[g][2] = __builtin_amdgcn_alignbit(z[g][1], z[g][2], 4);
+      z[g][1] = __builtin_amdgcn_alignbit(z[g][0], z[g][1], 4);
+      z[g][0] = z[g][0] >> 4;
+      const uint4 m = M[nib];
+      z[g][0] ^= m.x; z[g][1] ^= m.y; z[g][2] ^= m.z; z[g][3] ^= m.w;
+    }
+  }
+  uint4 r[4];
+#pragma unroll
+  for (int g = 0; g < 4; g++) {
+    const uint32_t sp = z[g][4];
+    r[g] = make_uint4(z[g][0] ^ sp ^ (sp >> 1) ^ (sp >> 2) ^ (sp >> 7),
+                      z[g][1] ^ (sp << 31) ^ (sp << 30) ^ (sp << 25), z[g][2], z[g][3]);
+  }
+  uint4 acc = r[3];
+#pragma unroll
+  for (int g = 2; g >= 0; g--) acc = xor4(mulx32(acc), r[g]);
+  return acc;
+}
+
 // Record lanes: lane q of the record in slot `slot` (BSSL_AMD_SIV_GROUP).
 // Lane within the 32-lane half of the record's q-th lane (set B = the
 // {4-11,16-19,28-31} group).
@@ -528,7 +569,9 @@ __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyD
       blk = make_uint4((uint32_t)abits, (uint32_t)(abits >> 32), (uint32_t)mbits,
                        (uint32_t)(mbits >> 32));
     }
-#if BSSL_AMD_SIV_SPLIT
+#if BSSL_AMD_SIV_SPLIT && BSSL_AMD_SIV_DEFER
+    acc = any ? xor4(gmul4d(acc, L.m[slot][kPows - 1]), rev(blk)) : rev(blk);
+#elif BSSL_AMD_SIV_SPLIT
     acc = any ? xor4(gmul4(acc, L.m[slot][kPows - 1]), rev(blk)) : rev(blk);
 #else
     acc = any ? xor4(gmul(acc, L.m[slot][kPows - 1]), rev(blk)) : rev(blk);
