@@ -20,7 +20,7 @@ run() {
 for s in $STEPS; do
   case $s in
     smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    pytest) run pytest 1500 python -m pytest tests/test_gpu_parity.py -q -m gpu -rf ${PYTEST_ARGS:-} ;;
+    pytest) run pytest 1500 python -u -m pytest tests/ -v -m gpu -rf --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} ;;
     pmc)
