@@ -5,58 +5,79 @@ Metric (BASELINE.json): "GiB/s device-resident AEAD seal (AES-128-GCM, 16 KiB
 records) at 1/2/4/8 GPUs".  Default workload = BASELINE config 2: AES-128-GCM
 seal of 1,048,576 x 16 KiB synthetic records (16 GiB in, 16 GiB out, one key)
 per GPU.  One step = one seal pass over the whole per-GPU batch, inputs
-already resident in HBM.  Multi-GPU: one process per GPU; every rank seals
-its own 1M-record shard (weak scaling, no collective on the data path); the
-only collectives are the timing barrier and the max-over-ranks reduction.
+already resident in HBM.
+
+Multi-GPU: one process per GPU, records sharded with no
+collective on the data path; the only collectives are the timing barrier, the
+max of the step time and the sum of the bytes.
+  * `python bench.py --gpus N` (WORLD_SIZE unset) starts N rank processes
+    itself, before anything touches a GPU, and prints rank 0's line;
+    under `torch.distributed.run` each rank reads RANK/LOCAL_RANK/WORLD_SIZE.
+  * configs 2, 3, 3x, S are per-GPU workloads (weak scaling: 1M records per
+    GPU); config 4 is ONE fixed batch of 4M mixed-length records split into
+    contiguous ranges balanced by bytes (prefix sum of the record lengths), and
+    config 5 is ONE fixed set of 64K keys x 64 records split by key ranges
+    (strong scaling: the total work is fixed as N grows).
+  * `--plan-only` runs the launcher, the rendezvous, the shard plan and the
+    reductions on CPU (gloo) without a GPU (tests/test_multirank.py).
 
 Prints ONE JSON line on rank 0 (contract in the task description), including
 `roofline` (algorithmic HBM bytes per launch / HIP-event kernel time vs the
 8 TB/s HBM peak) and `cpu_baseline` (the reference library's CPU path,
-oracle/_ref/ref_tool, on this host's cores, rank 0 at N=1 only).
+oracle/_ref/ref_tool bench1 = bench/aead.cc's BM_SpeedAEAD, one pinned
+process per physical host core, rank 0 at N=1 only).
 """
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-import boringssl_amd as ba  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 METRIC = "GiB/s device-resident AEAD seal (AES-128-GCM, 16 KiB records) at 1/2/4/8 GPUs"
 
 CONFIGS = {
-    # name: (aead, key_len, records per GPU, record length or "mixed", description)
-    # Only config2 is the BASELINE metric; the others are reported under their
-    # own metric names.
-    "config2": ("aes-128-gcm", 16, 1 << 20, 16384,
+    # name: (aead, key_len, records, record length or "mixed", scaling, description)
+    # Weak configs: `records` per GPU.  Strong configs: `records` in total,
+    # split across the GPUs.  Only config2 is the BASELINE metric; the others
+    # are reported under their own metric names.
+    "config2": ("aes-128-gcm", 16, 1 << 20, 16384, "weak",
                 "config2: AES-128-GCM seal, 1M x 16 KiB records per GPU, single key"),
-    "config3": ("chacha20-poly1305", 32, 1 << 20, 1350,
+    "config3": ("chacha20-poly1305", 32, 1 << 20, 1350, "weak",
                 "config3: ChaCha20-Poly1305 seal, 1M x 1350 B records per GPU"),
     # XChaCha20-Poly1305 (SURVEY.md 8(f) f3): config 3's records with 24-byte
     # nonces (oracle/ref/ref_tool.cc make_nonce).
-    "config3x": ("xchacha20-poly1305", 32, 1 << 20, 1350,
+    "config3x": ("xchacha20-poly1305", 32, 1 << 20, 1350, "weak",
                  "config3x: XChaCha20-Poly1305 seal, 1M x 1350 B records per GPU"),
     # AES-GCM-SIV (SURVEY.md 8(f) f3): config 2's records.
-    "configS": ("aes-128-gcm-siv", 16, 1 << 20, 16384,
+    "configS": ("aes-128-gcm-siv", 16, 1 << 20, 16384, "weak",
                 "configS: AES-128-GCM-SIV seal, 1M x 16 KiB records per GPU, single key"),
-    "config4": ("aes-256-gcm", 32, 1 << 22, "mixed",
-                "config4: AES-256-GCM seal, 4M records of 64 B-16 KiB (mixed) per GPU"),
-    # 64K keys x 64 records over 8 GPUs: per GPU 8192 keys x 64 records of
-    # 16 KiB (BSSL_AMD_KEYSET, key_index per record, records grouped by key).
-    "config5": ("aes-128-gcm", 16, 8192 * 64, 16384,
-                "config5: AES-128-GCM seal, 8192 keys x 64 records x 16 KiB per GPU "
-                "(64K keys over 8 GPUs), keyset"),
+    "config4": ("aes-256-gcm", 32, 1 << 22, "mixed", "strong",
+                "config4: AES-256-GCM seal, one batch of 4M records of 64 B-16 KiB (mixed), "
+                "split across the GPUs by bytes"),
+    # 64K keys x 64 records of 16 KiB (BSSL_AMD_KEYSET, key_index per record,
+    # records grouped by key), split across the GPUs by key ranges.
+    "config5": ("aes-128-gcm", 16, 65536 * 64, 16384, "strong",
+                "config5: AES-128-GCM seal, 64K keys x 64 records x 16 KiB (keyset), "
+                "split across the GPUs by key ranges"),
 }
 RECORDS_PER_KEY = {"config5": 64}
+
+METRICS = {
+    "config2": METRIC,
+    "config3": "GiB/s device-resident AEAD seal (ChaCha20-Poly1305, 1350 B records)",
+    "config3x": "GiB/s device-resident AEAD seal (XChaCha20-Poly1305, 1350 B records)",
+    "configS": "GiB/s device-resident AEAD seal (AES-128-GCM-SIV, 16 KiB records)",
+    "config4": "GiB/s device-resident AEAD seal (AES-256-GCM, mixed 64 B-16 KiB records)",
+    "config5": "GiB/s device-resident AEAD seal (AES-128-GCM, 16 KiB records, 64 records per key)",
+}
 
 
 def synth_key(k, key_len):
@@ -73,6 +94,7 @@ def synth_key(k, key_len):
 
 
 def mixed_lengths(first, n):
+    """oracle/synth.h synth_mixed_len for records first .. first+n-1."""
     i = np.arange(first, first + n, dtype=np.uint64)
     z = i + np.uint64(42) + np.uint64(0x9E3779B97F4A7C15)
     z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
@@ -81,109 +103,276 @@ def mixed_lengths(first, n):
     return np.uint64(64) + z % np.uint64(16321)
 
 
-METRICS = {
-    "config2": METRIC,
-    "config3": "GiB/s device-resident AEAD seal (ChaCha20-Poly1305, 1350 B records)",
-    "config3x": "GiB/s device-resident AEAD seal (XChaCha20-Poly1305, 1350 B records)",
-    "configS": "GiB/s device-resident AEAD seal (AES-128-GCM-SIV, 16 KiB records)",
-    "config4": "GiB/s device-resident AEAD seal (AES-256-GCM, mixed 64 B-16 KiB records)",
-    "config5": "GiB/s device-resident AEAD seal (AES-128-GCM, 16 KiB records, 64 records per key)",
-}
+def _pad16(lens):
+    return (lens + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+
+
+class Shard:
+    """Records [first, first + n) of the global record sequence on one rank.
+    `lens`/`offs` describe the rank's packed batch (16-byte-aligned records)."""
+
+    def __init__(self, first, lens, key_first=0, nkeys=0):
+        self.first = int(first)
+        self.lens = lens
+        padded = _pad16(lens)
+        self.offs = np.zeros(len(lens), dtype=np.uint64)
+        if len(lens):
+            self.offs[1:] = np.cumsum(padded[:-1])
+        self.total_pad = int(padded.sum())
+        self.key_first, self.nkeys = key_first, nkeys
+
+    @property
+    def n(self):
+        return len(self.lens)
+
+
+def byte_balanced_split(lens, world):
+    """Split points s_0 = 0 <= s_1 <= ... <= s_world = n of a record sequence
+    into contiguous ranges of nearly equal bytes: s_r is the first record whose
+    exclusive prefix sum of (padded) lengths reaches r/world of the total."""
+    prefix = np.zeros(len(lens) + 1, dtype=np.float64)
+    prefix[1:] = np.cumsum(_pad16(lens).astype(np.float64))
+    targets = prefix[-1] * np.arange(world + 1) / world
+    s = np.searchsorted(prefix, targets, side="left")
+    s[0], s[-1] = 0, len(lens)
+    return [int(x) for x in s]
 
 
 def shard_plan(config, rank, world, records=0):
-    """Records of rank `rank`: a disjoint shard [first, first + n) of the
-    global record sequence (weak scaling: n records per GPU).  Returns
-    (first, lengths[n], offsets[n], padded_total_bytes)."""
-    aead, key_len, nrec, length, _ = CONFIGS[config]
+    """The records of rank `rank` of `world`.
+
+    Weak configs: rank r seals records [r*n, (r+1)*n) of the synthetic
+    sequence (n = `records` or the config's per-GPU count).  config4: the fixed
+    batch of `records` (default 4M) mixed-length records, split by bytes.
+    config5: the fixed 64K keys (or records/64) split by key ranges."""
+    aead, key_len, nrec, length, scaling, _ = CONFIGS[config]
     if records:
         nrec = records
-    first = rank * nrec
-    lens = mixed_lengths(first, nrec) if length == "mixed" else np.full(nrec, length, np.uint64)
-    padded = (lens + np.uint64(15)) // np.uint64(16) * np.uint64(16)
-    offs = np.zeros(nrec, dtype=np.uint64)
-    offs[1:] = np.cumsum(padded[:-1])
-    return first, lens, offs, int(padded.sum())
+    if scaling == "weak":
+        first = rank * nrec
+        lens = mixed_lengths(first, nrec) if length == "mixed" else np.full(nrec, length,
+                                                                            np.uint64)
+        return Shard(first, lens)
+    if config in RECORDS_PER_KEY:
+        rpk = RECORDS_PER_KEY[config]
+        nkeys_total = nrec // rpk
+        k0, k1 = nkeys_total * rank // world, nkeys_total * (rank + 1) // world
+        return Shard(k0 * rpk, np.full((k1 - k0) * rpk, length, np.uint64), k0, k1 - k0)
+    all_lens = mixed_lengths(0, nrec) if length == "mixed" else np.full(nrec, length, np.uint64)
+    s = byte_balanced_split(all_lens, world)
+    return Shard(s[rank], all_lens[s[rank]:s[rank + 1]].copy())
+
+
+# ---------------------------------------------------------------------------
+# rank-process launcher (python bench.py --gpus N without torch.distributed.run)
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """Start n rank processes of this script (one per GPU) and wait for them.
+    Runs before anything in this process touches a GPU; the children are
+    fresh processes (never exec).  Rank 0's stdout is passed through; if a
+    rank fails, the others are stopped.  Returns the exit code."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+# ---------------------------------------------------------------------------
+# reductions over ranks (timing only; no data-path collective)
+
+def _dist():
+    import torch.distributed as dist
+    return dist
+
+
+def _reduce(value, world, op):
+    if world == 1:
+        return value
+    import torch
+    dist = _dist()
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" \
+        else torch.device("cpu")
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=op)
+    return float(t.item())
 
 
 def reduce_max(value, world):
     """Max over ranks of a host float (the step time), via the process group."""
-    if world == 1:
-        return value
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" \
-        else torch.device("cpu")
-    t = torch.tensor([value], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return _reduce(value, world, _dist().ReduceOp.MAX if world > 1 else None)
 
 
 def reduce_sum(value, world):
-    if world == 1:
-        return value
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" \
-        else torch.device("cpu")
-    t = torch.tensor([value], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    return _reduce(value, world, _dist().ReduceOp.SUM if world > 1 else None)
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline (BASELINE.md section 3)
+
+def physical_cores(limit=16):
+    """One logical CPU per physical core of this process's affinity set,
+    at most `limit` (the box's CPU share for one GPU)."""
+    seen, cores = set(), []
+    for c in sorted(os.sched_getaffinity(0)):
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                sib = f.read().strip()
+        except OSError:
+            sib = str(c)
+        if sib not in seen:
+            seen.add(sib)
+            cores.append(c)
+    return cores[:limit]
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _pinned_runs(cmd, cores, timeout):
+    procs = [subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True,
+                              preexec_fn=(lambda c=c: os.sched_setaffinity(0, {c})))
+             for c in cores]
+    out = []
+    for p in procs:
+        o, _ = p.communicate(timeout=timeout)
+        if p.returncode != 0:
+            raise RuntimeError(f"{cmd} exited {p.returncode}")
+        out.append(json.loads(o))
+    return out
 
 
 def cpu_baseline(aead, length, seconds):
-    """Reference CPU path (oracle/_ref/ref_tool: the reference library built
-    from /root/reference sources) on a bounded resident sample."""
+    """The reference CPU path timed on this host: oracle/_ref/ref_tool bench1
+    (the reference library built from /root/reference sources, driven exactly
+    as bench/aead.cc:41-133 BM_SpeedAEAD drives it: one EVP_AEAD_CTX, zero
+    key/nonce/13-byte AD/input, the same 16-byte-aligned buffer resealed, so
+    the data is cache-resident) as one single-threaded process pinned to each
+    physical core, seal and open.  value = the sum over cores (whole host)."""
     tool = os.path.join(ROOT, "oracle", "_ref", "ref_tool")
-    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
-    if isinstance(length, str):
+    if isinstance(length, str):  # mixed 64 B-16 KiB: bench/aead.cc's 8192-byte size
         length = 8192
-    nrec = max(1024, (1 << 30) // length)  # ~1 GiB resident sample
+    cores = physical_cores()
     if os.path.exists(tool):
         try:
-            out = subprocess.check_output(
-                [tool, "bench", aead, str(length), str(nrec), str(threads), str(seconds)],
-                text=True, timeout=seconds * 4 + 120)
-            r = json.loads(out)
-            return {"value": round(r["gib_per_s"], 3), "unit": "GiB/s", "cores": threads,
+            res = {}
+            for op in ("seal", "open"):
+                runs = _pinned_runs([tool, "bench1", aead, op, str(length), str(seconds)], cores,
+                                    seconds * 4 + 60)
+                v = [r["gib_per_s"] for r in runs]
+                res[op] = (sum(v), sum(v) / len(v), min(v), max(v))
+            return {"value": round(res["seal"][0], 3), "unit": "GiB/s", "cores": len(cores),
                     "kind": "reference",
-                    "sample": f"{nrec} synthetic records x {length} B (~1 GiB resident), "
-                              f"{r['records_sealed']} seals in {r['seconds']:.1f} s, "
-                              f"{threads} threads, reference EVP_AEAD_CTX_seal_scatter "
-                              "(bench/aead.cc method, asm dispatch on this host)"}
+                    "per_core": round(res["seal"][1], 3),
+                    "per_core_min_max": [round(res["seal"][2], 3), round(res["seal"][3], 3)],
+                    "open": {"value": round(res["open"][0], 3),
+                             "per_core": round(res["open"][1], 3)},
+                    "cpu_model": cpu_model(),
+                    "sample": f"BM_SpeedAEAD method (bench/aead.cc:41-133): {aead} seal and open "
+                              f"of one {length}-byte input, 13-byte AD, resealed for {seconds} s, "
+                              f"one single-threaded process pinned per physical core x "
+                              f"{len(cores)} cores (cache-resident, as the reference bench; the "
+                              f"GPU value is HBM-resident)"}
         except Exception as e:  # pragma: no cover
             print(f"cpu baseline (reference) failed: {e}", file=sys.stderr)
-    # Fallback: the C oracle restatement (a port, not the reference).
+    # Fallback: the C oracle restatement (a port, not the reference), one thread.
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as o
-    n = 256
-    pt, offs, nonces, ads = o.synth_batch(0, np.full(n, length, dtype=np.uint64))
+    n = 64
+    lens = np.full(n, length, dtype=np.uint64)
+    pt, offs, nonces, ads = o.synth_batch(0, lens)
     keys = np.frombuffer(synth_key(0, 16 if "128" in aead else 32), dtype=np.uint8).copy()
     out = np.zeros_like(pt)
     tags = np.zeros(16 * n, dtype=np.uint8)
     adoff = np.arange(n, dtype=np.uint64) * np.uint64(13)
     adl = np.full(n, 13, dtype=np.uint64)
-    lens = np.full(n, length, dtype=np.uint64)
     aid = o.AES_GCM if "gcm" in aead else o.CHACHA20_POLY1305
     t0, done = time.time(), 0
     while time.time() - t0 < seconds:
         o.batch(aid, 1, keys, len(keys), None, pt, out, offs, lens, nonces, 12, ads, adoff, adl,
-                tags, 16, None, threads)
+                tags, 16, None, 1)
         done += n
     dt = time.time() - t0
-    return {"value": round(done * length / dt / 2**30, 4), "unit": "GiB/s", "cores": threads,
-            "kind": "port", "sample": f"{done} records x {length} B via the C oracle"}
+    return {"value": round(done * length / dt / 2**30, 4), "unit": "GiB/s", "cores": 1,
+            "kind": "port", "cpu_model": cpu_model(),
+            "sample": f"{done} records x {length} B via the C oracle, one thread"}
 
 
-def load_traffic(kernel_prefix):
-    """HBM bytes per launch from the rocprofv3 PMC pass (tools/pmc_traffic.py)."""
+def load_profile(kernel_prefix):
+    """HBM bytes per launch and LDS/VALU busy fractions from the rocprofv3 PMC
+    passes (tools/pmc_traffic.py -> profiles/traffic.json)."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(p):
-        return None
+        return None, None
     try:
         d = json.load(open(p))
         for k, v in d.items():
             if k.startswith(kernel_prefix):
-                return v.get("hbm_bytes_per_launch")
+                cb = {x: round(v[x], 3) for x in ("lds_busy", "valu_busy") if x in v}
+                if cb:
+                    cb["source"] = "profiles/traffic.json (rocprofv3 PMC)"
+                return v.get("hbm_bytes_per_launch"), cb or None
     except Exception:
-        return None
-    return None
+        return None, None
+    return None, None
+
+
+# ---------------------------------------------------------------------------
+
+def plan_only(args, world, rank):
+    """The launcher/plan/reduction path without a GPU (gloo)."""
+    dist = _dist()
+    if world > 1:
+        dist.init_process_group("gloo")
+    sh = shard_plan(args.config, rank, world, args.records)
+    mine = {"rank": rank, "first": sh.first, "n": sh.n, "bytes": int(sh.lens.sum()),
+            "key_first": sh.key_first, "nkeys": sh.nkeys}
+    plans = [mine]
+    if world > 1:
+        plans = [None] * world
+        dist.all_gather_object(plans, mine)
+    t_max = reduce_max(float(rank + 1), world)
+    total = reduce_sum(float(mine["bytes"]), world)
+    if rank == 0:
+        print(json.dumps({"plan_only": True, "config": args.config, "n_gpus": world,
+                          "scaling": CONFIGS[args.config][4], "plan": plans,
+                          "reduce_max": t_max, "reduce_sum": total}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -192,36 +381,54 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
-    ap.add_argument("--records", type=int, default=0, help="override records per GPU")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--records", type=int, default=0,
+                    help="override the record count (per GPU for weak configs, total for "
+                         "config4/config5)")
+    ap.add_argument("--cpu-seconds", type=float, default=5.0,
+                    help="seconds per CPU-baseline measurement (seal, then open)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="launcher + shard plan + reductions on CPU (gloo), no GPU")
     ap.add_argument("--op", default="seal", choices=["seal", "open"],
                     help="open: time EVP_AEAD open of the sealed batch (ct -> separate out)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}",
+              file=sys.stderr)
+    if args.plan_only:
+        plan_only(args, world, rank)
+        return
+
+    import torch
+    import boringssl_amd as ba  # fails loudly without the HIP library
+
+    dist = _dist()
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     torch.cuda.set_device(local)
     ba.set_device(local)
     dev = torch.device(f"cuda:{local}")
 
-    aead, key_len, _, length, desc = CONFIGS[args.config]
-    first, lens, offs, total_pad = shard_plan(args.config, rank, world, args.records)
-    nrec = len(lens)
-    padded = (lens + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+    aead, key_len, _, length, scaling, desc = CONFIGS[args.config]
+    sh = shard_plan(args.config, rank, world, args.records)
+    first, lens, offs, nrec = sh.first, sh.lens, sh.offs, sh.n
+    padded = _pad16(lens)
     pt_bytes = int(lens.sum())
 
     d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
     d_lens = torch.from_numpy(lens.astype(np.int64)).to(dev)
-    d_pt = torch.empty(total_pad, dtype=torch.uint8, device=dev)
-    d_ct = torch.empty(total_pad, dtype=torch.uint8, device=dev)
-    d_nonce = torch.empty(12 * nrec, dtype=torch.uint8, device=dev)
-    d_ad = torch.empty(13 * nrec, dtype=torch.uint8, device=dev)
-    d_tags = torch.empty(16 * nrec, dtype=torch.uint8, device=dev)
-    d_status = torch.zeros(nrec, dtype=torch.uint8, device=dev)
+    d_pt = torch.empty(max(1, sh.total_pad), dtype=torch.uint8, device=dev)
+    d_ct = torch.empty(max(1, sh.total_pad), dtype=torch.uint8, device=dev)
+    d_nonce = torch.empty(max(1, 12 * nrec), dtype=torch.uint8, device=dev)
+    d_ad = torch.empty(max(1, 13 * nrec), dtype=torch.uint8, device=dev)
+    d_tags = torch.empty(max(1, 16 * nrec), dtype=torch.uint8, device=dev)
+    d_status = torch.zeros(max(1, nrec), dtype=torch.uint8, device=dev)
     ba.synth_fill_device(first, nrec, d_offs, d_lens, d_pt, d_nonce, d_ad)
     nonce_len = 12
     if aead == "xchacha20-poly1305":  # 24-byte nonces (ref_tool.cc make_nonce)
@@ -233,18 +440,18 @@ def main():
     rpk = RECORDS_PER_KEY.get(args.config)
     d_kidx = None
     if rpk:
-        # Keys of this rank's shard: global key ids first/rpk .. (synth_key).
-        nkeys = (nrec + rpk - 1) // rpk
-        k0 = first // rpk
-        ctx = ba.Keyset(aead, b"".join(synth_key(k0 + k, key_len) for k in range(nkeys)), nkeys,
-                        16)
+        # The rank's keys: global key ids key_first .. (synth_key).
+        nkeys = sh.nkeys
+        ctx = ba.Keyset(aead, b"".join(synth_key(sh.key_first + k, key_len)
+                                       for k in range(nkeys)), nkeys, 16)
         d_kidx = torch.from_numpy((np.arange(nrec) // rpk).astype(np.int32)).to(dev)
     else:
         ctx = ba.AEADCtx(aead, synth_key(0, key_len), 16)
+    stride = int(padded[0]) if nrec else 16
     batch = ba.make_batch(nrec, d_pt, d_ct, d_tags, d_nonce, nonce_len, d_ad,
                           offsets=None if uniform else d_offs,
                           lengths=None if uniform else d_lens,
-                          record_stride=int(padded[0]) if uniform else 0,
+                          record_stride=stride if uniform else 0,
                           record_len=int(length) if uniform else 0,
                           ad_stride=13, ad_len=13, status=d_status, key_index=d_kidx)
     stream = torch.cuda.current_stream()
@@ -258,7 +465,7 @@ def main():
         batch = ba.make_batch(nrec, d_ct, d_back, d_tags, d_nonce, nonce_len, d_ad,
                               offsets=None if uniform else d_offs,
                               lengths=None if uniform else d_lens,
-                              record_stride=int(padded[0]) if uniform else 0,
+                              record_stride=stride if uniform else 0,
                               record_len=int(length) if uniform else 0,
                               ad_stride=13, ad_len=13, status=d_status, key_index=d_kidx)
         op = ctx.open_batch_device
@@ -266,7 +473,7 @@ def main():
     for _ in range(args.warmup):
         op(batch, stream)
     torch.cuda.synchronize()
-    if args.warmup and not bool(d_status.all()):
+    if args.warmup and nrec and not bool(d_status[:nrec].all()):
         raise SystemExit(f"{args.op} reported failed records")
 
     # Kernel-level timing: the library records HIP events on `stream`
@@ -285,7 +492,7 @@ def main():
     elapsed = t1 - t0
     kernel_ms = ba.collect_kernel_times()
     ba.set_kernel_timing(False)
-    if not bool(d_status.all()):
+    if nrec and not bool(d_status[:nrec].all()):
         raise SystemExit(f"{args.op} reported failed records")
     if args.op == "open" and not torch.equal(d_back[:16 << 10], d_pt[:16 << 10]):
         raise SystemExit("open did not return the plaintext")
@@ -299,7 +506,9 @@ def main():
     value = total_bytes * args.steps / elapsed / 2**30
     algo_bytes = 2 * pt_bytes + (29 + nonce_len) * nrec  # PT in + CT out + tag + nonce + AD
     achieved = algo_bytes / (avg_kernel_ms / 1000.0) / 1e9
-    traffic = load_traffic(kname)
+    traffic, compute_bound = load_profile(kname)
+    if world > 1 or args.records or args.op != "seal":
+        traffic, compute_bound = None, None  # the profile is of the default N=1 seal run
 
     result = {
         "metric": METRICS[args.config] if args.op == "seal" else
@@ -311,17 +520,20 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (device-generated records, oracle/synth.h definition)",
-        "config": {"workload": desc, "aead": aead, "records_per_gpu": nrec,
-                   "record_bytes": length, "plaintext_bytes_per_gpu": pt_bytes,
+        "config": {"workload": desc, "aead": aead,
+                   "records_per_gpu" if scaling == "weak" else "records_rank0": nrec,
+                   "record_bytes": length, "plaintext_bytes_rank0": pt_bytes,
+                   "plaintext_bytes_all_ranks": int(total_bytes),
                    "parallelism": f"dp{world} (independent record shards, no collective)"},
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "algorithmic_bytes_per_launch": algo_bytes,
-                     "avg_kernel_ms": round(avg_kernel_ms, 4)},
+                     "avg_kernel_ms": round(avg_kernel_ms, 4),
+                     "compute_bound": compute_bound},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(aead, length, args.cpu_seconds)

@@ -89,11 +89,38 @@ const evp_aead_st kAes256GcmTls13 = {32, 12, 16, 16, kAeadAesGcm, 13};
 // Device-resident key material for one or more keys.
 struct KeyMaterial {
   const EVP_AEAD *aead;
-  int device;
+  int device;  // the HIP device the key material lives on
   size_t num_keys;
   int nr;
   void *dev;  // GcmKeyDev[num_keys] or ChaChaKeyDev[num_keys]
+  size_t bytes;
 };
+
+// Makes `dev` the calling thread's current HIP device for the guard's scope
+// and restores the previous one (host-buffer calls may come from any thread,
+// as the reference's EVP_AEAD_CTX allows, aead.h:298-299).
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) return;
+    ok = prev == dev || hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (ok) hipSetDevice(prev);
+  }
+};
+
+// Device-batch calls take device pointers and a stream of the caller's
+// current device; they must be made on the device that holds the keys.
+bool on_key_device(const KeyMaterial *km) {
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev != km->device) {
+    PUT_ERROR(ERR_R_SHOULD_NOT_HAVE_BEEN_CALLED);
+    return false;
+  }
+  return true;
+}
 
 // State kept in EVP_AEAD_CTX.state (560 bytes, reference aead.h:222-235).
 struct CtxState {
@@ -110,10 +137,14 @@ CtxState *state_of(const EVP_AEAD_CTX *ctx) {
 KeyMaterial *make_keys(const EVP_AEAD *aead, const uint8_t *keys, size_t num_keys) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  KeyMaterial *km = new (std::nothrow) KeyMaterial{aead, dev, num_keys, 0, nullptr};
+  KeyMaterial *km = new (std::nothrow) KeyMaterial{aead, dev, num_keys, 0, nullptr, 0};
   if (!km) return nullptr;
   size_t bytes;
   std::vector<uint8_t> host;
+  struct Wipe {  // the expanded keys in host memory are wiped on every path
+    std::vector<uint8_t> &v;
+    ~Wipe() { secure_zero(v.data(), v.size()); }
+  } wipe{host};
   if (aead->kind == kAeadAesGcm || aead->kind == kAeadAesGcmSiv) {
     bytes = num_keys * sizeof(GcmKeyDev);
     host.resize(bytes);
@@ -135,6 +166,7 @@ KeyMaterial *make_keys(const EVP_AEAD *aead, const uint8_t *keys, size_t num_key
     delete km;
     return nullptr;
   }
+  km->bytes = bytes;
   if (hipMemcpy(km->dev, host.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
     hipFree(km->dev);
     delete km;
@@ -145,7 +177,12 @@ KeyMaterial *make_keys(const EVP_AEAD *aead, const uint8_t *keys, size_t num_key
 
 void free_keys(KeyMaterial *km) {
   if (!km) return;
-  if (km->dev) hipFree(km->dev);
+  if (km->dev) {
+    DeviceGuard g(km->device);
+    hipMemset(km->dev, 0, km->bytes);  // wipe the device copy (OPENSSL_cleanse)
+    hipDeviceSynchronize();
+    hipFree(km->dev);
+  }
   delete km;
 }
 
@@ -263,8 +300,9 @@ bool check_batch(const EVP_AEAD *aead, const BSSL_AMD_BATCH *b) {
 
 // ---- single-record helper: host buffers -> one-record device batch --------
 
+// Per-thread staging buffer and stream of the host-buffer calls, one per
+// device (a thread may use contexts of several GPUs).
 struct Scratch {
-  int device = -1;
   uint8_t *dev = nullptr;
   size_t cap = 0;
   hipStream_t stream = nullptr;
@@ -273,31 +311,28 @@ struct Scratch {
     if (stream) hipStreamDestroy(stream);
   }
 };
-thread_local Scratch t_scratch;
+constexpr int kMaxDevices = 64;
+thread_local Scratch t_scratch[kMaxDevices];
 
+// Scratch of the current device (the caller holds a DeviceGuard).
 uint8_t *scratch(size_t bytes, hipStream_t *stream) {
   int dev = 0;
-  hipGetDevice(&dev);
-  if (t_scratch.device != dev) {
-    t_scratch.dev = nullptr;  // buffers of another device are kept until exit
-    t_scratch.cap = 0;
-    t_scratch.stream = nullptr;
-    t_scratch.device = dev;
-  }
-  if (!t_scratch.stream && hipStreamCreateWithFlags(&t_scratch.stream, hipStreamNonBlocking) != hipSuccess)
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+  Scratch &sc = t_scratch[dev];
+  if (!sc.stream && hipStreamCreateWithFlags(&sc.stream, hipStreamNonBlocking) != hipSuccess)
     return nullptr;
-  if (t_scratch.cap < bytes) {
-    if (t_scratch.dev) hipFree(t_scratch.dev);
+  if (sc.cap < bytes) {
+    if (sc.dev) hipFree(sc.dev);
     size_t cap = bytes < (1u << 20) ? (1u << 20) : bytes;
-    if (hipMalloc(&t_scratch.dev, cap) != hipSuccess) {
-      t_scratch.dev = nullptr;
-      t_scratch.cap = 0;
+    if (hipMalloc(&sc.dev, cap) != hipSuccess) {
+      sc.dev = nullptr;
+      sc.cap = 0;
       return nullptr;
     }
-    t_scratch.cap = cap;
+    sc.cap = cap;
   }
-  *stream = t_scratch.stream;
-  return t_scratch.dev;
+  *stream = sc.stream;
+  return sc.dev;
 }
 
 size_t round16(size_t n) { return (n + 15) & ~size_t(15); }
@@ -308,6 +343,11 @@ int one_record(const EVP_AEAD_CTX *ctx, bool open, const uint8_t *in, uint8_t *o
                size_t len, const uint8_t *nonce, size_t nonce_len, const uint8_t *ad,
                size_t ad_len, uint8_t *tag, size_t tag_len) {
   CtxState *st = state_of(ctx);
+  DeviceGuard guard(st->km->device);
+  if (!guard.ok) {
+    PUT_ERROR(ERR_R_INTERNAL_ERROR);
+    return 0;
+  }
   const size_t o_in = 0, o_nonce = round16(len), o_ad = o_nonce + round16(nonce_len),
                o_tag = o_ad + round16(ad_len), o_status = o_tag + 16,
                total = o_status + 16;
@@ -500,6 +540,18 @@ bool aead_record_checks(const EVP_AEAD_CTX *ctx, size_t nonce_len, size_t in_len
   return true;
 }
 
+// The per-AEAD tag-length rule of init (e_aes.cc.inc:742-749,
+// e_chacha20poly1305.cc:51-57, e_aesgcmsiv.cc:542-548): 0 means the maximum.
+bool resolve_tag_len(const EVP_AEAD *aead, size_t *tag_len) {
+  if (*tag_len == EVP_AEAD_DEFAULT_TAG_LENGTH) *tag_len = aead->max_tag_len;
+  if (*tag_len > aead->max_tag_len || (aead->kind == kAeadAesGcmSiv && *tag_len != 16)) {
+    PUT_ERROR(aead->kind == kAeadAesGcm || aead->kind == kAeadAesGcmSiv ? CIPHER_R_TAG_TOO_LARGE
+                                                                       : CIPHER_R_TOO_LARGE);
+    return false;
+  }
+  return true;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -558,12 +610,7 @@ int EVP_AEAD_CTX_init_with_direction(EVP_AEAD_CTX *ctx, const EVP_AEAD *aead,
     ctx->aead = nullptr;
     return 0;
   }
-  // e_aes.cc.inc:742-749 / e_chacha20poly1305.cc:51-57
-  if (tag_len == EVP_AEAD_DEFAULT_TAG_LENGTH) tag_len = aead->max_tag_len;
-  if (tag_len > aead->max_tag_len ||
-      (aead->kind == kAeadAesGcmSiv && tag_len != 16)) {  // e_aesgcmsiv.cc:542-548
-    PUT_ERROR(aead->kind == kAeadAesGcm || aead->kind == kAeadAesGcmSiv ? CIPHER_R_TAG_TOO_LARGE
-                                                                       : CIPHER_R_TOO_LARGE);
+  if (!resolve_tag_len(aead, &tag_len)) {
     ctx->aead = nullptr;
     return 0;
   }
@@ -921,6 +968,7 @@ int EVP_AEAD_CTX_seal_batch_device(const EVP_AEAD_CTX *ctx, const BSSL_AMD_BATCH
   if (!ctx || !ctx->aead || !check_batch(ctx->aead, batch)) return 0;
   if (batch->num_records == 0) return 1;
   CtxState *st = state_of(ctx);
+  if (!on_key_device(st->km)) return 0;
   if (!ctx->aead->tls)
     return run_batch(st->km, ctx->tag_len, batch, false, false, hip_stream);
   if (batch->nonce_len != 12) {  // e_aes.cc.inc:1077-1080, 1168-1171 (seal only)
@@ -948,6 +996,7 @@ int EVP_AEAD_CTX_open_batch_device(const EVP_AEAD_CTX *ctx, const BSSL_AMD_BATCH
                                    void *hip_stream) {
   if (!ctx || !ctx->aead || !check_batch(ctx->aead, batch)) return 0;
   if (batch->num_records == 0) return 1;
+  if (!on_key_device(state_of(ctx)->km)) return 0;
   return run_batch(state_of(ctx)->km, ctx->tag_len, batch, true, false, hip_stream);
 }
 
@@ -1014,6 +1063,7 @@ int EVP_AEAD_CTX_sealv_batch_device(const EVP_AEAD_CTX *ctx, const BSSL_AMD_IOV_
   if (!ctx || !ctx->aead || !check_iov_batch(ctx->aead, batch)) return 0;
   if (batch->num_records == 0) return 1;
   CtxState *st = state_of(ctx);
+  if (!on_key_device(st->km)) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(hip_stream);
   uint8_t *valid = nullptr;
   if (ctx->aead->tls) {  // the monotonic-nonce check, as for contiguous batches
@@ -1049,6 +1099,7 @@ int EVP_AEAD_CTX_openv_detached_batch_device(const EVP_AEAD_CTX *ctx,
                                              const BSSL_AMD_IOV_BATCH *batch, void *hip_stream) {
   if (!ctx || !ctx->aead || !check_iov_batch(ctx->aead, batch)) return 0;
   if (batch->num_records == 0) return 1;
+  if (!on_key_device(state_of(ctx)->km)) return 0;
   const int rc = iov_batch_run(
       iov_desc(batch), KeyRunner(state_of(ctx)->km, ctx->tag_len, true, hip_stream, nullptr),
       hip_stream);
@@ -1070,11 +1121,7 @@ BSSL_AMD_KEYSET *BSSL_AMD_KEYSET_new(const EVP_AEAD *aead, const uint8_t *keys,
     PUT_ERROR(ERR_R_SHOULD_NOT_HAVE_BEEN_CALLED);
     return nullptr;
   }
-  if (tag_len == EVP_AEAD_DEFAULT_TAG_LENGTH) tag_len = aead->max_tag_len;
-  if (tag_len > aead->max_tag_len) {
-    PUT_ERROR(CIPHER_R_TAG_TOO_LARGE);
-    return nullptr;
-  }
+  if (!resolve_tag_len(aead, &tag_len)) return nullptr;
   KeyMaterial *km = make_keys(aead, keys, num_keys);
   if (!km) {
     PUT_ERROR(ERR_R_MALLOC_FAILURE);
@@ -1101,6 +1148,7 @@ int BSSL_AMD_KEYSET_seal_batch_device(const BSSL_AMD_KEYSET *ks, const BSSL_AMD_
     return 0;
   }
   if (batch->num_records == 0) return 1;
+  if (!on_key_device(ks->km)) return 0;
   return run_batch(ks->km, ks->tag_len, batch, false, true, hip_stream);
 }
 
@@ -1108,6 +1156,7 @@ int BSSL_AMD_KEYSET_open_batch_device(const BSSL_AMD_KEYSET *ks, const BSSL_AMD_
                                       void *hip_stream) {
   if (!ks || !check_batch(ks->km->aead, batch)) return 0;
   if (batch->num_records == 0) return 1;
+  if (!on_key_device(ks->km)) return 0;
   return run_batch(ks->km, ks->tag_len, batch, true, true, hip_stream);
 }
 
@@ -1194,6 +1243,7 @@ int tls_records(BSSL_AMD_TLS_AEAD *t, const BSSL_AMD_TLS_RECORDS *r, void *strea
   }
   const EVP_AEAD_CTX *ctx = &t->ctx;
   CtxState *st = state_of(ctx);
+  if (!on_key_device(st->km)) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const uint32_t ad_stride = t->tls13 ? 5 : 13;
   const uint32_t extra_len = t->tls13 ? 1 : 0;
@@ -1338,6 +1388,15 @@ BSSL_AMD_TLS_AEAD *BSSL_AMD_TLS_AEAD_new(enum evp_aead_direction_t direction, ui
   memset(t->fixed_iv, 0, sizeof(t->fixed_iv));
   memcpy(t->fixed_iv, fixed_iv, fixed_iv_len);
   t->seq = seq;
+  if (t->seal && tls13 && t->ctx.aead->tls == 13 && seq != 0) {
+    // The tls13 AEAD takes its nonce mask from the first sealed nonce, which
+    // it assumes is sequence number 0 (e_aes.cc.inc:1181-1185).  A writer
+    // that starts mid-stream gets the state the AEAD would have after
+    // sealing records 0 .. seq-1: mask = the IV's low 64 bits, next >= seq.
+    CtxState *st = state_of(&t->ctx);
+    st->mask = load_be64(t->fixed_iv + 4);
+    st->min_next_nonce = seq;
+  }
   return t;
 }
 

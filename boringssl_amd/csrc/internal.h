@@ -189,6 +189,9 @@ int launch_synth(uint64_t first, size_t n, const uint64_t *offsets,
                  const uint64_t *lengths, uint8_t *pt, uint8_t *nonces,
                  uint8_t *ads, void *stream);
 
+// Wipes key material that goes out of scope (reference: OPENSSL_cleanse).
+void secure_zero(void *p, size_t n);
+
 // Host-side key setup (key_setup.cc).
 bool gcm_key_setup(const uint8_t *key, size_t key_len, GcmKeyDev *out);
 void chacha_key_setup(const uint8_t *key, ChaChaKeyDev *out);

@@ -9,6 +9,11 @@
 #include "internal.h"
 
 namespace bssl_amd {
+
+void secure_zero(void *p, size_t n) {
+  if (n) explicit_bzero(p, n);
+}
+
 namespace {
 
 struct SboxTable {
@@ -154,7 +159,10 @@ uint32_t rotl32(uint32_t v, int n) { return (v << n) | (v >> (32 - n)); }
 bool gcm_key_setup(const uint8_t *key, size_t key_len, GcmKeyDev *out) {
   uint8_t w[240];
   int nr = expand_key(key, key_len, w);
-  if (!nr) return false;
+  if (!nr) {
+    secure_zero(w, sizeof(w));
+    return false;
+  }
   memset(out, 0, sizeof(*out));
   out->nr = (uint32_t)nr;
   out->key_bytes = (uint32_t)key_len;
@@ -184,9 +192,16 @@ bool gcm_key_setup(const uint8_t *key, size_t key_len, GcmKeyDev *out) {
           store_u128(acc, b);
           for (int j = 0; j < 4; j++)
             out->htab[pw][2 * k + half][val][j] = load_le32(b + 4 * j);
+          secure_zero(b, sizeof(b));
         }
     p = gf_mul(p, p);
+    secure_zero(v, sizeof(v));
   }
+  // The reference wipes key state on cleanup (OPENSSL_cleanse); so do the
+  // host temporaries here.
+  secure_zero(w, sizeof(w));
+  secure_zero(hb, sizeof(hb));
+  secure_zero(&p, sizeof(p));
   return true;
 }
 

@@ -13,6 +13,11 @@
 //   ref_tool bench AEAD LEN NREC T SECS    CPU baseline: T threads seal a
 //                                          resident sample of NREC synthetic
 //                                          records for about SECS seconds
+//   ref_tool bench1 AEAD seal|open LEN SECS  one thread, exactly BM_SpeedAEAD
+//                                          (bench/aead.cc:41-133): zero key,
+//                                          nonce, 13-byte AD and input, one
+//                                          16-byte-aligned buffer resealed
+//                                          (reopened) for about SECS seconds
 #include <openssl/aead.h>
 #include <openssl/sha.h>
 #include <omp.h>
@@ -247,6 +252,63 @@ int cmd_bench(int argc, char **argv) {
   return 0;
 }
 
+// bench/aead.cc:41-133 for one (AEAD, direction, input size): the CPU
+// baseline of BASELINE.md section 3, one single-threaded process per core.
+int cmd_bench1(int argc, char **argv) {
+  if (argc < 6) return 2;
+  size_t key_len;
+  const char *name = argv[2];
+  const EVP_AEAD *aead = aead_by_name(name, &key_len);
+  const bool open = std::string(argv[3]) == "open";
+  const size_t len = strtoull(argv[4], nullptr, 0);
+  const double secs = atof(argv[5]);
+  const size_t nl = EVP_AEAD_nonce_length(aead), overhead = EVP_AEAD_max_overhead(aead);
+  const size_t kAlign = 16, kAdLen = 13;
+  std::vector<uint8_t> key(key_len), nonce(nl), ad(kAdLen);
+  std::vector<uint8_t> in_s(len + kAlign), out_s(len + overhead + kAlign),
+      in2_s(len + overhead + kAlign), tag_s(overhead + kAlign);
+  auto align = [](uint8_t *p) {
+    return reinterpret_cast<uint8_t *>((reinterpret_cast<uintptr_t>(p) + 15) & ~uintptr_t(15));
+  };
+  uint8_t *in = align(in_s.data()), *out = align(out_s.data()), *in2 = align(in2_s.data()),
+          *tag = align(tag_s.data());
+  bssl::ScopedEVP_AEAD_CTX ctx;
+  if (!EVP_AEAD_CTX_init_with_direction(ctx.get(), aead, key.data(), key_len,
+                                        EVP_AEAD_DEFAULT_TAG_LENGTH, evp_aead_seal))
+    return 1;
+  size_t out_len = 0;
+  if (open) {
+    if (!EVP_AEAD_CTX_seal(ctx.get(), out, &out_len, len + overhead, nonce.data(), nl, in, len,
+                           ad.data(), kAdLen))
+      return 1;
+    ctx.Reset();
+    if (!EVP_AEAD_CTX_init_with_direction(ctx.get(), aead, key.data(), key_len,
+                                          EVP_AEAD_DEFAULT_TAG_LENGTH, evp_aead_open))
+      return 1;
+  }
+  uint64_t iters = 0;
+  auto t0 = std::chrono::steady_clock::now();
+  double e = 0;
+  do {
+    for (int k = 0; k < 64; k++) {
+      size_t l;
+      int ok = open ? EVP_AEAD_CTX_open(ctx.get(), in2, &l, len + overhead, nonce.data(), nl, out,
+                                        out_len, ad.data(), kAdLen)
+                    : EVP_AEAD_CTX_seal_scatter(ctx.get(), out, tag, &l, overhead, nonce.data(),
+                                                nl, in, len, nullptr, 0, ad.data(), kAdLen);
+      if (!ok) return 1;
+      __asm__ volatile("" ::: "memory");  // benchmark::ClobberMemory
+    }
+    iters += 64;
+    e = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  } while (e < secs);
+  printf("{\"aead\": \"%s\", \"op\": \"%s\", \"len\": %zu, \"iterations\": %llu, "
+         "\"seconds\": %.4f, \"gib_per_s\": %.4f}\n",
+         name, open ? "open" : "seal", len, (unsigned long long)iters, e,
+         (double)iters * (double)len / e / (1024.0 * 1024 * 1024));
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -258,5 +320,6 @@ int main(int argc, char **argv) {
   if (cmd == "edge") return cmd_edge();
   if (cmd == "digest") return cmd_digest(argc, argv);
   if (cmd == "bench") return cmd_bench(argc, argv);
+  if (cmd == "bench1") return cmd_bench1(argc, argv);
   return 2;
 }

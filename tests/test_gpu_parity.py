@@ -632,10 +632,11 @@ def test_tls_record_layer(version, aead):
     key = bytes(rng.getrandbits(8) for _ in range(16 if "128" in aead else 32))
     xor = version == 0x0304 or aead == "chacha20-poly1305"
     fixed_iv = bytes(rng.getrandbits(8) for _ in range(12 if xor else 4))
-    # TLS 1.3 traffic keys start at sequence number 0 (RFC 8446 5.3); the tls13
-    # AEAD's nonce check takes the first nonce as the mask on that basis
-    # (e_aes.cc.inc:1181-1185), so only TLS 1.2 starts mid-stream here.
-    seq0 = 0 if version == 0x0304 else rng.getrandbits(40)
+    # TLS 1.3 traffic keys start at sequence number 0 (RFC 8446 5.3) and the
+    # tls13 AEAD takes its nonce mask from the first nonce on that basis
+    # (e_aes.cc.inc:1181-1185); a writer created mid-stream starts from the
+    # state the AEAD has after records 0 .. seq0-1.  Both starts are covered.
+    seq0 = 0 if (version == 0x0304 and aead == "aes-128-gcm") else rng.getrandbits(40)
     n = 300
     lens = [rng.choice([0, 1, 15, 16, 17, 31, 64, 100, 1350, 4096, 16384]) for _ in range(n)]
     lens[7] = 16385  # over SSL3_RT_MAX_PLAIN_LENGTH: that record fails
@@ -811,3 +812,29 @@ def test_iovec_batch_vs_oracle(aead):
             assert st[i] == 0 and got == bytes(len(pts[i])), i
         else:
             assert st[i] == 1 and got == pts[i], i
+
+
+def test_context_used_from_another_device():
+    """A context created on GPU 0 and used after the thread switched to GPU 1:
+    host-buffer calls run on the key's device (and restore the caller's
+    device); device-batch calls on the wrong device fail cleanly instead of
+    launching kernels against another GPU's key memory."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    key, nonce = bytes(range(16)), bytes(12)
+    ctx = ba.AEADCtx("aes-128-gcm", key, 16)
+    ok, ct, tag = o.seal(o.AES_GCM, key, nonce, b"hello", b"ad")
+    try:
+        ba.set_device(1)
+        torch.cuda.set_device(1)
+        assert ctx.seal(nonce, b"hello", b"ad") == ct + tag
+        assert ctx.open(nonce, ct + tag, b"ad") == b"hello"
+        assert torch.cuda.current_device() == 1
+        d = torch.zeros(64, dtype=torch.uint8, device="cuda:1")
+        with pytest.raises(ba.AEADError) as e:
+            ctx.seal_batch_device(ba.make_batch(1, d, d, d, d, 12, d, record_len=16,
+                                                record_stride=16))
+        assert e.value.reason == 66  # ERR_R_SHOULD_NOT_HAVE_BEEN_CALLED
+    finally:
+        ba.set_device(0)
+        torch.cuda.set_device(0)

@@ -1,15 +1,21 @@
-"""Multi-rank (N>1) path on CPU with the gloo backend, world_size 2.
+"""Multi-rank (N>1) path on CPU with the gloo backend.
 
-bench.py shards the record sequence across ranks (weak scaling, no data-path
-collective): rank r seals records [r*n, (r+1)*n) with its own synthetic
-inputs, and the only collectives are the timing barrier and max/sum
-reductions.  This test runs those pieces on two gloo ranks and checks that the
+bench.py shards the record sequence across ranks with no data-path
+collective: weak configs seal records [r*n, (r+1)*n) per rank, config 4 splits
+ONE fixed batch into contiguous ranges balanced by bytes and config 5 splits
+the fixed key set by key ranges; the only collectives are the timing barrier
+and max/sum reductions.  These tests run those pieces on gloo ranks: the
 per-rank seals (done here by the CPU oracle, the checker) concatenate to
-exactly the single-process result, and that the reductions are max/sum.
+exactly the single-process result, the reductions are max/sum, and
+`bench.py --gpus N --plan-only` (the launcher itself: N fresh rank processes,
+rendezvous on 127.0.0.1) produces disjoint, covering, byte-balanced shards.
 """
 import hashlib
+import json
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -51,7 +57,8 @@ def _worker(rank, world, port, config, n, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    first, lens, offs, _ = bench.shard_plan(config, rank, world, records=n)
+    sh = bench.shard_plan(config, rank, world, records=n)
+    first, lens, offs = sh.first, sh.lens, sh.offs
     ct_d, tags = _seal_shard(config, first, lens, offs)
     t_max = bench.reduce_max(float(rank + 1), world)
     t_sum = bench.reduce_sum(float(lens.sum()), world)
@@ -63,6 +70,8 @@ def _worker(rank, world, port, config, n, q):
 @pytest.mark.parametrize("config", ["config2", "config3", "config4"])
 def test_two_rank_shards_match_single_process(config):
     world, n = 2, 24
+    if bench.CONFIGS[config][4] == "strong":
+        n = 48  # the fixed batch, split in two
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -73,16 +82,72 @@ def test_two_rank_shards_match_single_process(config):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # shards are disjoint and contiguous
-    assert [r[1] for r in res] == [0, n] and all(r[2] == n for r in res)
+    strong = bench.CONFIGS[config][4] == "strong"
+    total = n if strong else world * n
+    # shards are disjoint and contiguous and cover the batch
+    assert res[0][1] == 0 and res[1][1] == res[0][2] and res[0][2] + res[1][2] == total
     # concatenation of per-rank results == one process sealing both shards
-    first, lens, offs, _ = bench.shard_plan(config, 0, 1, records=world * n)
-    all_ct, all_tags = _seal_shard(config, first, lens, offs)
+    sh = bench.shard_plan(config, 0, 1, records=total)
+    all_ct, all_tags = _seal_shard(config, sh.first, sh.lens, sh.offs)
     assert res[0][4] + res[1][4] == all_tags
-    lens0 = lens[:n]
-    # ciphertext digests per shard
-    pt, offs_all, nonces, ads = o.synth_batch(0, lens)
-    assert res[0][3] == _seal_shard(config, 0, lens0, offs[:n])[0]
+    n0 = res[0][2]
+    sh0 = bench.shard_plan(config, 0, world, records=n)
+    assert res[0][3] == _seal_shard(config, 0, sh.lens[:n0], sh0.offs)[0]
     # reductions
     assert all(r[5] == 2.0 for r in res)
-    assert all(r[6] == float(lens.sum()) for r in res)
+    assert all(r[6] == float(sh.lens.sum()) for r in res)
+
+
+def _plan(config, gpus, records=0):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(os.path.dirname(bench.__file__), "bench.py"), "--gpus",
+           str(gpus), "--plan-only", "--config", config]
+    if records:
+        cmd += ["--records", str(records)]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = [x for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, out.stdout
+    return json.loads(line[0])
+
+
+@pytest.mark.parametrize("gpus", [2, 4, 8])
+def test_launcher_config4_byte_balanced(gpus):
+    """bench.py --gpus N starts N ranks itself; config 4 = ONE batch of 4M
+    mixed-length records split into contiguous, byte-balanced ranges."""
+    r = _plan("config4", gpus)
+    assert r["n_gpus"] == gpus and r["scaling"] == "strong"
+    plan = sorted(r["plan"], key=lambda x: x["rank"])
+    assert [p["rank"] for p in plan] == list(range(gpus))
+    pos = 0
+    for p in plan:
+        assert p["first"] == pos
+        pos += p["n"]
+    assert pos == 1 << 22
+    all_bytes = int(bench.mixed_lengths(0, 1 << 22).sum())
+    assert sum(p["bytes"] for p in plan) == all_bytes == r["reduce_sum"]
+    mean = all_bytes / gpus
+    # within about one record (the split is on 16-byte-padded lengths)
+    assert max(abs(p["bytes"] - mean) for p in plan) <= 65536
+    assert r["reduce_max"] == float(gpus)
+
+
+@pytest.mark.parametrize("gpus", [2, 8])
+def test_launcher_config5_key_ranges(gpus):
+    """config 5 = ONE set of 64K keys x 64 records split by key ranges."""
+    r = _plan("config5", gpus)
+    plan = sorted(r["plan"], key=lambda x: x["rank"])
+    assert sum(p["nkeys"] for p in plan) == 65536
+    kpos = 0
+    for p in plan:
+        assert p["key_first"] == kpos and p["first"] == 64 * kpos and p["n"] == 64 * p["nkeys"]
+        kpos += p["nkeys"]
+    assert len({p["nkeys"] for p in plan}) == 1
+
+
+def test_launcher_weak_config_per_gpu_shards():
+    r = _plan("config2", 2, records=1000)
+    plan = sorted(r["plan"], key=lambda x: x["rank"])
+    assert r["scaling"] == "weak"
+    assert [(p["first"], p["n"]) for p in plan] == [(0, 1000), (1000, 1000)]

@@ -45,7 +45,16 @@ def main():
             e.update({"fetch_bytes_corrected": fetch, "write_bytes": write,
                       "hbm_bytes_per_launch": fetch + write})
         if "GRBM_GUI_ACTIVE" in avg:
-            e["grbm_gui_active_per_xcd"] = avg["GRBM_GUI_ACTIVE"] / 8
+            cyc = avg["GRBM_GUI_ACTIVE"] / 8  # kernel cycles (GRBM sums the 8 XCDs)
+            e["grbm_gui_active_per_xcd"] = cyc
+            # Busy fractions of the compute units that can bind an integer
+            # kernel (MI355X_MICROARCH.md: SQ_LDS_IDX_ACTIVE = LDS-array cycles,
+            # summed over the 256 CUs; a wave64 VALU instruction occupies its
+            # SIMD32 for 2 cycles, 1024 SIMDs).
+            if "SQ_LDS_IDX_ACTIVE" in avg:
+                e["lds_busy"] = avg["SQ_LDS_IDX_ACTIVE"] / 256 / cyc
+            if "SQ_INSTS_VALU" in avg:
+                e["valu_busy"] = avg["SQ_INSTS_VALU"] * 2 / 1024 / cyc
         res[k] = e
     json.dump(res, open(dst, "w"), indent=1, sort_keys=True)
     for k, e in res.items():
