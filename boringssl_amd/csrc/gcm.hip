@@ -30,6 +30,7 @@
 //   records use several keys is processed in one pass per distinct key.
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "internal.h"
 #include "bs_aes.h"
@@ -43,17 +44,6 @@ namespace {
 
 // Waves per workgroup (one workgroup per CU: the LDS tables take 104 KiB); a
 // build-time knob for tuning (-DBSSL_AMD_GCM_WAVES=..).
-// Diagnostic build: per-phase s_memtime stamps of one wave of the bitsliced
-// kernel, printed with printf (never in the shipped library).
-#ifndef BSSL_AMD_BS_STAMPS
-#define BSSL_AMD_BS_STAMPS 0
-#endif
-#if BSSL_AMD_BS_STAMPS
-#define BS_STAMP(i) ts[i] = __builtin_amdgcn_s_memtime()
-#else
-#define BS_STAMP(i)
-#endif
-
 #ifndef BSSL_AMD_GHASH_GROUP
 #define BSSL_AMD_GHASH_GROUP 1
 #endif
@@ -83,9 +73,7 @@ __device__ __forceinline__ uint64_t stamp() {
 struct StampVec {
   uint64_t v[3];
 };
-constexpr int kThreads = kWaves * 64;
 constexpr int kRecPerWave = 4;
-constexpr int kRecPerTile = kWaves * kRecPerWave;  // <= 64 (one planning wave)
 
 // ---------------------------------------------------------------------------
 // Compile-time AES tables.
@@ -1008,25 +996,32 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
 // multiple of 256 its p and (e & 15) are fixed and e >> 4 steps by
 // kThreads/256, so all of its global loads are issued before the first LDS
 // write (one memory latency per key change instead of one per entry).
+template <int THREADS>
 __device__ __forceinline__ void build_g8(uint8_t *smem, const uint4 *__restrict__ t16, int tid) {
-  static_assert(kThreads % 256 == 0 && 4096 % kThreads == 0, "table build split");
-  constexpr int kPer = 4096 / kThreads;
+  static_assert(THREADS % 256 == 0 && 4096 % THREADS == 0, "table build split");
+  constexpr int kPer = 4096 / THREADS;
   const uint32_t p = (uint32_t)tid & 15u, lo = ((uint32_t)tid >> 4) & 15u;
   const uint32_t hi = (uint32_t)tid >> 8;
   const uint4 b = t16[(2 * p + 1) * 16 + lo];
   uint4 a[kPer];
 #pragma unroll
-  for (int i = 0; i < kPer; i++) a[i] = t16[(2 * p) * 16 + hi + (uint32_t)i * (kThreads / 256)];
+  for (int i = 0; i < kPer; i++) a[i] = t16[(2 * p) * 16 + hi + (uint32_t)i * (THREADS / 256)];
 #pragma unroll
   for (int i = 0; i < kPer; i++)
-    reinterpret_cast<uint4 *>(smem + kLdsG8)[tid + i * kThreads] = xor4(a[i], b);
+    reinterpret_cast<uint4 *>(smem + kLdsG8)[tid + i * THREADS] = xor4(a[i], b);
 }
 
-template <int NR, bool OPEN, bool XT>
-__global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restrict__ keys,
-                                                      BatchDesc b,
-                                                      const RecState *__restrict__ st,
-                                                      uint32_t *__restrict__ units) {
+// W waves per workgroup (one workgroup per CU).
+// Declared for 1024 threads whatever W is, so every variant is compiled
+// into 128 VGPRs (an 8-wave workgroup then leaves half of each SIMD's
+// register file free).
+template <int NR, bool OPEN, bool XT, int W>
+__global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__ keys,
+                                                    BatchDesc b,
+                                                    const RecState *__restrict__ st,
+                                                    uint32_t *__restrict__ units) {
+  constexpr int kThreads = W * 64;
+  constexpr int kRecPerTile = W * kRecPerWave;
   static_assert(kRecPerTile <= 64, "one wave plans a tile with ballots");
   __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
   // Pass list of the current tile: key and 64-bit record mask per pass.
@@ -1058,7 +1053,7 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
     // grid-wide counter, so waves that the SIMD arbiter favours (older
     // waves issue first) simply process more units instead of waiting at a
     // per-tile barrier for the slowest wave.
-    build_g8(smem, reinterpret_cast<const uint4 *>(keys[0].htab[4]), tid);
+    build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab[4]), tid);
     __syncthreads();
     RoundKeys rk;
 #pragma unroll
@@ -1118,7 +1113,7 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
         __syncthreads();
         // Byte table of H^16 from the key's nibble tables (power 4): entry
         // (e, p) = T[2p][e >> 4] ^ T[2p+1][e & 15] (key_setup.cc layout).
-        build_g8(smem, reinterpret_cast<const uint4 *>(keys[k].htab[4]), tid);
+        build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[k].htab[4]), tid);
         __syncthreads();
         loaded = k;
       }
@@ -1142,89 +1137,103 @@ __global__ __launch_bounds__(kThreads) void gcm_kernel(const GcmKeyDev *__restri
 }
 
 // ---------------------------------------------------------------------------
-// Bitsliced bulk kernel, for batches of long uniform-length records (DESIGN.md
-// §4.2b).  L lanes per record; lane q owns the record's blocks
-// j = 32*L*c + L*n + q of chunk c, n = 0..31, i.e. 32 blocks per chunk that
-// are encrypted together as bit-planes (bs_aes.h: block n in bit n).  The AES
-// is all VALU (v_bitop3 S-box circuit), leaving the LDS to GHASH alone; the
-// per-lane GHASH chain runs over the lane's blocks in order with multiplier
-// H^L and ends in the same rotation + tree as gcm_kernel (finish_record).
-constexpr int kBsWaves = 4;  // per workgroup; 2 workgroups per CU (VGPR-bound)
-constexpr int kBsThreads = kBsWaves * 64;
-constexpr uint32_t kBsLdsBytes = kGhashPowers * 8192;
+// Bitsliced AES engine: AES on the VALU only, no tables.
+// 16 lanes per record, as in process_records; lane q owns the record's
+// blocks j = 512*c + 16*n + q of chunk c, n = 0..31, and encrypts those 32
+// counter blocks together as 128 bit-planes (bs_aes.h: plane (i, b) = bit b
+// of state byte i, block n in bit n).  The plaintext of one n is a coalesced
+// 256-byte run per record.  GHASH runs per lane over its blocks in order
+// with multiplier H^16 -- exactly the lane algebra of process_records -- on
+// the same lane-rotated byte table of H^16 in LDS (kLdsG8), and the record
+// ends in the same finish_record<16>.
+//
+// Code size matters: the round loop is rolled (the last round reuses the
+// S-box code with the MixColumns step skipped), and the keystream of the 32
+// blocks is read back by a rolled loop through dynamic vector indexing
+// (s_set_gpr_idx), so the engine stays a small fraction of the 64 KiB
+// instruction cache it shares with the T-table role (gcm_hy_kernel).
+typedef uint32_t v32u __attribute__((ext_vector_type(32)));
 
-// acc <- Horner over the lane's 32 chunk blocks j = jc + L*n (< nb) of buf,
-// multiplier H^L (table log2(L)), loads kAhead blocks ahead.  FULL (every
-// block of the chunk exists, wave-uniform): addresses are one base plus
-// constant offsets.  Otherwise loads are unconditional (a block past the end
-// re-reads block 0 of the record, which exists for every record this kernel
-// runs on) and the update is a select -- straight-line code either way, so
-// the waitcnt pass counts the loads exactly.
-template <int L, bool FULL>
-__device__ __forceinline__ uint4 ghash_chunk(uint4 acc, const uint8_t *buf, uint32_t jc,
-                                             uint32_t nb, uint32_t lds_base, uint32_t mf0) {
-  constexpr int kLogL = L == 32 ? 5 : L == 16 ? 4 : 3;
-  constexpr int kAhead = 4;
-  const uint8_t *bp = buf + (uint64_t)jc * 16;
-  auto ld = [&](int n) {
-    const uint32_t j = jc + L * n;
-    if (FULL) return *reinterpret_cast<const uint4 *>(bp + 16 * L * n);
-    return *reinterpret_cast<const uint4 *>(buf + (uint64_t)(j < nb ? j : 0u) * 16);
-  };
-  uint4 cb[32];
-#pragma unroll
-  for (int n = 0; n < kAhead; n++) cb[n] = ld(n);
-#pragma unroll
-  for (int n = 0; n < 32; n++) {
-    if (n + kAhead < 32) cb[n + kAhead] = ld(n + kAhead);
-    const uint4 nx = xor4(gmul_batched<kLdsGhash + kLogL * 8192>(acc, lds_base, mf0), cb[n]);
-    if (FULL || jc + L * n < nb) acc = nx;
-  }
-  return acc;
+// 0 or 0xffffffff: bit `k` of w (v_bfe_i32 / s_bfe_i32).
+__device__ __forceinline__ uint32_t bit_mask(uint32_t w, int k) {
+  return (uint32_t)(((int32_t)(w << (31 - k))) >> 31);
 }
 
-// dst word `col` of the lane's 32 chunk blocks = src word ^ t[n] (keystream
-// word col of block n).  All loads are issued before the stores.
-template <int L, bool FULL>
-__device__ __forceinline__ void apply_keystream_word(const uint32_t t[32], const uint8_t *src,
-                                                     uint8_t *dst, uint32_t jc, uint32_t nb,
-                                                     int col) {
-  const uint8_t *sp = src + 4 * col;
-  uint8_t *dp = dst + 4 * col;
-  uint32_t x[32];
-  if (FULL) {
-    const uint8_t *sb = sp + (uint64_t)jc * 16;
-    uint8_t *db = dp + (uint64_t)jc * 16;
+// AES rounds 1..NR on the bit-planes (round 0 is in the planes already).
+// rkp: the key's FIPS-197 round-key words (GcmKeyDev::rk_plain), wave-uniform.
+template <int NR>
+__device__ __forceinline__ void bs_cipher(uint32_t (&p)[16][8], const uint32_t *__restrict__ rkp) {
+#pragma unroll 1
+  for (int r = 1; r <= NR; r++) {
+    uint32_t w[4];
 #pragma unroll
-    for (int n = 0; n < 32; n++) x[n] = *reinterpret_cast<const uint32_t *>(sb + 16 * L * n);
+    for (int i = 0; i < 4; i++) w[i] = (uint32_t)__builtin_amdgcn_readfirstlane(rkp[4 * r + i]);
+    const bool last = r == NR;
+    uint32_t np[16][8];
 #pragma unroll
-    for (int n = 0; n < 32; n++) *reinterpret_cast<uint32_t *>(db + 16 * L * n) = x[n] ^ t[n];
-  } else {
+    for (int c = 0; c < 4; c++) {
+      uint32_t a[4][8];
 #pragma unroll
-    for (int n = 0; n < 32; n++) {
-      const uint32_t j = jc + L * n;
-      x[n] = *reinterpret_cast<const uint32_t *>(sp + (uint64_t)(j < nb ? j : 0u) * 16);
+      for (int row = 0; row < 4; row++) sbox_planes(p[row + 4 * ((c + row) & 3)], a[row]);
+      if (!last) {
+        uint32_t o[4][8];
+        bs_mix_column(a, o, w, c);
+#pragma unroll
+        for (int row = 0; row < 4; row++)
+#pragma unroll
+          for (int k = 0; k < 8; k++) np[4 * c + row][k] = o[row][k];
+      } else {
+#pragma unroll
+        for (int row = 0; row < 4; row++)
+#pragma unroll
+          for (int k = 0; k < 8; k++) np[4 * c + row][k] = a[row][k] ^ bs_kmask(w, 4 * c + row, k);
+      }
     }
 #pragma unroll
-    for (int n = 0; n < 32; n++) {
-      const uint32_t j = jc + L * n;
-      if (j < nb) *reinterpret_cast<uint32_t *>(dp + (uint64_t)j * 16) = x[n] ^ t[n];
-    }
+    for (int i = 0; i < 16; i++)
+#pragma unroll
+      for (int k = 0; k < 8; k++) p[i][k] = np[i][k];
   }
 }
 
-template <int NR, bool OPEN, int L>
-__device__ __forceinline__ void process_records_bs(const GcmKeyDev *__restrict__ kp,
+// Keystream word c of the lane's 32 blocks (after the last round p[4c+row]
+// holds row `row` of output column c).
+__device__ __forceinline__ v32u bs_column_words(const uint32_t (&p)[16][8], int c) {
+  uint32_t o[32];
+#pragma unroll
+  for (int row = 0; row < 4; row++)
+#pragma unroll
+    for (int k = 0; k < 8; k++) o[8 * row + k] = p[4 * c + row][k];
+  bs_transpose32(o);
+  v32u v;
+#pragma unroll
+  for (int n = 0; n < 32; n++) v[n] = o[n];
+  return v;
+}
+
+// x * H^16 with the lane-rotated byte table (all 16 lookups in flight).
+__device__ __forceinline__ uint4 g8_mul(uint4 x, bool rs1, bool rs2, uint32_t rbs,
+                                        const uint32_t (&P)[4], const uint8_t *smem) {
+  Gh8 h;
+  g8_rotate(h, x, rs1, rs2, rbs);
+  const uint4 t0 = xor4_3(g8_load<0>(h, P, smem), g8_load<1>(h, P, smem), g8_load<2>(h, P, smem));
+  const uint4 t1 = xor4_3(g8_load<3>(h, P, smem), g8_load<4>(h, P, smem), g8_load<5>(h, P, smem));
+  const uint4 t2 = xor4_3(g8_load<6>(h, P, smem), g8_load<7>(h, P, smem), g8_load<8>(h, P, smem));
+  const uint4 t3 = xor4_3(g8_load<9>(h, P, smem), g8_load<10>(h, P, smem), g8_load<11>(h, P, smem));
+  const uint4 t4 = xor4_3(g8_load<12>(h, P, smem), g8_load<13>(h, P, smem), g8_load<14>(h, P, smem));
+  return xor4(xor4_3(t0, t1, t2), xor4_3(t3, t4, g8_load<15>(h, P, smem)));
+}
+
+// Role B: the (up to) 4 records of a wave with the bitsliced engine.
+// Eligible batches only (gcm_bs_eligible: uniform, 16-byte-multiple,
+// 16-byte-aligned records, no extra bytes, one key).
+template <int NR, bool OPEN>
+__device__ __forceinline__ void process_records_bs(const uint32_t *__restrict__ rkp,
                                                    const BatchDesc &b,
                                                    const RecState *__restrict__ st, uint64_t rec,
                                                    bool active, const uint8_t *smem,
-                                                   uint32_t mf0, bool report) {
-#if BSSL_AMD_BS_STAMPS
-  uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-  BS_STAMP(0);
-  static_assert(L == 8 || L == 16 || L == 32, "lanes per record");
-  const int q = threadIdx.x & (L - 1);
+                                                   const uint8_t *gtab, uint32_t mf0) {
+  const int q = threadIdx.x & 15;
   RecordMeta m = {0, 0, 0, 0, 0};
   RecState s;
   s.j0 = s.ek0 = s.ya = make_uint4(0, 0, 0, 0);
@@ -1233,182 +1242,184 @@ __device__ __forceinline__ void process_records_bs(const GcmKeyDev *__restrict__
     m = record_meta(b, rec);
     s = st[rec];
   }
+  m.xlen = 0;
   const bool live = active && s.live;
-  // Eligibility (host): uniform length, multiple of 16, 16-byte aligned
-  // records -- every block of a live record is a full aligned block.
-  const uint64_t nb = live ? m.len / 16 : 0;
+  const uint32_t nb = live ? (uint32_t)(m.len / 16) : 0u;  // nb < 2^32 (GCM length limit)
   const uint32_t ctr0 = bswap32(s.j0.w);
   const uint8_t *src = b.in + m.off;
   uint8_t *dst = b.out + m.off;
-  uint4 acc = (q == L - 1 && live) ? s.ya : make_uint4(0, 0, 0, 0);
-  const uint32_t lds_base = (uint32_t)reinterpret_cast<uintptr_t>(smem);
-  const uint32_t *rkp = &kp->rk_plain[0][0];
-  const int nchunks = wave_max((int)((nb + 32 * L - 1) / (32 * L)));
+  uint4 acc = (q == 15 && live) ? s.ya : make_uint4(0, 0, 0, 0);
+  const bool rs1 = (q >> 2) & 1, rs2 = (q >> 3) & 1;
+  const uint32_t rbs = (uint32_t)q & 3u;
+  uint32_t P[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) v |= (uint32_t)(((4 * k + i + q) & 15) << 4) << (8 * i);
+    P[k] = v;
+  }
+  uint32_t rk0[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) rk0[i] = (uint32_t)__builtin_amdgcn_readfirstlane(rkp[i]);
+  const int nchunks = wave_max((int)((nb + 511) / 512));
+  auto load_blk = [&](uint32_t j) {
+    return *reinterpret_cast<const uint4 *>(src + (uint64_t)(j < nb ? j : 0u) * 16);
+  };
 #pragma unroll 1
   for (int c = 0; c < nchunks; c++) {
-    const uint32_t jc = (uint32_t)(32 * L * c + q);
-    const uint32_t nb32 = (uint32_t)nb;
-    // Every lane of the wave live with all 32 chunk blocks present.
-    const bool full = __all(live && jc + L * 31 < nb32);
-    if (OPEN)
-      acc = full ? ghash_chunk<L, true>(acc, src, jc, nb32, lds_base, mf0)
-                 : ghash_chunk<L, false>(acc, src, jc, nb32, lds_base, mf0);
+    const uint32_t jc = 512u * (uint32_t)c + (uint32_t)q;
     uint32_t p[16][8];
     {
-      // Round 0 (AddRoundKey) of the counter blocks: words 0..2 are constant
-      // per record (bit masks), word 3 holds the 32 counters.
-      uint32_t w0 = s.j0.x ^ rkp[0], w1 = s.j0.y ^ rkp[1], w2 = s.j0.z ^ rkp[2];
-      // Rebuilt per chunk: hoisted out of the loop, the 96 masks would stay
-      // live (and spill) across the rounds.
-      asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2));
+      // Round 0: bytes 0..11 of every counter block are the record's J0
+      // (per-lane constants: all-0 / all-1 planes); word 3 holds the 32
+      // counters inc32(J0, 1 + j), transposed into planes.
+      uint32_t w0 = s.j0.x ^ rk0[0], w1 = s.j0.y ^ rk0[1], w2 = s.j0.z ^ rk0[2];
+      asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2));  // rebuilt per chunk, not hoisted
 #pragma unroll
       for (int k = 0; k < 32; k++) {
-        p[k / 8][k % 8] = 0u - ((w0 >> k) & 1u);
-        p[4 + k / 8][k % 8] = 0u - ((w1 >> k) & 1u);
-        p[8 + k / 8][k % 8] = 0u - ((w2 >> k) & 1u);
+        p[k / 8][k % 8] = bit_mask(w0, k);
+        p[4 + k / 8][k % 8] = bit_mask(w1, k);
+        p[8 + k / 8][k % 8] = bit_mask(w2, k);
       }
       const uint32_t cb = ctr0 + 1u + jc;  // inc32: mod 2^32
       uint32_t t[32];
 #pragma unroll
-      for (int n = 0; n < 32; n++) t[n] = bswap32(cb + (uint32_t)(L * n)) ^ rkp[3];
+      for (int n = 0; n < 32; n++) t[n] = bswap32(cb + 16u * (uint32_t)n) ^ rk0[3];
       bs_transpose32(t);
 #pragma unroll
       for (int k = 0; k < 32; k++) p[12 + k / 8][k % 8] = t[k];
     }
-    BS_STAMP(1);
-#pragma unroll 1
-    for (int r = 1; r < NR; r++) {
-      uint32_t w[4];
+    bs_cipher<NR>(p, rkp);
+    // The chunk's first input blocks are requested before the transposes.
+    uint4 xa[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++) w[i] = rkp[4 * r + i];
-      bs_round(p, w);
-    }
-    BS_STAMP(2);
-    // Last round one output column (= keystream word c of the 32 blocks) at
-    // a time, transposed back to blocks and applied to word c of each block
-    // with dword loads/stores: the keystream never needs 128 live VGPRs
-    // next to the GHASH state.  (Block indices fit 32 bits: nb < 2^32 by the
-    // GCM length limit.)
-    {
-      uint32_t w[4];
+    for (int i = 0; i < 4; i++) xa[i] = load_blk(jc + 16u * i);
+    const v32u K0 = bs_column_words(p, 0), K1 = bs_column_words(p, 1),
+               K2 = bs_column_words(p, 2), K3 = bs_column_words(p, 3);
+    // Blocks n = 0..31 in order: out = in ^ keystream, GHASH Horner step
+    // acc = acc * H^16 ^ C (C = the ciphertext: the output when sealing, the
+    // input when opening), inputs loaded 4 blocks ahead.
+#pragma unroll 1
+    for (int n0 = 0; n0 < 32; n0 += 4) {
+      uint4 xb[4];
+      if (n0 + 4 < 32) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) xb[i] = load_blk(jc + 16u * (uint32_t)(n0 + 4 + i));
+      }
 #pragma unroll
       for (int i = 0; i < 4; i++) {
-        w[i] = rkp[4 * NR + i];
-        asm volatile("" : "+s"(w[i]));  // masks are rebuilt per chunk, not hoisted
+        const int n = n0 + i;
+        const uint32_t j = jc + 16u * (uint32_t)n;
+        const uint4 ks = make_uint4(K0[n], K1[n], K2[n], K3[n]);
+        const uint4 y = xor4(xa[i], ks);
+        if (j < nb) *reinterpret_cast<uint4 *>(dst + (uint64_t)j * 16) = y;
+        const uint4 h = g8_mul(acc, rs1, rs2, rbs, P, smem);
+        if (j < nb) acc = xor4(h, OPEN ? xa[i] : y);
       }
 #pragma unroll
-      for (int col = 0; col < 4; col++) {
-        uint32_t t[32];
-        bs_last_round_col(p, w, col, t);
-        bs_transpose32(t);
-        if (full)
-          apply_keystream_word<L, true>(t, src, dst, jc, nb32, col);
-        else
-          apply_keystream_word<L, false>(t, src, dst, jc, nb32, col);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    // GHASH over the chunk's ciphertext blocks in order (OPEN: the input was
-    // hashed before it could be overwritten in place, see above).
-    BS_STAMP(3);
-    if (!OPEN) {
-      __builtin_amdgcn_s_waitcnt(0);  // this lane's stores before re-reading them
-      BS_STAMP(4);
-      acc = full ? ghash_chunk<L, true>(acc, dst, jc, nb32, lds_base, mf0)
-                 : ghash_chunk<L, false>(acc, dst, jc, nb32, lds_base, mf0);
+      for (int i = 0; i < 4; i++) xa[i] = xb[i];
     }
   }
-  BS_STAMP(5);
-  finish_record<OPEN, L>(acc, nb, m, s, b, rec, active, live, dst, smem + kLdsGhash, mf0);
-  BS_STAMP(6);
-#if BSSL_AMD_BS_STAMPS
-  if (report && (threadIdx.x & 63) == 0)
-    printf("bs-stamps wave %d: ctr %llu rounds %llu cols %llu wait %llu ghash %llu finish %llu total %llu\n",
-           (int)(threadIdx.x >> 6), (unsigned long long)(ts[1] - ts[0]), (unsigned long long)(ts[2] - ts[1]),
-           (unsigned long long)(ts[3] - ts[2]), (unsigned long long)(ts[4] - ts[3]),
-           (unsigned long long)(ts[5] - ts[4]), (unsigned long long)(ts[6] - ts[5]),
-           (unsigned long long)(ts[6] - ts[0]));
-#else
-  (void)report;
-#endif
+  finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, gtab, mf0);
 }
 
-template <int NR, bool OPEN, int L>
+// Bitsliced-only kernel (BSSL_AMD_GCM_MODE=bs): 8 waves, one workgroup per
+// CU, every wave role B; one key.
+constexpr int kBsThreads = 512;
+
+template <int NR, bool OPEN>
 __global__ __launch_bounds__(kBsThreads, 2) void gcm_bs_kernel(const GcmKeyDev *__restrict__ keys,
                                                               BatchDesc b,
-                                                              const RecState *__restrict__ st) {
-  constexpr int kRecPerWaveBs = 64 / L;
-  constexpr int kTile = kBsWaves * kRecPerWaveBs;
-  static_assert(kTile <= 64, "one wave plans a tile with ballots");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kBsLdsBytes];
-  __shared__ uint32_t s_pass_key[kTile];
-  __shared__ uint64_t s_pass_mask[kTile];
-  __shared__ int s_npass;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const uint32_t mf0 = 0xf0u;
-  uint32_t loaded = 0xffffffffu;
+                                                              const RecState *__restrict__ st,
+                                                              uint32_t *__restrict__ units) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kG8Bytes];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
+  build_g8<kBsThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab[4]), tid);
+  __syncthreads();
+  const uint32_t *rkp = &keys[0].rk_plain[0][0];
+  const uint8_t *gtab = reinterpret_cast<const uint8_t *>(keys[0].htab);
   const uint64_t n = b.num_records;
-  for (uint64_t base = (uint64_t)blockIdx.x * kTile; base < n;
-       base += (uint64_t)gridDim.x * kTile) {
-    __syncthreads();
-    if (wave == 0) {
-      const uint64_t i = base + lane;
-      uint32_t k = (lane < kTile && i < n) ? (b.key_index ? b.key_index[rec_at(b, i)] : 0u)
-                                           : 0xffffffffu;
-      if (k != 0xffffffffu && k >= b.num_keys) k = 0;  // flagged dead by the prologue
-      uint64_t pending = __ballot(k != 0xffffffffu);
-      int np = 0;
-      while (pending) {
-        const uint32_t kk = __shfl(k, __builtin_ctzll(pending), 64);
-        const uint64_t mask = __ballot(k == kk) & pending;
-        if (lane == 0) {
-          s_pass_key[np] = kk;
-          s_pass_mask[np] = mask;
-        }
-        pending &= ~mask;
-        np++;
-      }
-      if (lane == 0) s_npass = np;
-    }
-    __syncthreads();
-    const int npass = s_npass;
-    for (int pi = 0; pi < npass; pi++) {
-      const uint32_t k = __builtin_amdgcn_readfirstlane(s_pass_key[pi]);
-      const uint64_t mask = s_pass_mask[pi];
-      if (k != loaded) {
-        __syncthreads();
-        const uint4 *srcp = reinterpret_cast<const uint4 *>(keys[k].htab);
-        for (uint32_t e = tid; e < kBsLdsBytes / 16; e += kBsThreads)
-          reinterpret_cast<uint4 *>(smem + kLdsGhash)[e] = srcp[e];
-        __syncthreads();
-        loaded = k;
-      }
-      const int t = wave * kRecPerWaveBs + lane / L;
-      const bool active = (mask >> t) & 1;
-      process_records_bs<NR, OPEN, L>(keys + k, b, st, active ? rec_at(b, base + t) : 0, active,
-                                      smem, mf0,
-                                      blockIdx.x == 0 && base / ((uint64_t)gridDim.x * kTile) == 20);
-    }
+  for (;;) {
+    uint32_t u = 0;
+    if (lane == 0) u = atomicAdd(units, 1u);
+    u = __builtin_amdgcn_readfirstlane(__shfl(u, 0, 64));
+    const uint64_t first = (uint64_t)u * kRecPerWave;
+    if (first >= n) break;
+    const uint64_t i = first + g;
+    const bool active = i < n;
+    process_records_bs<NR, OPEN>(rkp, b, st, active ? rec_at(b, i) : 0, active, smem, gtab, 0xf0u);
+  }
+}
+
+// Hybrid kernel (BSSL_AMD_GCM_MODE=hybrid): 8 waves per CU, two per SIMD;
+// the first four (one per SIMD) are role A -- the T-table engine of
+// process_records, which keeps the LDS busy and uses under half of the
+// VALU -- and the other four role B, the bitsliced engine, which needs only
+// the VALU.  Both take units of 4 records from the same counter, so the
+// split follows whatever each role sustains; both read the same GHASH byte
+// table.  One key.
+template <int NR, bool OPEN>
+__global__ __launch_bounds__(512, 2) void gcm_hy_kernel(const GcmKeyDev *__restrict__ keys,
+                                                       BatchDesc b,
+                                                       const RecState *__restrict__ st,
+                                                       uint32_t *__restrict__ units) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsPlan];
+  constexpr int kThreads = 512;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  for (int e = tid; e < 256 * 64; e += kThreads) {
+    const int idx = e >> 6, slot = (e >> 5) & 1;
+    const uint32_t v = kTables.te0[idx];
+    reinterpret_cast<uint32_t *>(smem + kLdsAes)[e] = slot ? rotl(v, 8) : v;
+  }
+  build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab[4]), tid);
+  __syncthreads();
+  const uint8_t *gtab = reinterpret_cast<const uint8_t *>(keys[0].htab);
+  const uint64_t n = b.num_records;
+  const bool role_b = wave >= 4;
+  if (!role_b) __builtin_amdgcn_s_setprio(1);  // the LDS feeder wins VALU arbitration
+  RoundKeys rk;
+  if (!role_b) {
+#pragma unroll
+    for (int r = 0; r <= NR; r++)
+#pragma unroll
+      for (int c = 0; c < 4; c++) rk.w[r][c] = keys[0].rk[r][c];
+  }
+  const uint32_t lc0 = kLdsAes + (uint32_t)(lane & 31) * 4u, lc1 = lc0 + 128u;
+  StampVec stamps = {{0, 0, 0}};
+  for (;;) {
+    uint32_t u = 0;
+    if (lane == 0) u = atomicAdd(units, 1u);
+    u = __builtin_amdgcn_readfirstlane(__shfl(u, 0, 64));
+    const uint64_t first = (uint64_t)u * kRecPerWave;
+    if (first >= n) break;
+    const uint64_t i = first + g;
+    const bool active = i < n;
+    if (role_b)
+      process_records_bs<NR, OPEN>(&keys[0].rk_plain[0][0], b, st, active ? rec_at(b, i) : 0,
+                                   active, smem, gtab, 0xf0u);
+    else
+      process_records<NR, OPEN, false>(rk, b, st, active ? rec_at(b, i) : 0, active, smem, gtab,
+                                       lc0, lc1, 0xf0u, stamps);
   }
 }
 
 int g_num_cus = 0;
 
-// Lanes per record for the bitsliced kernel, or 0 for the T-table kernel:
-// uniform-length batches of 16-byte-multiple, 16-byte-aligned records long
-// enough to fill 32 blocks per lane.  Opt-in (BSSL_AMD_GCM_BS=1) until it
-// outruns the T-table kernel (DESIGN.md §4.2b has the measurements).
-int bs_lanes(const BatchDesc &b) {
-  const char *e = getenv("BSSL_AMD_GCM_BS");
-  const int enabled = e ? atoi(e) : 0;
-  if (!enabled || b.lengths || b.offsets || b.extra_len || b.tag_stride) return 0;
+// 0 = T-table kernel, 1 = bitsliced-only, 2 = hybrid (BSSL_AMD_GCM_MODE =
+// table | bs | hybrid) for batches the bitsliced engine takes: uniform,
+// 16-byte-multiple, 16-byte-aligned records of >= 4 KiB, one key, no extra
+// bytes.
+int gcm_mode(const BatchDesc &b) {
+  const char *e = getenv("BSSL_AMD_GCM_MODE");
+  int mode = 0;
+  if (e && !strcmp(e, "bs")) mode = 1;
+  if (e && !strcmp(e, "hybrid")) mode = 2;
+  if (!mode || b.lengths || b.offsets || b.extra_len || b.tag_stride || b.key_index) return 0;
   if ((b.record_len | b.record_stride | reinterpret_cast<uintptr_t>(b.in) |
        reinterpret_cast<uintptr_t>(b.out)) & 15)
     return 0;
-  const uint64_t nb = b.record_len / 16;
-  return nb >= 1024 ? 32 : 0;
+  return b.record_len >= 4096 ? mode : 0;
 }
 
 template <int NR, bool OPEN>
@@ -1421,7 +1432,7 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
       return 1;
   }
   // Per-record state plus one extra entry whose first word is the unit
-  // counter of gcm_kernel's one-key mode.
+  // counter of the one-key kernels.
   RecState *st = nullptr;
   if (hipMallocAsync(reinterpret_cast<void **>(&st), (b.num_records + 1) * sizeof(RecState), s) !=
       hipSuccess)
@@ -1449,23 +1460,28 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
     }
     bo.order = order;
   }
-  const int L = bs_lanes(b);
+  const int mode = gcm_mode(b);
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
-  if (L) {
-    const uint64_t tiles = (b.num_records + kBsWaves * (64 / L) - 1) / (kBsWaves * (64 / L));
-    const uint64_t slots = 2ull * (uint64_t)g_num_cus;  // 2 workgroups per CU
-    const unsigned grid = (unsigned)(tiles < slots ? tiles : slots);
-    const RecState *cst = st;
-    hipLaunchKernelGGL((gcm_bs_kernel<NR, OPEN, 32>), dim3(grid), dim3(kBsThreads), 0, s, keys, bo, cst);
+  const RecState *cst = st;
+  if (mode) {
+    const uint64_t units_needed = (b.num_records + 4 * 8 - 1) / (4 * 8);
+    const unsigned grid = (unsigned)(units_needed < (uint64_t)g_num_cus ? units_needed
+                                                                       : (uint64_t)g_num_cus);
+    if (mode == 1)
+      hipLaunchKernelGGL((gcm_bs_kernel<NR, OPEN>), dim3(grid), dim3(kBsThreads), 0, s, keys, bo,
+                         cst, units);
+    else
+      hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN>), dim3(grid), dim3(512), 0, s, keys, bo, cst,
+                         units);
   } else {
-    const uint64_t tiles = (b.num_records + kRecPerTile - 1) / kRecPerTile;
+    const uint64_t tiles = (b.num_records + kWaves * kRecPerWave - 1) / (kWaves * kRecPerWave);
     const unsigned grid = (unsigned)(tiles < (uint64_t)g_num_cus ? tiles : (uint64_t)g_num_cus);
     if (b.extra_len)
-      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, true>), dim3(grid), dim3(kThreads), 0, s, keys, bo,
-                         (const RecState *)st, units);
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, true, kWaves>), dim3(grid), dim3(kWaves * 64), 0, s,
+                         keys, bo, cst, units);
     else
-      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false>), dim3(grid), dim3(kThreads), 0, s, keys, bo,
-                         (const RecState *)st, units);
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves>), dim3(grid), dim3(kWaves * 64), 0, s,
+                         keys, bo, cst, units);
   }
   int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);

@@ -230,14 +230,17 @@ def test_batch_large_ragged_reordered(aead, multikey):
     assert st.all() and back == ins
 
 
-@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm"])
-@pytest.mark.parametrize("rlen", [16384, 17408, 32768])
-def test_bitsliced_gcm_path(aead, rlen, monkeypatch):
-    """The opt-in bitsliced kernel (BSSL_AMD_GCM_BS=1; uniform, 16-byte
-    multiple records of >= 1024 blocks: full and partial 32-block chunks)."""
-    monkeypatch.setenv("BSSL_AMD_GCM_BS", "1")
-    rng = np.random.default_rng(rlen)
-    n = 24
+@pytest.mark.parametrize("mode", ["bs", "hybrid"])
+@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-192-gcm", "aes-256-gcm"])
+@pytest.mark.parametrize("rlen", [4096, 16384, 17408, 32768])
+def test_bitsliced_gcm_path(aead, rlen, mode, monkeypatch):
+    """The bitsliced engine (BSSL_AMD_GCM_MODE=bs: every wave; =hybrid: half
+    the waves, beside the T-table engine) on uniform, 16-byte-multiple
+    records: full and partial 512-block chunks, seal and open (tags verified,
+    one tampered record)."""
+    monkeypatch.setenv("BSSL_AMD_GCM_MODE", mode)
+    rng = np.random.default_rng(rlen + len(mode))
+    n = 50
     key = rng.integers(0, 256, size=AEAD_KEYLEN[aead], dtype=np.uint8).tobytes()
     pt = rng.integers(0, 256, size=n * rlen, dtype=np.uint8)
     nonces = rng.integers(0, 256, size=n * 12, dtype=np.uint8)
@@ -257,11 +260,17 @@ def test_bitsliced_gcm_path(aead, rlen, monkeypatch):
                           pt[rlen * i:rlen * (i + 1)].tobytes(), ad[13 * i:13 * i + 13].tobytes())
         assert ok and ct[rlen * i:rlen * (i + 1)].tobytes() == c and tg[16 * i:16 * i + 16].tobytes() == t, i
     d_back = torch.zeros_like(d_pt)
-    b2 = ba.make_batch(n, d_ct, d_back, d_tags, _t(nonces), 12, _t(ad), record_stride=rlen,
+    bad_tags = d_tags.clone()
+    bad_tags[16 * 7] ^= 1
+    b2 = ba.make_batch(n, d_ct, d_back, bad_tags, _t(nonces), 12, _t(ad), record_stride=rlen,
                        record_len=rlen, ad_stride=13, ad_len=13, status=d_st)
     ctx.open_batch_device(b2)
     torch.cuda.synchronize()
-    assert bool(d_st.all()) and torch.equal(d_back, d_pt)
+    stv = d_st.cpu().numpy()
+    assert stv[7] == 0 and stv.sum() == n - 1
+    back = d_back.cpu().numpy()
+    assert not back[7 * rlen:8 * rlen].any()
+    assert np.array_equal(np.delete(back.reshape(n, rlen), 7, 0), np.delete(pt.reshape(n, rlen), 7, 0))
 
 
 def test_batch_gcm_nonce_lengths_and_truncated_tags():
