@@ -1154,6 +1154,13 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
 // instruction cache it shares with the T-table role (gcm_hy_kernel).
 typedef uint32_t v32u __attribute__((ext_vector_type(32)));
 
+// Diagnostic ablations of the bitsliced engine (csrc/Makefile `bsablate`;
+// never in the shipped library): 1 = no GHASH step, 2 = no AES rounds,
+// 3 = no output stores, 4 = no record-end tree/tag (finish_record).
+#ifndef BSSL_AMD_BS_ABLATE
+#define BSSL_AMD_BS_ABLATE 0
+#endif
+
 // 0 or 0xffffffff: bit `k` of w (v_bfe_i32 / s_bfe_i32).
 __device__ __forceinline__ uint32_t bit_mask(uint32_t w, int k) {
   return (uint32_t)(((int32_t)(w << (31 - k))) >> 31);
@@ -1196,6 +1203,37 @@ __device__ __forceinline__ void bs_cipher(uint32_t (&p)[16][8], const uint32_t *
   }
 }
 
+// 32x32 bit transpose (the swap-move network of bs_transpose32): the 16- and
+// 8-bit stages are byte permutations (one v_perm_b32 per output word), the
+// 4/2/1-bit stages one shift plus one v_bitop3 bit-select per output word.
+template <int S>
+__device__ __forceinline__ void tr_stage(uint32_t m[32]) {
+  constexpr uint32_t kLo = S == 4 ? 0x0f0f0f0fu : S == 2 ? 0x33333333u : 0x55555555u;
+#pragma unroll
+  for (int k = 0; k < 32; k++) {
+    if (k & S) continue;
+    const uint32_t a = m[k], b = m[k + S];
+    if constexpr (S == 16) {
+      m[k] = __builtin_amdgcn_perm(b, a, 0x05040100u);
+      m[k + S] = __builtin_amdgcn_perm(b, a, 0x07060302u);
+    } else if constexpr (S == 8) {
+      m[k] = __builtin_amdgcn_perm(b, a, 0x06020400u);
+      m[k + S] = __builtin_amdgcn_perm(b, a, 0x07030501u);
+    } else {
+      m[k] = (a & kLo) | ((b << S) & ~kLo);
+      m[k + S] = (b & ~kLo) | ((a >> S) & kLo);
+    }
+  }
+}
+
+__device__ __forceinline__ void transpose32_fast(uint32_t m[32]) {
+  tr_stage<16>(m);
+  tr_stage<8>(m);
+  tr_stage<4>(m);
+  tr_stage<2>(m);
+  tr_stage<1>(m);
+}
+
 // Keystream word c of the lane's 32 blocks (after the last round p[4c+row]
 // holds row `row` of output column c).
 __device__ __forceinline__ v32u bs_column_words(const uint32_t (&p)[16][8], int c) {
@@ -1204,7 +1242,7 @@ __device__ __forceinline__ v32u bs_column_words(const uint32_t (&p)[16][8], int 
   for (int row = 0; row < 4; row++)
 #pragma unroll
     for (int k = 0; k < 8; k++) o[8 * row + k] = p[4 * c + row][k];
-  bs_transpose32(o);
+  transpose32_fast(o);
   v32u v;
 #pragma unroll
   for (int n = 0; n < 32; n++) v[n] = o[n];
@@ -1286,42 +1324,71 @@ __device__ __forceinline__ void process_records_bs(const uint32_t *__restrict__ 
       uint32_t t[32];
 #pragma unroll
       for (int n = 0; n < 32; n++) t[n] = bswap32(cb + 16u * (uint32_t)n) ^ rk0[3];
-      bs_transpose32(t);
+      transpose32_fast(t);
 #pragma unroll
       for (int k = 0; k < 32; k++) p[12 + k / 8][k % 8] = t[k];
     }
+#if BSSL_AMD_BS_ABLATE != 2
     bs_cipher<NR>(p, rkp);
+#endif
     // The chunk's first input blocks are requested before the transposes.
-    uint4 xa[4];
+    uint4 xa[4], xb[4];
 #pragma unroll
-    for (int i = 0; i < 4; i++) xa[i] = load_blk(jc + 16u * i);
-    const v32u K0 = bs_column_words(p, 0), K1 = bs_column_words(p, 1),
-               K2 = bs_column_words(p, 2), K3 = bs_column_words(p, 3);
-    // Blocks n = 0..31 in order: out = in ^ keystream, GHASH Horner step
-    // acc = acc * H^16 ^ C (C = the ciphertext: the output when sealing, the
-    // input when opening), inputs loaded 4 blocks ahead.
+    for (int i = 0; i < 4; i++) {
+      xa[i] = load_blk(jc + 16u * i);
+      xb[i] = load_blk(jc + 16u * (4 + i));
+    }
+    v32u K0 = bs_column_words(p, 0), K1 = bs_column_words(p, 1), K2 = bs_column_words(p, 2),
+         K3 = bs_column_words(p, 3);
+    // Pass 1 (memory): out = in ^ keystream for blocks n = 0..31, inputs
+    // loaded 8 blocks ahead; the ciphertext of block n (the output when
+    // sealing, the input when opening) replaces its keystream in K.
 #pragma unroll 1
     for (int n0 = 0; n0 < 32; n0 += 4) {
-      uint4 xb[4];
-      if (n0 + 4 < 32) {
+      uint4 xc[4];  // (past the chunk: a clamped, in-bounds load whose value is unused)
 #pragma unroll
-        for (int i = 0; i < 4; i++) xb[i] = load_blk(jc + 16u * (uint32_t)(n0 + 4 + i));
-      }
+      for (int i = 0; i < 4; i++) xc[i] = load_blk(jc + 16u * (uint32_t)(n0 + 8 + i));
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         const int n = n0 + i;
         const uint32_t j = jc + 16u * (uint32_t)n;
-        const uint4 ks = make_uint4(K0[n], K1[n], K2[n], K3[n]);
-        const uint4 y = xor4(xa[i], ks);
+        const uint4 y = xor4(xa[i], make_uint4(K0[n], K1[n], K2[n], K3[n]));
+#if BSSL_AMD_BS_ABLATE == 3
+        if (j < nb) asm volatile("" ::"v"(y.x), "v"(y.y), "v"(y.z), "v"(y.w));
+#else
         if (j < nb) *reinterpret_cast<uint4 *>(dst + (uint64_t)j * 16) = y;
-        const uint4 h = g8_mul(acc, rs1, rs2, rbs, P, smem);
-        if (j < nb) acc = xor4(h, OPEN ? xa[i] : y);
+#endif
+        const uint4 cb = OPEN ? xa[i] : y;
+        K0[n] = cb.x;
+        K1[n] = cb.y;
+        K2[n] = cb.z;
+        K3[n] = cb.w;
       }
 #pragma unroll
-      for (int i = 0; i < 4; i++) xa[i] = xb[i];
+      for (int i = 0; i < 4; i++) {
+        xa[i] = xb[i];
+        xb[i] = xc[i];
+      }
+    }
+    // Pass 2 (LDS): the GHASH chain acc = acc * H^16 ^ C over the lane's
+    // valid blocks of the chunk.
+    const int nv = (int)min(32u, jc < nb ? (nb - jc + 15u) / 16u : 0u);
+#pragma unroll 1
+    for (int n = 0; n < 32; n++) {
+#if BSSL_AMD_BS_ABLATE == 1
+      const uint4 h = acc;
+#else
+      const uint4 h = g8_mul(acc, rs1, rs2, rbs, P, smem);
+#endif
+      if (n < nv) acc = xor4(h, make_uint4(K0[n], K1[n], K2[n], K3[n]));
     }
   }
+#if BSSL_AMD_BS_ABLATE == 4
+  if (active && q == 0 && b.status) b.status[rec] = live;
+  asm volatile("" ::"v"(acc.x), "v"(acc.y), "v"(acc.z), "v"(acc.w));
+#else
   finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, gtab, mf0);
+#endif
 }
 
 // Bitsliced-only kernel (BSSL_AMD_GCM_MODE=bs): 8 waves, one workgroup per
@@ -1333,12 +1400,16 @@ __global__ __launch_bounds__(kBsThreads, 2) void gcm_bs_kernel(const GcmKeyDev *
                                                               BatchDesc b,
                                                               const RecState *__restrict__ st,
                                                               uint32_t *__restrict__ units) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kG8Bytes];
+  // [0, 64 KiB) the GHASH byte table of H^16; then the nibble tables of
+  // H, H^2, H^4, H^8 for the record-end tree (32 KiB).
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kG8Bytes + 4 * 8192];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   build_g8<kBsThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab[4]), tid);
+  for (int e = tid; e < 4 * 8192 / 16; e += kBsThreads)
+    reinterpret_cast<uint4 *>(smem + kG8Bytes)[e] = reinterpret_cast<const uint4 *>(keys[0].htab)[e];
   __syncthreads();
   const uint32_t *rkp = &keys[0].rk_plain[0][0];
-  const uint8_t *gtab = reinterpret_cast<const uint8_t *>(keys[0].htab);
+  const uint8_t *gtab = smem + kG8Bytes;
   const uint64_t n = b.num_records;
   for (;;) {
     uint32_t u = 0;
@@ -1405,6 +1476,7 @@ __global__ __launch_bounds__(512, 2) void gcm_hy_kernel(const GcmKeyDev *__restr
 }
 
 int g_num_cus = 0;
+
 
 // 0 = T-table kernel, 1 = bitsliced-only, 2 = hybrid (BSSL_AMD_GCM_MODE =
 // table | bs | hybrid) for batches the bitsliced engine takes: uniform,
