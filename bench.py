@@ -103,18 +103,26 @@ def mixed_lengths(first, n):
     return np.uint64(64) + z % np.uint64(16321)
 
 
-def _pad16(lens):
-    return (lens + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+def _pad16(lens, align=16):
+    a = np.uint64(align)
+    return (lens + a - np.uint64(1)) // a * a
+
+
+# Record alignment of the batch layout (bytes; BSSL_AMD_ALIGN overrides).
+# 128-byte-aligned config 3 records (no two records on one cache line)
+# measured the same speed and write traffic as the packed 16-byte layout.
+def record_align(config):
+    return int(os.environ.get("BSSL_AMD_ALIGN", 16))
 
 
 class Shard:
     """Records [first, first + n) of the global record sequence on one rank.
     `lens`/`offs` describe the rank's packed batch (16-byte-aligned records)."""
 
-    def __init__(self, first, lens, key_first=0, nkeys=0):
+    def __init__(self, first, lens, key_first=0, nkeys=0, align=16):
         self.first = int(first)
         self.lens = lens
-        padded = _pad16(lens)
+        padded = _pad16(lens, align)
         self.offs = np.zeros(len(lens), dtype=np.uint64)
         if len(lens):
             self.offs[1:] = np.cumsum(padded[:-1])
@@ -152,7 +160,7 @@ def shard_plan(config, rank, world, records=0):
         first = rank * nrec
         lens = mixed_lengths(first, nrec) if length == "mixed" else np.full(nrec, length,
                                                                             np.uint64)
-        return Shard(first, lens)
+        return Shard(first, lens, align=record_align(config))
     if config in RECORDS_PER_KEY:
         rpk = RECORDS_PER_KEY[config]
         nkeys_total = nrec // rpk
@@ -418,7 +426,7 @@ def main():
     aead, key_len, _, length, scaling, desc = CONFIGS[args.config]
     sh = shard_plan(args.config, rank, world, args.records)
     first, lens, offs, nrec = sh.first, sh.lens, sh.offs, sh.n
-    padded = _pad16(lens)
+    padded = _pad16(lens, record_align(args.config))
     pt_bytes = int(lens.sum())
 
     d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)

@@ -207,6 +207,42 @@ __device__ __forceinline__ uint32_t load_le32_bytes(const uint8_t *p, uint64_t a
   return v;
 }
 
+// Bytes [p, p + n) (n <= 16) as 4 little-endian words, zero past n, read
+// with aligned dword loads: only dwords that hold at least one of the bytes
+// are read (they lie in the same pages as those bytes), then funnel-shifted.
+__device__ __forceinline__ void load16_partial(const uint8_t *p, uint32_t n, uint32_t w[4]) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t *base = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t nd = n ? (sh + n + 3) / 4 : 0u;  // dwords touched
+  uint32_t d[5];
+#pragma unroll
+  for (int k = 0; k < 5; k++) d[k] = (uint32_t)k < nd ? base[k] : 0u;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t v = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+    const uint32_t mask = n >= 4u * i + 4 ? 0xffffffffu
+                          : n <= 4u * i   ? 0u
+                                          : ((1u << (8 * (n - 4 * i))) - 1u);
+    w[i] = v & mask;
+  }
+}
+
+// Stores bytes [0, n) of the words y[] to p, which is 4-byte aligned: whole
+// dwords, then one short and/or one byte (no byte-per-lane store loops).
+__device__ __forceinline__ void store_words_partial(uint8_t *p, const uint32_t *y, uint32_t n) {
+  uint32_t *pw = reinterpret_cast<uint32_t *>(p);
+  const uint32_t nw = n / 4;
+  for (uint32_t i = 0; i < nw; i++) pw[i] = y[i];
+  const uint32_t r = n & 3;
+  if (r) {
+    const uint32_t last = y[nw];
+    uint8_t *q = p + 4 * nw;
+    if (r & 2) *reinterpret_cast<uint16_t *>(q) = (uint16_t)last;
+    if (r & 1) q[r & 2] = (uint8_t)(last >> (8 * (r & 2)));
+  }
+}
+
 // Final reduction and tag: (h mod p + s) mod 2^128 (poly1305.cc:255-313).
 __device__ void poly_finish(P h, const uint32_t s[4], uint32_t tag[4]) {
   uint32_t c;
@@ -417,12 +453,8 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   {
     const uint8_t *ad = b.ad + (live ? m.ad_off : 0);
     const uint64_t k = (uint64_t)q;
-    if (live && 16 * k < m.ad_len) {
-      const uint64_t avail = m.ad_len - 16 * k;
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-        adw[i] = load_le32_bytes(ad + 16 * k + 4 * i, avail > 4u * i ? avail - 4u * i : 0);
-    }
+    if (live && 16 * k < m.ad_len)
+      load16_partial(ad + 16 * k, (uint32_t)min<uint64_t>(m.ad_len - 16 * k, 16), adw);
   }
   // Message = the record's `in` bytes then b.extra_len extra bytes
   // (BatchDesc::extra, the TLS 1.3 inner type), whose ciphertext goes to
@@ -478,6 +510,25 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
 #pragma unroll
       for (int i = 0; i < 4; i++)
         dp[i] = make_uint4(y[4 * i], y[4 * i + 1], y[4 * i + 2], y[4 * i + 3]);
+    } else if (!XT && aligned) {
+      // The record's last, partial block: aligned dword loads (only dwords
+      // holding record bytes), dword / short / byte stores.
+      const uint8_t *sp = src + 64 * d;
+      uint8_t *dp = dst + 64 * d;
+      const uint32_t n = (uint32_t)min<uint64_t>(rem, 64);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t nk = n > 16u * k ? min(n - 16u * k, 16u) : 0u;
+        load16_partial(sp + 16 * k, nk, x + 4 * k);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        const uint32_t mask = n >= 4u * i + 4 ? 0xffffffffu
+                              : n <= 4u * i   ? 0u
+                                              : ((1u << (8 * (n - 4 * i))) - 1u);
+        y[i] = (x[i] ^ ks[i]) & mask;
+      }
+      store_words_partial(dp, y, n);
     } else if (!XT) {
       const uint8_t *sp = src + 64 * d;
       uint8_t *dp = dst + 64 * d;
@@ -688,9 +739,16 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
       ok = diff == 0;  // CRYPTO_memcmp, e_chacha20poly1305.cc:322-326
     }
     if (active) {
-      if (!OPEN)
-        for (uint32_t i = 0; i < b.tag_len; i++)
-          tagp[i] = ok ? (uint8_t)(tag[i >> 2] >> (8 * (i & 3))) : 0;
+      if (!OPEN) {
+        const uint32_t tw[4] = {ok ? tag[0] : 0u, ok ? tag[1] : 0u, ok ? tag[2] : 0u,
+                                ok ? tag[3] : 0u};
+        if (b.tag_len == 16 && (reinterpret_cast<uintptr_t>(tagp) & 15) == 0)
+          *reinterpret_cast<uint4 *>(tagp) = make_uint4(tw[0], tw[1], tw[2], tw[3]);
+        else if ((reinterpret_cast<uintptr_t>(tagp) & 3) == 0)
+          store_words_partial(tagp, tw, b.tag_len);
+        else
+          for (uint32_t i = 0; i < b.tag_len; i++) tagp[i] = (uint8_t)(tw[i >> 2] >> (8 * (i & 3)));
+      }
       if (b.status) b.status[rec] = ok ? 1 : 0;
     }
   }
