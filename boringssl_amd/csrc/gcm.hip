@@ -571,15 +571,54 @@ __device__ __forceinline__ uint4 shfl_down4(uint4 v, int d, int width) {
 
 // ---------------------------------------------------------------------------
 // Record buffers.
+// Bytes [p, p + n) (n <= 16), zero past n, with aligned dword loads: only
+// dwords holding at least one of the bytes are read (they lie in the same
+// pages as those bytes), then funnel-shifted.  (Byte loads cost one memory
+// request per byte.)
 __device__ __forceinline__ uint4 load_partial(const uint8_t *p, uint32_t n) {
-  uint32_t w[4] = {0, 0, 0, 0};
-  for (uint32_t i = 0; i < n; i++) w[i >> 2] |= (uint32_t)p[i] << (8 * (i & 3));
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t *base = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t nd = n ? (sh + n + 3) / 4 : 0u;  // dwords touched
+  uint32_t d[5];
+#pragma unroll
+  for (int k = 0; k < 5; k++) d[k] = (uint32_t)k < nd ? base[k] : 0u;
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t v = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+    const uint32_t lo = 4u * i;
+    w[i] = v & ((n >= lo + 4) ? 0xffffffffu : (n <= lo) ? 0u : ((1u << (8 * (n - lo))) - 1u));
+  }
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// Bytes [0, n) of v to p: one 16-byte store for a whole aligned block,
+// dword (+ short / byte) stores when p is 4-byte aligned, else bytes.
+// (Each narrow store is a memory request of its own; a record's tag and
+// tail otherwise cost up to 31 of them.)
 __device__ __forceinline__ void store_partial(uint8_t *p, uint4 v, uint32_t n) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  for (uint32_t i = 0; i < n; i++) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  if (n >= 16 && (a & 15) == 0) {
+    *reinterpret_cast<uint4 *>(p) = v;
+  } else if ((a & 3) == 0) {
+    uint32_t *pw = reinterpret_cast<uint32_t *>(p);
+    uint32_t last = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (4u * i + 4 <= n) pw[i] = w[i];
+      if (n / 4 == (uint32_t)i) last = w[i];
+    }
+    const uint32_t r = n & 3;
+    if (r) {
+      uint8_t *q = p + (n & ~3u);
+      if (r & 2) *reinterpret_cast<uint16_t *>(q) = (uint16_t)last;
+      if (r & 1) q[r & 2] = (uint8_t)(last >> (8 * (r & 2)));
+    }
+  } else {
+    for (uint32_t i = 0; i < n; i++) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+  }
 }
 
 __device__ __forceinline__ uint4 mask_block(uint4 v, uint32_t n) {
@@ -785,12 +824,7 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
       ok = diff == 0;  // CRYPTO_memcmp, e_aes.cc.inc:860-864
     }
     if (active) {
-      if (!OPEN) {
-        if (ok)
-          store_partial(tagp, tag, b.tag_len);
-        else
-          for (uint32_t i = 0; i < b.tag_len; i++) tagp[i] = 0;
-      }
+      if (!OPEN) store_partial(tagp, ok ? tag : make_uint4(0, 0, 0, 0), b.tag_len);
       if (b.status) b.status[rec] = ok ? 1 : 0;
     }
   }
