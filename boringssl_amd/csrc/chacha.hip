@@ -68,15 +68,22 @@ struct ChaState {
   a += b; d = rotl(d ^ a, 8);          \
   c += d; b = rotl(b ^ c, 7);
 
-__device__ __forceinline__ void chacha_block(const uint32_t key[8], uint32_t ctr,
-                                             const uint32_t nonce[3], uint32_t out[16]) {
+// Opaque copy of the key words: otherwise hipcc hoists the key-only first
+// steps of the column round out of the block loop and keeps them live
+// (registers).
+__device__ __forceinline__ void launder_key(const uint32_t key[8], uint32_t k[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) k[i] = key[i];
+  asm volatile("" : "+v"(k[0]), "+v"(k[1]), "+v"(k[2]), "+v"(k[3]), "+v"(k[4]), "+v"(k[5]),
+               "+v"(k[6]), "+v"(k[7]));
+}
+
+// The ChaCha20 block function over an already laundered key.
+__device__ __forceinline__ void chacha_block_raw(const uint32_t key[8], uint32_t ctr,
+                                                 const uint32_t nonce[3], uint32_t out[16]) {
   uint32_t x0 = 0x61707865, x1 = 0x3320646e, x2 = 0x79622d32, x3 = 0x6b206574;
   uint32_t x4 = key[0], x5 = key[1], x6 = key[2], x7 = key[3];
   uint32_t x8 = key[4], x9 = key[5], x10 = key[6], x11 = key[7];
-  // Opaque copies: otherwise hipcc hoists the key-only first steps of the
-  // column round out of the block loop and keeps them live (registers).
-  asm volatile("" : "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7), "+v"(x8), "+v"(x9), "+v"(x10),
-               "+v"(x11));
   uint32_t x12 = ctr, x13 = nonce[0], x14 = nonce[1], x15 = nonce[2];
   CHACHA_PRAGMA(unroll BSSL_AMD_CHACHA_UNROLL)
   for (int i = 0; i < 10; i++) {
@@ -99,6 +106,13 @@ __device__ __forceinline__ void chacha_block(const uint32_t key[8], uint32_t ctr
   out[13] = x13 + nonce[0];
   out[14] = x14 + nonce[1];
   out[15] = x15 + nonce[2];
+}
+
+__device__ __forceinline__ void chacha_block(const uint32_t key[8], uint32_t ctr,
+                                             const uint32_t nonce[3], uint32_t out[16]) {
+  uint32_t k[8];
+  launder_key(key, k);
+  chacha_block_raw(k, ctr, nonce, out);
 }
 
 // HChaCha20 (CRYPTO_hchacha20, crypto/chacha/chacha.cc:43-63): the state of
@@ -376,6 +390,15 @@ __device__ __forceinline__ void crypt_block_x(const uint8_t *src, uint8_t *dst, 
 #else
 #define CHACHA_OCC
 #endif
+// Coalesced record I/O for L = 4 (default): a wave's loads and stores move
+// 256 contiguous bytes per record per instruction (lane = 16-byte chunk of a
+// record's 4-block run), staged through LDS to the lane that owns each
+// 64-byte block.  With the lane-per-block pattern (0) each 16-byte access
+// sits at a 64-byte lane stride: the same copy costs 1.32x the time and
+// 1.3x the counted HBM bytes (tools/micro/calib_copy.hip).
+#ifndef BSSL_AMD_CHACHA_COAL
+#define BSSL_AMD_CHACHA_COAL 1
+#endif
 #ifndef BSSL_AMD_CHACHA_STAMPS
 #define BSSL_AMD_CHACHA_STAMPS 0
 #endif
@@ -471,6 +494,24 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   uint8_t *dst = b.out + m.off;
   const bool aligned = ((reinterpret_cast<uintptr_t>(src) |
                          reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+  // LDS: one 64-byte block per thread (the first ciphertext block while the
+  // powers of r are built, then the staging area of the coalesced record
+  // I/O: record slot r of the wave at r * 256, block q at + 64 q, its 16-byte
+  // chunk j at + 16 ((j + q + r) mod 4) -- conflict-free both for the 16
+  // chunks of a record and for the 4 chunks a lane reads of its own block).
+  __shared__ uint4 s_c0[kThreads][4];
+  constexpr bool kCoal = BSSL_AMD_CHACHA_COAL && L == 4;
+  // Per record slot: byte offset and the number of full 64-byte blocks the
+  // coalesced path moves (0 unless the record is live and 16-byte aligned).
+  __shared__ uint4 s_rinfo[kThreads / L];
+  const int wbase = threadIdx.x & ~63;
+  uint8_t *const stage = reinterpret_cast<uint8_t *>(&s_c0[wbase][0]);
+  const int rslot = lane / L;
+  if (kCoal && q == 0) {
+    const uint32_t nfull = live && aligned ? (uint32_t)(m.len / 64) : 0u;
+    s_rinfo[threadIdx.x / L] = make_uint4((uint32_t)m.off, (uint32_t)(m.off >> 32), nfull, 0u);
+  }
+  auto saddr = [](int r, int qq, int j) { return r * 256 + qq * 64 + ((j + qq + r) & 3) * 16; };
 
   // Encrypt (or decrypt) the data block of ChaCha block u held in ks; returns
   // the ciphertext words (masked past the end) in c[].
@@ -491,11 +532,27 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
       for (int i = 0; i < 4; i++) pre[i] = sp[i];
     }
   };
-  auto crypt_block = [&](uint64_t u, const uint32_t ks[16], const uint4 pre[4], uint32_t c[16]) {
+  auto crypt_block = [&](uint64_t u, const uint32_t ks[16], const uint4 pre[4], uint32_t c[16],
+                         bool staged) {
     const uint64_t d = u - 1;
     const uint64_t rem = vlen - 64 * d;
     uint32_t x[16], y[16];
-    if (m.len >= 64 * d + 64 && aligned) {
+    if (kCoal && staged && m.len >= 64 * d + 64 && aligned) {
+      // Full block, coalesced I/O: input from the staging area, output back
+      // to it (stored after the iteration by record-contiguous stores).
+      uint8_t *my = stage + rslot * 256 + q * 64;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(my + ((i + q + rslot) & 3) * 16);
+        x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
+      }
+#pragma unroll
+      for (int i = 0; i < 16; i++) y[i] = x[i] ^ ks[i];
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        *reinterpret_cast<uint4 *>(my + ((i + q + rslot) & 3) * 16) =
+            make_uint4(y[4 * i], y[4 * i + 1], y[4 * i + 2], y[4 * i + 3]);
+    } else if (m.len >= 64 * d + 64 && aligned) {
       uint4 *dp = reinterpret_cast<uint4 *>(dst + 64 * d);
 #pragma unroll
       for (int i = 0; i < 4; i++) {
@@ -558,7 +615,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   prefetch((uint64_t)q, pre);
   chacha_block(key, (uint32_t)q, nonce, ks);
   const bool have0 = q >= 1 && (uint64_t)q <= nblk;
-  if (have0) crypt_block((uint64_t)q, ks, pre, c0);
+  if (have0) crypt_block((uint64_t)q, ks, pre, c0, false);
   CSTAMP(1);
   if (BSSL_AMD_CHACHA_PRIO) __builtin_amdgcn_s_setprio(0);
   uint32_t kw[8];
@@ -566,7 +623,6 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   for (int i = 0; i < 8; i++) kw[i] = __shfl(ks[i], 0, L);
   // The first block's ciphertext waits in LDS while the powers of r are
   // built (the register peak of the kernel otherwise).
-  __shared__ uint4 s_c0[kThreads][4];
   if (have0) {
 #pragma unroll
     for (int i = 0; i < 4; i++)
@@ -684,22 +740,77 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     absorb((uint64_t)q, c0);
   }
   CSTAMP(2);
+  // Coalesced I/O: in instruction k, lane l moves 16-byte chunk l mod 16 of
+  // record slot 4k + l/16's data blocks 4 it - 1 .. 4 it + 2 (256 bytes).
+  const int cq = (lane & 15) >> 2, cj = lane & 3;
+  auto coal_addr = [&](int k, int it, uint64_t &addr) {
+    uint32_t slot = wbase / L + 4 * k + (lane >> 4);
+    asm volatile("" : "+v"(slot));  // re-read per use, not hoisted (registers)
+    const uint4 inf = s_rinfo[slot];
+    const uint64_t dd = (uint64_t)it * 4 + cq - 1;
+    addr = ((uint64_t)inf.y << 32 | inf.x) + 64 * dd + 16 * cj;
+    return dd < inf.z;
+  };
   for (int it = 1; it < iters; it++) {
     const uint64_t u = (uint64_t)it * L + q;
-    prefetch(u, pre);
+    // Laundered ahead of the LDS-DMA loads: hipcc waits for every
+    // outstanding LDS-DMA load at an inline asm statement, so none may sit
+    // between the loads and the rounds.
+    uint32_t kl[8];
+    launder_key(key, kl);
+    if constexpr (kCoal) {
+      // Direct-to-LDS loads (global_load_lds_dwordx4, no VGPRs): instruction
+      // k writes the wave's staging bytes [1024 k, 1024 k + 1024) lane-
+      // linearly, so lane l lands at record slot r = 4k + l/16, position
+      // l mod 16 = 4 qq + p, and loads the chunk j whose swizzled position
+      // (j + qq + r) mod 4 is p.
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        uint64_t a;
+        const int r = 4 * k + (lane >> 4);
+        const int j = (cj - cq - r) & 3;
+        if (coal_addr(k, it, a))
+          __builtin_amdgcn_global_load_lds(
+              reinterpret_cast<const void *>(b.in + a - 16 * cj + 16 * j),
+              reinterpret_cast<__attribute__((address_space(3))) void *>(
+                  reinterpret_cast<uintptr_t>(stage + 1024 * k)),
+              16, 0, 0);
+      }
+    } else {
+      prefetch(u, pre);
+    }
 #if BSSL_AMD_CHACHA_ABLATE == 3
 #pragma unroll
     for (int i = 0; i < 16; i++) ks[i] = key[i & 7] ^ (uint32_t)u ^ nonce[i % 3];
 #else
-    chacha_block(key, (uint32_t)u, nonce, ks);
+    chacha_block_raw(kl, (uint32_t)u, nonce, ks);
 #endif
+    if constexpr (kCoal) {
+      // vmcnt(0): the LDS-DMA loads have landed.  The keystream words are
+      // inputs so the rounds stay ahead of the wait (hipcc otherwise sinks
+      // them below it and the load latency is exposed).
+      asm volatile("s_waitcnt vmcnt(0)" ::"v"(ks[0]), "v"(ks[1]), "v"(ks[2]), "v"(ks[3]),
+                   "v"(ks[4]), "v"(ks[5]), "v"(ks[6]), "v"(ks[7]), "v"(ks[8]), "v"(ks[9]),
+                   "v"(ks[10]), "v"(ks[11]), "v"(ks[12]), "v"(ks[13]), "v"(ks[14]), "v"(ks[15])
+                   : "memory");
+    }
     if (u <= nblk) {
       uint32_t c[16];
-      crypt_block(u, ks, pre, c);
+      crypt_block(u, ks, pre, c, true);
 #if BSSL_AMD_CHACHA_ABLATE == 2
       if (c[0] == 0x12345678u)
 #endif
       absorb(u, c);
+    }
+    if constexpr (kCoal) {
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        uint64_t a;
+        if (coal_addr(k, it, a))
+          *reinterpret_cast<uint4 *>(b.out + a) =
+              *reinterpret_cast<const uint4 *>(stage + saddr(4 * k + (lane >> 4), cq, cj));
+      }
     }
   }
 

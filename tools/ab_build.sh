@@ -1,15 +1,18 @@
 #!/bin/bash
-# Build a variant library from gcm.hip at git revision REV into
-# boringssl_amd/csrc/build/ab_NAME/libbssl_amd.so (A/B timing on one box:
-# BSSL_AMD_LIB selects it).  Usage: tools/ab_build.sh NAME REV [extra hipcc flags]
+# Build a variant library from one kernel source (SRC, default gcm.hip) at git
+# revision REV (or the working tree: REV=WT) with extra hipcc flags into
+# boringssl_amd/csrc/build/ab_NAME/libbssl_amd.so, linked with the current
+# objects of every other source (A/B timing on one box: BSSL_AMD_LIB selects
+# it).  Usage: [SRC=chacha.hip] tools/ab_build.sh NAME REV [extra hipcc flags]
 set -eu
 NAME=$1; REV=$2; shift 2
+SRC=${SRC:-gcm.hip}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 C=$ROOT/boringssl_amd/csrc
 O=$C/build/ab_$NAME
 mkdir -p $O
-git -C $ROOT show $REV:boringssl_amd/csrc/gcm.hip > $O/gcm.hip
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I$ROOT/include -I$C -fvisibility=hidden "$@" -c $O/gcm.hip -o $O/gcm.o
-OBJS=$(ls $C/build/*.o | grep -v gcm.hip.o)
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $O/libbssl_amd.so $O/gcm.o $OBJS -Wl,-Bsymbolic
+if [ "$REV" = WT ]; then cp $C/$SRC $O/$SRC; else git -C $ROOT show $REV:boringssl_amd/csrc/$SRC > $O/$SRC; fi
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I$ROOT/include -I$C -fvisibility=hidden "$@" -c $O/$SRC -o $O/variant.o
+OBJS=$(ls $C/build/*.o | grep -v "/$SRC.o")
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $O/libbssl_amd.so $O/variant.o $OBJS -Wl,-Bsymbolic
 echo $O/libbssl_amd.so

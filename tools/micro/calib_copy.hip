@@ -1,0 +1,124 @@
+// FETCH_SIZE / WRITE_SIZE calibration for the record access patterns of the
+// AEAD kernels (MI355X_MICROARCH.md, HBM section: only 16 B/lane streaming
+// reads and stores are calibrated; other widths must be calibrated on a known
+// byte count).  Each kernel copies the same records (1M x 1350 B at a 1360-byte
+// stride, plus a 16-byte tag per record) with a different lane pattern:
+//   copy_stream  : 16 B per lane, consecutive lanes consecutive 16 B chunks
+//                  over the whole padded buffer (the guide's calibrated case)
+//   copy_chacha  : chacha.hip's pattern: 4 lanes per record, lane q moves
+//                  64-byte block 4*it+q as four 16-byte loads / stores
+//   copy_quad    : same bytes, transposed: store k of lane q is chunk q of
+//                  block 4*it+k (each instruction covers 64 contiguous bytes
+//                  per record)
+//   copy_gcm     : gcm.hip's pattern: 16 lanes per record, lane q moves
+//                  16-byte block 16*it+q (256 contiguous bytes per record)
+// Known bytes per launch: read = write = records * 1350 (+ tags written).
+// Build: hipcc --offload-arch=gfx950 -O3 -o calib_copy calib_copy.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <cstring>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); return 1; } } while (0)
+
+constexpr uint64_t kRecs = 1 << 20, kLen = 1350, kStride = 1360;
+
+// Tail of a record: dword copies of the last (len % 16) bytes' 16-byte chunk.
+__device__ __forceinline__ void copy_tail(const uint8_t *s, uint8_t *d, uint32_t n) {
+  for (uint32_t i = 0; i + 4 <= n; i += 4)
+    *reinterpret_cast<uint32_t *>(d + i) = *reinterpret_cast<const uint32_t *>(s + i);
+  const uint32_t r = n & ~3u;
+  if (n & 2) *reinterpret_cast<uint16_t *>(d + r) = *reinterpret_cast<const uint16_t *>(s + r);
+  if (n & 1) d[n - 1] = s[n - 1];
+}
+
+__global__ __launch_bounds__(256) void copy_stream(const uint4 *s, uint4 *d, uint64_t n16) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += gridDim.x * 256ull) d[i] = s[i];
+}
+
+template <int MODE>  // 0 chacha, 1 quad
+__global__ __launch_bounds__(256) void copy_rec4(const uint8_t *s, uint8_t *d, uint8_t *tags) {
+  const uint64_t rec = (blockIdx.x * 256ull + threadIdx.x) / 4;
+  const int q = threadIdx.x & 3;
+  if (rec >= kRecs) return;
+  const uint8_t *sp = s + rec * kStride;
+  uint8_t *dp = d + rec * kStride;
+  constexpr uint32_t kFull = kLen / 64;  // 21 full blocks
+  for (uint32_t it = 0; it * 4 < kFull + 1; it++) {
+    const uint32_t blk = it * 4 + q;
+    if (MODE == 0) {
+      if (blk < kFull) {
+        const uint4 *a = reinterpret_cast<const uint4 *>(sp + 64 * blk);
+        uint4 v[4];
+        for (int k = 0; k < 4; k++) v[k] = a[k];
+        uint4 *b = reinterpret_cast<uint4 *>(dp + 64 * blk);
+        for (int k = 0; k < 4; k++) b[k] = v[k];
+      } else if (blk == kFull) {
+        copy_tail(sp + 64 * blk, dp + 64 * blk, kLen - 64 * kFull);
+      }
+    } else {
+      uint4 v[4];
+      for (int k = 0; k < 4; k++) {
+        const uint32_t bk = it * 4 + k;
+        if (bk < kFull) v[k] = reinterpret_cast<const uint4 *>(sp + 64 * bk)[q];
+      }
+      for (int k = 0; k < 4; k++) {
+        const uint32_t bk = it * 4 + k;
+        if (bk < kFull) reinterpret_cast<uint4 *>(dp + 64 * bk)[q] = v[k];
+        else if (bk == kFull && q == 0) copy_tail(sp + 64 * bk, dp + 64 * bk, kLen - 64 * kFull);
+      }
+    }
+  }
+  if (q == 0) reinterpret_cast<uint4 *>(tags)[rec] = make_uint4(rec, 1, 2, 3);
+}
+
+__global__ __launch_bounds__(256) void copy_gcm(const uint8_t *s, uint8_t *d, uint8_t *tags) {
+  const uint64_t rec = (blockIdx.x * 256ull + threadIdx.x) / 16;
+  const int q = threadIdx.x & 15;
+  if (rec >= kRecs) return;
+  const uint8_t *sp = s + rec * kStride;
+  uint8_t *dp = d + rec * kStride;
+  constexpr uint32_t kFull = kLen / 16;  // 84 full 16-byte blocks
+  for (uint32_t j = q; j <= kFull; j += 16) {
+    if (j < kFull) reinterpret_cast<uint4 *>(dp)[j] = reinterpret_cast<const uint4 *>(sp)[j];
+    else copy_tail(sp + 16 * j, dp + 16 * j, kLen - 16 * kFull);
+  }
+  if (q == 0) reinterpret_cast<uint4 *>(tags)[rec] = make_uint4(rec, 1, 2, 3);
+}
+
+int main(int argc, char **argv) {
+  const int reps = argc > 1 ? atoi(argv[1]) : 5;
+  const uint64_t bytes = kRecs * kStride;
+  uint8_t *s, *d, *t;
+  CK(hipMalloc(&s, bytes));
+  CK(hipMalloc(&d, bytes));
+  CK(hipMalloc(&t, kRecs * 16));
+  CK(hipMemset(s, 0x5a, bytes));
+  CK(hipMemset(d, 0, bytes));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const char *names[4] = {"copy_stream", "copy_chacha", "copy_quad", "copy_gcm"};
+  for (int v = 0; v < 4; v++) {
+    float best = 1e30f;
+    for (int r = 0; r < reps; r++) {
+      CK(hipEventRecord(e0));
+      if (v == 0) copy_stream<<<8192, 256>>>((const uint4 *)s, (uint4 *)d, bytes / 16);
+      if (v == 1) copy_rec4<0><<<kRecs * 4 / 256, 256>>>(s, d, t);
+      if (v == 2) copy_rec4<1><<<kRecs * 4 / 256, 256>>>(s, d, t);
+      if (v == 3) copy_gcm<<<kRecs * 16 / 256, 256>>>(s, d, t);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      if (ms < best) best = ms;
+    }
+    const double moved = v == 0 ? 2.0 * bytes : 2.0 * kRecs * kLen + 16.0 * kRecs;
+    printf("%-12s best %.3f ms  %.0f GB/s (known bytes read %.0f write %.0f)\n", names[v], best,
+           moved / best / 1e6, v == 0 ? (double)bytes : (double)kRecs * kLen,
+           v == 0 ? (double)bytes : kRecs * kLen + 16.0 * kRecs);
+  }
+  CK(hipDeviceSynchronize());
+  return 0;
+}
