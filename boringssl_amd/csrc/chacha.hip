@@ -307,6 +307,23 @@ struct PAcc {
 
 __device__ __forceinline__ PAcc pacc_zero() { return PAcc{{0, 0, 0, 0, 0}}; }
 
+// Lazy product with the 5x multiples of r's limbs 1..4 supplied (s[i-1] =
+// 5 r_i, precomputed once per record).
+__device__ __forceinline__ void pmac_s(PAcc &acc, const P &a, const uint32_t *r,
+                                       const uint32_t *s) {
+  const uint32_t s1 = s[0], s2 = s[1], s3 = s[2], s4 = s[3];
+  acc.d[0] += mul64(a.h[0], r[0]) + mul64(a.h[1], s4) + mul64(a.h[2], s3) +
+              mul64(a.h[3], s2) + mul64(a.h[4], s1);
+  acc.d[1] += mul64(a.h[0], r[1]) + mul64(a.h[1], r[0]) + mul64(a.h[2], s4) +
+              mul64(a.h[3], s3) + mul64(a.h[4], s2);
+  acc.d[2] += mul64(a.h[0], r[2]) + mul64(a.h[1], r[1]) + mul64(a.h[2], r[0]) +
+              mul64(a.h[3], s4) + mul64(a.h[4], s3);
+  acc.d[3] += mul64(a.h[0], r[3]) + mul64(a.h[1], r[2]) + mul64(a.h[2], r[1]) +
+              mul64(a.h[3], r[0]) + mul64(a.h[4], s4);
+  acc.d[4] += mul64(a.h[0], r[4]) + mul64(a.h[1], r[3]) + mul64(a.h[2], r[2]) +
+              mul64(a.h[3], r[1]) + mul64(a.h[4], r[0]);
+}
+
 __device__ __forceinline__ void pmac(PAcc &acc, const P &a, const P &r) {
   const uint32_t s1 = r.h[1] * 5, s2 = r.h[2] * 5, s3 = r.h[3] * 5, s4 = r.h[4] * 5;
   acc.d[0] += mul64(a.h[0], r.h[0]) + mul64(a.h[1], s4) + mul64(a.h[2], s3) +
@@ -650,6 +667,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   // ChaCha rounds they cost ~35 VGPRs and thereby a wave per SIMD.
   // Slot layout: pw[0..kLog+2] then r^3, 5 limbs each.
   __shared__ uint32_t s_pow[kThreads / L][5 * (kLog + 4)];
+  __shared__ uint4 s_apow[kThreads / L][9];
   uint32_t *const mypow = s_pow[threadIdx.x / L];
   if (q == 0) {
     const P r3v = pmul(pw[1], pw[0]);
@@ -659,6 +677,17 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
       for (int i = 0; i < 5; i++) mypow[5 * k + i] = pw[k].h[i];
 #pragma unroll
     for (int i = 0; i < 5; i++) mypow[5 * (kLog + 3) + i] = r3v.h[i];
+    // The block loop's four multipliers R^L, r^3, r^2, r with their 5x
+    // multiples, 16-byte aligned: one batch of ds_read_b128 per absorb.
+    const P *am[4] = {&pw[kLog + 2], &r3v, &pw[1], &pw[0]};
+    uint32_t *ap = reinterpret_cast<uint32_t *>(s_apow[threadIdx.x / L]);
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+#pragma unroll
+      for (int i = 0; i < 5; i++) ap[9 * m + i] = am[m]->h[i];
+#pragma unroll
+      for (int i = 1; i < 5; i++) ap[9 * m + 4 + i] = am[m]->h[i] * 5;
+    }
   }
   __builtin_amdgcn_wave_barrier();
   // Power k (k = kLog + 3: r^3), re-read at each use (the address is
@@ -713,10 +742,20 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     const uint64_t d = u - 1;
     if (d < nunits) {
       PAcc t = pacc_zero();
-      pmac(t, acc, pwr(kStride));
-      pmac(t, pblock(c[0], c[1], c[2], c[3]), pwr(kR3));
-      pmac(t, pblock(c[4], c[5], c[6], c[7]), pwr(1));
-      pmac(t, pblock(c[8], c[9], c[10], c[11]), pwr(0));
+      uint32_t ap[36];
+      {
+        uint32_t slot = threadIdx.x / L;
+        asm volatile("" : "+v"(slot));  // re-read per block, not hoisted (registers)
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+          const uint4 v = s_apow[slot][i];
+          ap[4 * i] = v.x; ap[4 * i + 1] = v.y; ap[4 * i + 2] = v.z; ap[4 * i + 3] = v.w;
+        }
+      }
+      pmac_s(t, acc, ap, ap + 5);
+      pmac_s(t, pblock(c[0], c[1], c[2], c[3]), ap + 9, ap + 14);
+      pmac_s(t, pblock(c[4], c[5], c[6], c[7]), ap + 18, ap + 23);
+      pmac_s(t, pblock(c[8], c[9], c[10], c[11]), ap + 27, ap + 32);
       acc = padd(preduce(t), pblock(c[12], c[13], c[14], c[15]));
     } else {
       P tt = pblock(c[0], c[1], c[2], c[3]);
