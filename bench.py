@@ -340,19 +340,20 @@ def cpu_baseline(aead, length, seconds):
             "sample": f"{done} records x {length} B via the C oracle, one thread"}
 
 
-def load_profile(kernel_prefix):
-    """HBM bytes per launch and LDS/VALU busy fractions from the rocprofv3 PMC
-    passes (tools/pmc_traffic.py -> profiles/traffic.json)."""
+def load_profile(config, kernel_prefix):
+    """HBM bytes per launch and LDS/VALU busy fractions of `config`'s bulk
+    kernel from the rocprofv3 PMC passes (tools/profile_r02.sh ->
+    tools/pmc_traffic.py -> profiles/traffic.json)."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(p):
         return None, None
     try:
-        d = json.load(open(p))
+        d = json.load(open(p)).get(config, {})
         for k, v in d.items():
             if k.startswith(kernel_prefix):
                 cb = {x: round(v[x], 3) for x in ("lds_busy", "valu_busy") if x in v}
                 if cb:
-                    cb["source"] = "profiles/traffic.json (rocprofv3 PMC)"
+                    cb["source"] = f"profiles/traffic.json[{config}] (rocprofv3 PMC)"
                 return v.get("hbm_bytes_per_launch"), cb or None
     except Exception:
         return None, None
@@ -514,7 +515,7 @@ def main():
     value = total_bytes * args.steps / elapsed / 2**30
     algo_bytes = 2 * pt_bytes + (29 + nonce_len) * nrec  # PT in + CT out + tag + nonce + AD
     achieved = algo_bytes / (avg_kernel_ms / 1000.0) / 1e9
-    traffic, compute_bound = load_profile(kname)
+    traffic, compute_bound = load_profile(args.config, kname)
     if world > 1 or args.records or args.op != "seal":
         traffic, compute_bound = None, None  # the profile is of the default N=1 seal run
 

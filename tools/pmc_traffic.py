@@ -1,12 +1,18 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc passes (tools/gpu_check.sh `pmc` step) into
-profiles/traffic.json: HBM bytes per launch of each kernel.
+"""Summarise the rocprofv3 --pmc passes of tools/profile_r02.sh into
+profiles/traffic.json: per config, the bulk kernel's HBM bytes per launch and
+its LDS / VALU busy fractions, plus the FETCH/WRITE calibration copies.
 
 Corrections per /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
 FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports exactly half
-of the bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled;
-WRITE_SIZE is exact for 16 B/lane streaming stores.
-Usage: tools/pmc_traffic.py gpurun_out [profiles/traffic.json]
+of the bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled
+(`hbm_bytes_per_launch`, the guide's rule); WRITE_SIZE is exact for 16 B/lane
+streaming stores.  Other access patterns are uncalibrated in the guide, so
+tools/micro/calib_copy.hip copies a known byte count with each record access
+pattern of the kernels and the ratio counted/known per pattern is stored under
+"calibration" (DESIGN.md 5.1 reads the kernels' counts through it).
+
+Usage: tools/pmc_traffic.py gpurun_out/r02 [profiles/traffic.json]
 """
 import collections
 import csv
@@ -15,51 +21,93 @@ import os
 import re
 import sys
 
+CALIB_KNOWN = {  # bytes per launch moved by each tools/micro/calib_copy kernel
+    "copy_stream": (1 << 20) * 1360,
+    "copy_chacha": (1 << 20) * 1350,
+    "copy_quad": (1 << 20) * 1350,
+    "copy_gcm": (1 << 20) * 1350,
+}
+CALIB_TAGS = (1 << 20) * 16  # the record kernels also write one 16-byte tag per record
 
-def load(d):
+
+def short_name(name):
+    m = re.search(r"::(\w+)(<[^>]*>)?\(", name)  # bssl_amd::(anon)::gcm_kernel<...>(
+    return m.group(1) if m else name.split("(")[0].split()[-1]  # copy_rec4<0>
+
+
+def load(path):
     out = collections.defaultdict(lambda: collections.defaultdict(list))
-    for sub in sorted(os.listdir(d)):
-        p = os.path.join(d, sub, "run_counter_collection.csv")
-        if not sub.startswith("pmc") or not os.path.exists(p):
-            continue
-        for r in csv.DictReader(open(p)):
-            name = r["Kernel_Name"]
-            m = re.search(r"::(\w+)(<[^>]*>)?\(", name)
-            short = m.group(1) if m else name
-            out[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    p = os.path.join(path, "run_counter_collection.csv")
+    if not os.path.exists(p):
+        return out
+    for r in csv.DictReader(open(p)):
+        out[short_name(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return out
 
 
+def summarise(c):
+    avg = {n: sum(v) / len(v) for n, v in c.items()}
+    e = {"counters_avg_per_dispatch": avg}
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        fetch = 2 * avg["FETCH_SIZE"] * 1024
+        write = avg["WRITE_SIZE"] * 1024
+        e.update({"fetch_bytes_corrected": fetch, "write_bytes": write,
+                  "hbm_bytes_per_launch": fetch + write})
+    if "GRBM_GUI_ACTIVE" in avg:
+        cyc = avg["GRBM_GUI_ACTIVE"] / 8  # kernel cycles (GRBM sums the 8 XCDs)
+        e["grbm_gui_active_per_xcd"] = cyc
+        # Busy fractions of the units that can bind an integer kernel
+        # (SQ_LDS_IDX_ACTIVE = LDS-array cycles summed over the 256 CUs; a
+        # wave64 VALU instruction occupies its SIMD32 for >= 2 cycles, 1024 SIMDs).
+        if "SQ_LDS_IDX_ACTIVE" in avg:
+            e["lds_busy"] = avg["SQ_LDS_IDX_ACTIVE"] / 256 / cyc
+        if "SQ_INSTS_VALU" in avg:
+            e["valu_busy"] = avg["SQ_INSTS_VALU"] * 2 / 1024 / cyc
+        if "SQ_WAVE_CYCLES" in avg:
+            for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY"):
+                if k in avg:
+                    e[k.lower() + "_frac"] = avg[k] / avg["SQ_WAVE_CYCLES"]
+    return e
+
+
 def main():
-    src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+    src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/r02"
     dst = sys.argv[2] if len(sys.argv) > 2 else os.path.join(
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "traffic.json")
-    data = load(src)
     res = {}
-    for k, c in data.items():
-        avg = {n: sum(v) / len(v) for n, v in c.items()}
-        e = {"counters_avg_per_dispatch": avg}
-        if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
-            fetch = 2 * avg["FETCH_SIZE"] * 1024
-            write = avg["WRITE_SIZE"] * 1024
-            e.update({"fetch_bytes_corrected": fetch, "write_bytes": write,
-                      "hbm_bytes_per_launch": fetch + write})
-        if "GRBM_GUI_ACTIVE" in avg:
-            cyc = avg["GRBM_GUI_ACTIVE"] / 8  # kernel cycles (GRBM sums the 8 XCDs)
-            e["grbm_gui_active_per_xcd"] = cyc
-            # Busy fractions of the compute units that can bind an integer
-            # kernel (MI355X_MICROARCH.md: SQ_LDS_IDX_ACTIVE = LDS-array cycles,
-            # summed over the 256 CUs; a wave64 VALU instruction occupies its
-            # SIMD32 for 2 cycles, 1024 SIMDs).
-            if "SQ_LDS_IDX_ACTIVE" in avg:
-                e["lds_busy"] = avg["SQ_LDS_IDX_ACTIVE"] / 256 / cyc
-            if "SQ_INSTS_VALU" in avg:
-                e["valu_busy"] = avg["SQ_INSTS_VALU"] * 2 / 1024 / cyc
-        res[k] = e
+    per_cfg = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(list)))
+    for sub in sorted(os.listdir(src)):
+        m = re.match(r"pmc_(config\w+?)_(fetch|write|sq)$", sub)
+        if not m:
+            continue
+        for k, c in load(os.path.join(src, sub)).items():
+            for n, v in c.items():
+                per_cfg[m.group(1)][k][n].extend(v)
+    for cfg, kernels in per_cfg.items():
+        res[cfg] = {k: summarise(c) for k, c in kernels.items()}
+    calib = collections.defaultdict(dict)
+    for sub, key in (("calib_fetch", "FETCH_SIZE"), ("calib_write", "WRITE_SIZE")):
+        for k, c in load(os.path.join(src, sub)).items():
+            base = k.split("<")[0]
+            name = {"copy_rec4<0>": "copy_chacha", "copy_rec4<1>": "copy_quad"}.get(k, base)
+            if name not in CALIB_KNOWN or key not in c:
+                continue
+            counted = sum(c[key]) / len(c[key]) * 1024
+            known = CALIB_KNOWN[name]
+            if key == "FETCH_SIZE":
+                calib[name]["fetch_counted_over_known"] = counted / known
+                calib[name]["fetch_x2_over_known"] = 2 * counted / known
+            else:
+                known_w = known + (CALIB_TAGS if name != "copy_stream" else 0)
+                calib[name]["write_counted_over_known"] = counted / known_w
+    if calib:
+        res["calibration"] = dict(calib)
     json.dump(res, open(dst, "w"), indent=1, sort_keys=True)
-    for k, e in res.items():
-        print(k, {x: (round(y / 1e9, 3) if isinstance(y, float) else y) for x, y in e.items()
-                  if x != "counters_avg_per_dispatch"})
+    for cfg, ks in res.items():
+        for k, e in ks.items():
+            print(cfg, k, {x: (round(y / 1e9, 3) if isinstance(y, float) and y > 1e6 else
+                               round(y, 3) if isinstance(y, float) else y)
+                           for x, y in e.items() if x != "counters_avg_per_dispatch"})
 
 
 if __name__ == "__main__":
