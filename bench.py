@@ -108,16 +108,20 @@ def _pad16(lens, align=16):
     return (lens + a - np.uint64(1)) // a * a
 
 
-# Record alignment of the batch layout (bytes; BSSL_AMD_ALIGN overrides).
-# 128-byte-aligned config 3 records (no two records on one cache line)
-# measured the same speed and write traffic as the packed 16-byte layout.
+# Record alignment of the batch layout (bytes; BSSL_AMD_ALIGN overrides): no
+# two records share a 128-byte cache line.  Config 3 (1350-byte records, so a
+# 1408- instead of 1360-byte stride) measured 1,130-1,136 GiB/s against
+# 1,091-1,124 for 16-byte alignment on one box, counted traffic within 2 %
+# (DESIGN.md 4.3); 16 KiB records are unaffected.  Algorithmic bytes do not
+# count the padding.
 def record_align(config):
-    return int(os.environ.get("BSSL_AMD_ALIGN", 16))
+    return int(os.environ.get("BSSL_AMD_ALIGN", 128))
 
 
 class Shard:
     """Records [first, first + n) of the global record sequence on one rank.
-    `lens`/`offs` describe the rank's packed batch (16-byte-aligned records)."""
+    `lens`/`offs` describe the rank's packed batch (records aligned to
+    `align` bytes, record_align)."""
 
     def __init__(self, first, lens, key_first=0, nkeys=0, align=16):
         self.first = int(first)
@@ -165,10 +169,11 @@ def shard_plan(config, rank, world, records=0):
         rpk = RECORDS_PER_KEY[config]
         nkeys_total = nrec // rpk
         k0, k1 = nkeys_total * rank // world, nkeys_total * (rank + 1) // world
-        return Shard(k0 * rpk, np.full((k1 - k0) * rpk, length, np.uint64), k0, k1 - k0)
+        return Shard(k0 * rpk, np.full((k1 - k0) * rpk, length, np.uint64), k0, k1 - k0,
+                     align=record_align(config))
     all_lens = mixed_lengths(0, nrec) if length == "mixed" else np.full(nrec, length, np.uint64)
     s = byte_balanced_split(all_lens, world)
-    return Shard(s[rank], all_lens[s[rank]:s[rank + 1]].copy())
+    return Shard(s[rank], all_lens[s[rank]:s[rank + 1]].copy(), align=record_align(config))
 
 
 # ---------------------------------------------------------------------------

@@ -13,6 +13,22 @@ for p in (HERE, ROOT):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
     config.addinivalue_line("markers", "slow: long-running (full BASELINE-size batches)")
+    config.addinivalue_line("markers", "multigpu: needs two or more GPUs in one process")
+
+
+def pytest_collection_modifyitems(config, items):
+    """Tests marked multigpu are deselected (not skipped) where fewer than two
+    GPUs are visible -- the one-GPU round-end box included.  Counting devices
+    does not initialise the GPU on this image."""
+    if not any(it.get_closest_marker("multigpu") for it in items):
+        return
+    import torch
+    if torch.cuda.device_count() >= 2:
+        return
+    keep = [it for it in items if not it.get_closest_marker("multigpu")]
+    dropped = [it for it in items if it.get_closest_marker("multigpu")]
+    config.hook.pytest_deselected(items=dropped)
+    items[:] = keep
 
 
 @pytest.fixture(scope="session")

@@ -823,13 +823,13 @@ def test_iovec_batch_vs_oracle(aead):
             assert st[i] == 1 and got == pts[i], i
 
 
+@pytest.mark.multigpu
 def test_context_used_from_another_device():
     """A context created on GPU 0 and used after the thread switched to GPU 1:
     host-buffer calls run on the key's device (and restore the caller's
     device); device-batch calls on the wrong device fail cleanly instead of
-    launching kernels against another GPU's key memory."""
-    if torch.cuda.device_count() < 2:
-        pytest.skip("needs two GPUs")
+    launching kernels against another GPU's key memory.  Needs two GPUs
+    (deselected elsewhere, tests/conftest.py)."""
     key, nonce = bytes(range(16)), bytes(12)
     ctx = ba.AEADCtx("aes-128-gcm", key, 16)
     ok, ct, tag = o.seal(o.AES_GCM, key, nonce, b"hello", b"ad")
