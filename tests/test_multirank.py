@@ -37,7 +37,7 @@ def _free_port():
 
 def _seal_shard(config, first, lens, offs):
     aead, key_len = bench.CONFIGS[config][0], bench.CONFIGS[config][1]
-    pt, offs2, nonces, ads = o.synth_batch(first, lens)
+    pt, offs2, nonces, ads = o.synth_batch(first, lens, align=bench.record_align(config))
     assert np.array_equal(offs2, offs)
     keys = np.frombuffer(bench.synth_key(0, key_len), dtype=np.uint8).copy()
     assert bytes(keys) == o.synth_key(0, key_len)
