@@ -71,9 +71,13 @@ __device__ __forceinline__ uint64_t stamp() {
 #endif
 // Per-wave diagnostic counters (stamps build only; see BSSL_AMD_GCM_STAMPS).
 struct StampVec {
-  uint64_t v[3];
+  uint64_t v[8];  // rounds, iters, loop; tile path: tiles, plan, build, process
 };
 constexpr int kRecPerWave = 4;
+// Tiled (multi-key) path: rotating wave priorities (process_records RP).
+#ifndef BSSL_AMD_GCM_TILE_RP
+#define BSSL_AMD_GCM_TILE_RP 1
+#endif
 
 // ---------------------------------------------------------------------------
 // Compile-time AES tables.
@@ -845,17 +849,25 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
 // Bulk kernel: CTR keystream + GHASH + tag for the (up to) 4 records of a
 // wave, 16 lanes per record.  `active` is per group (record in this key pass).
 // `gtab` = the key's nibble tables in global memory (record-end tree only).
-template <int NR, bool OPEN, bool XT>
+// L = lanes per record (16: 4 records per wave, GHASH stride H^16; 32: 2
+// records per wave, stride H^32 -- the byte table in LDS must be of H^L).
+// RP: rotate the wave's issue priority every iteration ((prio_base + it) mod
+// 4) -- in the tiled path all 16 waves must finish their units together, and
+// with fixed priorities the SIMD arbiter's age order makes the youngest wave
+// of each SIMD ~1.9x slower than the oldest.
+template <int NR, bool OPEN, bool XT, int L = 16, bool RP = false>
 __device__ __forceinline__ void process_records(const RoundKeys &rk, const BatchDesc &b,
                                                 const RecState *__restrict__ st, uint64_t rec,
                                                 bool active, const uint8_t *smem,
                                                 const uint8_t *gtab, uint32_t lc0, uint32_t lc1,
-                                                uint32_t mf0, StampVec &stamps) {
+                                                uint32_t mf0, StampVec &stamps,
+                                                int prio_base = 0) {
   (void)stamps;
 #if BSSL_AMD_GCM_STAMPS
   uint64_t *stv = stamps.v;
 #endif
-  const int q = threadIdx.x & 15;
+  static_assert(L == 16 || L == 32, "lanes per record");
+  const int q = threadIdx.x & (L - 1);
   RecordMeta m = {0, 0, 0, 0, 0};
   RecState s;
   s.j0 = s.ek0 = s.ya = make_uint4(0, 0, 0, 0);
@@ -878,9 +890,9 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   uint8_t *dst = b.out + m.off;
   const bool aligned = ((reinterpret_cast<uintptr_t>(src) |
                          reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
-  uint4 acc = (q == 15 && live) ? s.ya : make_uint4(0, 0, 0, 0);
+  uint4 acc = (q == L - 1 && live) ? s.ya : make_uint4(0, 0, 0, 0);
   // GHASH lane constants (Gh8): rotation by q bytes and the slot offsets.
-  const bool rs1 = (q >> 2) & 1, rs2 = (q >> 3) & 1;
+  const bool rs1 = (q >> 2) & 1, rs2 = (q >> 3) & 1;  // (rotation by q mod 16)
   const uint32_t rbs = (uint32_t)q & 3u;
   uint32_t P[4];
 #pragma unroll
@@ -898,7 +910,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   const uint32_t k0 = tload<T>(smem, taddr<0>(lc0, c0)) ^ tload<T>(smem, taddr<1>(lc1, c1)) ^
                       rotl(tload<T>(smem, taddr<2>(lc0, c2)) ^ rk.w[1][0], 16);
   WindowCache wc;
-  const int iters = wave_max((int)((nb + 15) / 16));
+  const int iters = wave_max((int)((nb + L - 1) / L));
   // Full aligned 16-byte blocks of this lane's record; the rest (the partial
   // last block, or every block of an unaligned record) take the byte path.
   const uint64_t nfull = aligned ? m.len / 16 : 0;
@@ -921,14 +933,22 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   // block j + 16 are interleaved with this block's rounds 3..NR.
   uint32_t cur[4];
   {
-    const uint32_t ctr = ctr0 + 1u + (uint32_t)q;
+    const uint32_t ctr = ctr0 + 1u + (uint32_t)q;  // block q
     const uint32_t s3 = bswap32(ctr) ^ rk.w[0][3];
     wc.update<T>(ctr, s3, c0, c1, c2, rk, smem, lc0, lc1);
     wc.rounds12<T>(k0, s3, cur[0], cur[1], cur[2], cur[3], smem, lc0, lc1);
   }
   auto step = [&](int it, uint4 x) {
-    const uint64_t j = (uint64_t)it * 16 + q;
-    const uint32_t ctrn = ctr0 + 1u + (uint32_t)(j + 16);  // next block, inc32 mod 2^32
+    if constexpr (RP) {
+      switch ((prio_base + it) & 3) {
+        case 0: __builtin_amdgcn_s_setprio(0); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+      }
+    }
+    const uint64_t j = (uint64_t)it * L + q;
+    const uint32_t ctrn = ctr0 + 1u + (uint32_t)(j + L);  // next block, inc32 mod 2^32
     uint32_t xs = bswap32(ctrn) ^ rk.w[0][3];
     wc.update<T>(ctrn, xs, c0, c1, c2, rk, smem, lc0, lc1);
     Gh8 h;
@@ -995,14 +1015,14 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
 #endif
 #if BSSL_AMD_GCM_PREFETCH == 2
   // Two iterations ahead (three buffers).
-  uint4 x0 = load_full(q), x1 = load_full(16 + q);
+  uint4 x0 = load_full(q), x1 = load_full(L + q);
   int it = 0;
   for (; it + 2 < iters; it += 3) {
-    const uint4 x2 = load_full((uint64_t)(it + 2) * 16 + q);
+    const uint4 x2 = load_full((uint64_t)(it + 2) * L + q);
     step(it, x0);
-    x0 = load_full((uint64_t)(it + 3) * 16 + q);
+    x0 = load_full((uint64_t)(it + 3) * L + q);
     step(it + 1, x1);
-    x1 = load_full((uint64_t)(it + 4) * 16 + q);
+    x1 = load_full((uint64_t)(it + 4) * L + q);
     step(it + 2, x2);
   }
   if (it < iters) step(it, x0);
@@ -1011,9 +1031,9 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   uint4 x0 = load_full(q);
   int it = 0;
   for (; it + 1 < iters; it += 2) {
-    const uint4 x1 = load_full((uint64_t)(it + 1) * 16 + q);
+    const uint4 x1 = load_full((uint64_t)(it + 1) * L + q);
     step(it, x0);
-    x0 = load_full((uint64_t)(it + 2) * 16 + q);
+    x0 = load_full((uint64_t)(it + 2) * L + q);
     step(it + 1, x1);
   }
   if (it < iters) step(it, x0);
@@ -1021,7 +1041,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
 #if BSSL_AMD_GCM_STAMPS
   g_stamp_loop += stamp() - sl0;
 #endif
-  finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, gtab, mf0);
+  finish_record<OPEN, L>(acc, nb, m, s, b, rec, active, live, dst, gtab, mf0);
 }
 
 // Byte table of H^16 from the key's nibble tables (power 4): entry (e, p) =
@@ -1079,7 +1099,7 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
   const uint32_t mf0 = 0xf0u;
 
   uint32_t loaded = 0xffffffffu;
-  StampVec stamps = {{0, 0, 0}};
+  StampVec stamps = {{0, 0, 0, 0, 0, 0, 0, 0}};
   const uint64_t n = b.num_records;
   if (!b.key_index) {
     // One key for the whole batch: no tiles or passes.  Each wave takes the
@@ -1116,6 +1136,10 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
   }
   for (uint64_t base = (uint64_t)blockIdx.x * kRecPerTile; base < n;
        base += (uint64_t)gridDim.x * kRecPerTile) {
+#if BSSL_AMD_GCM_STAMPS
+    const uint64_t tp0 = stamp();
+    stamps.v[3]++;
+#endif
     __syncthreads();
     if (wave == 0) {
       // Plan the tile: one pass per distinct key, in record order.
@@ -1138,11 +1162,17 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
       if (lane == 0) *s_npass = np;
     }
     __syncthreads();
+#if BSSL_AMD_GCM_STAMPS
+    stamps.v[4] += stamp() - tp0;
+#endif
     const int npass = *s_npass;
     for (int pi = 0; pi < npass; pi++) {
       const uint32_t k = __builtin_amdgcn_readfirstlane(s_pass_key[pi]);
       const uint64_t mask = s_pass_mask[pi];
       const uint8_t *gtab = reinterpret_cast<const uint8_t *>(keys[k].htab);
+#if BSSL_AMD_GCM_STAMPS
+      const uint64_t tb0 = stamp();
+#endif
       if (k != loaded) {
         __syncthreads();
         // Byte table of H^16 from the key's nibble tables (power 4): entry
@@ -1156,17 +1186,29 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
       for (int r = 0; r <= NR; r++)
 #pragma unroll
         for (int c = 0; c < 4; c++) rk.w[r][c] = keys[k].rk[r][c];
+#if BSSL_AMD_GCM_STAMPS
+      const uint64_t tq0 = stamp();
+      stamps.v[5] += tq0 - tb0;
+#endif
       const int t = wave * kRecPerWave + g;
       const bool active = (mask >> t) & 1;
-      process_records<NR, OPEN, XT>(rk, b, st, active ? rec_at(b, base + t) : 0, active, smem, gtab,
-                                lc0, lc1, mf0, stamps);
+      process_records<NR, OPEN, XT, 16, BSSL_AMD_GCM_TILE_RP != 0>(
+          rk, b, st, active ? rec_at(b, base + t) : 0, active, smem, gtab, lc0, lc1, mf0, stamps,
+          wave >> 2);
+      if (BSSL_AMD_GCM_TILE_RP) __builtin_amdgcn_s_setprio(0);
+#if BSSL_AMD_GCM_STAMPS
+      stamps.v[6] += stamp() - tq0;
+#endif
     }
   }
 #if BSSL_AMD_GCM_STAMPS
   if (blockIdx.x < 2 && (tid & 63) == 0)
-    printf("stamps block %d wave %d: iters %llu  cycles/iter %.0f  rounds3..NR/iter %.0f\n",
-           (int)blockIdx.x, wave, (unsigned long long)stamps.v[1],
-           (double)stamps.v[2] / (double)stamps.v[1], (double)stamps.v[0] / (double)stamps.v[1]);
+    printf("tiles block %d wave %d: tiles %llu per tile: plan+barriers %.0f build %.0f process %.0f "
+           "(loop %.0f) cycles/iter %.0f\n",
+           (int)blockIdx.x, wave, (unsigned long long)stamps.v[3],
+           (double)stamps.v[4] / stamps.v[3], (double)stamps.v[5] / stamps.v[3],
+           (double)stamps.v[6] / stamps.v[3], (double)stamps.v[2] / stamps.v[3],
+           (double)stamps.v[2] / (double)stamps.v[1]);
 #endif
 }
 
