@@ -300,14 +300,18 @@ bool check_batch(const EVP_AEAD *aead, const BSSL_AMD_BATCH *b) {
 
 // ---- single-record helper: host buffers -> one-record device batch --------
 
-// Per-thread staging buffer and stream of the host-buffer calls, one per
-// device (a thread may use contexts of several GPUs).
+// Per-thread staging buffers and stream of the host-buffer calls, one set per
+// device (a thread may use contexts of several GPUs): device memory for the
+// one-record batch and a pinned host mirror of it, so a call is one H2D and
+// one D2H DMA copy (pageable copies cost ~10 us each).
 struct Scratch {
   uint8_t *dev = nullptr;
+  uint8_t *host = nullptr;
   size_t cap = 0;
   hipStream_t stream = nullptr;
   ~Scratch() {
     if (dev) hipFree(dev);
+    if (host) hipHostFree(host);
     if (stream) hipStreamDestroy(stream);
   }
 };
@@ -315,7 +319,7 @@ constexpr int kMaxDevices = 64;
 thread_local Scratch t_scratch[kMaxDevices];
 
 // Scratch of the current device (the caller holds a DeviceGuard).
-uint8_t *scratch(size_t bytes, hipStream_t *stream) {
+Scratch *scratch(size_t bytes) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
   Scratch &sc = t_scratch[dev];
@@ -323,22 +327,32 @@ uint8_t *scratch(size_t bytes, hipStream_t *stream) {
     return nullptr;
   if (sc.cap < bytes) {
     if (sc.dev) hipFree(sc.dev);
+    if (sc.host) hipHostFree(sc.host);
+    sc.dev = sc.host = nullptr;
+    sc.cap = 0;
     size_t cap = bytes < (1u << 20) ? (1u << 20) : bytes;
     if (hipMalloc(&sc.dev, cap) != hipSuccess) {
       sc.dev = nullptr;
-      sc.cap = 0;
+      return nullptr;
+    }
+    if (hipHostMalloc(&sc.host, cap, hipHostMallocDefault) != hipSuccess) {
+      sc.host = nullptr;
+      hipFree(sc.dev);
+      sc.dev = nullptr;
       return nullptr;
     }
     sc.cap = cap;
   }
-  *stream = sc.stream;
-  return sc.dev;
+  return &sc;
 }
 
 size_t round16(size_t n) { return (n + 15) & ~size_t(15); }
 
 // Seal or open one record held in host memory.  `in`/`out` may be equal.
 // For open, `tag` is read; for seal it is written (tag_len bytes).
+// Staging layout (device and pinned host alike): nonce | AD | tag, status
+// (32 B) | record -- one H2D copy of all of it, one D2H copy of tag, status
+// and record.
 int one_record(const EVP_AEAD_CTX *ctx, bool open, const uint8_t *in, uint8_t *out,
                size_t len, const uint8_t *nonce, size_t nonce_len, const uint8_t *ad,
                size_t ad_len, uint8_t *tag, size_t tag_len) {
@@ -348,23 +362,20 @@ int one_record(const EVP_AEAD_CTX *ctx, bool open, const uint8_t *in, uint8_t *o
     PUT_ERROR(ERR_R_INTERNAL_ERROR);
     return 0;
   }
-  const size_t o_in = 0, o_nonce = round16(len), o_ad = o_nonce + round16(nonce_len),
-               o_tag = o_ad + round16(ad_len), o_status = o_tag + 16,
-               total = o_status + 16;
-  hipStream_t s;
-  uint8_t *d = scratch(total, &s);
-  if (!d) {
+  const size_t o_nonce = 0, o_ad = round16(nonce_len), o_tag = o_ad + round16(ad_len),
+               o_status = o_tag + 16, o_in = o_status + 16, total = o_in + round16(len);
+  Scratch *sc = scratch(total);
+  if (!sc) {
     PUT_ERROR(ERR_R_MALLOC_FAILURE);
     return 0;
   }
-  bool ok = true;
-  if (len) ok &= hipMemcpyAsync(d + o_in, in, len, hipMemcpyHostToDevice, s) == hipSuccess;
-  if (nonce_len)
-    ok &= hipMemcpyAsync(d + o_nonce, nonce, nonce_len, hipMemcpyHostToDevice, s) == hipSuccess;
-  if (ad_len) ok &= hipMemcpyAsync(d + o_ad, ad, ad_len, hipMemcpyHostToDevice, s) == hipSuccess;
-  if (open && tag_len)
-    ok &= hipMemcpyAsync(d + o_tag, tag, tag_len, hipMemcpyHostToDevice, s) == hipSuccess;
-  if (!ok) {
+  hipStream_t s = sc->stream;
+  uint8_t *d = sc->dev, *h = sc->host;
+  if (nonce_len) memcpy(h + o_nonce, nonce, nonce_len);
+  if (ad_len) memcpy(h + o_ad, ad, ad_len);
+  if (open && tag_len) memcpy(h + o_tag, tag, tag_len);
+  if (len) memcpy(h + o_in, in, len);
+  if (hipMemcpyAsync(d, h, o_in + len, hipMemcpyHostToDevice, s) != hipSuccess) {
     PUT_ERROR(ERR_R_INTERNAL_ERROR);
     return 0;
   }
@@ -381,17 +392,16 @@ int one_record(const EVP_AEAD_CTX *ctx, bool open, const uint8_t *in, uint8_t *o
   b.tags = d + o_tag;
   b.status = d + o_status;
   if (!run_batch(st->km, tag_len, &b, open, false, s)) return 0;
-  uint8_t status = 0;
-  ok = hipMemcpyAsync(&status, d + o_status, 1, hipMemcpyDeviceToHost, s) == hipSuccess;
-  if (len) ok &= hipMemcpyAsync(out, d + o_in, len, hipMemcpyDeviceToHost, s) == hipSuccess;
-  if (!open && tag_len)
-    ok &= hipMemcpyAsync(tag, d + o_tag, tag_len, hipMemcpyDeviceToHost, s) == hipSuccess;
+  bool ok = hipMemcpyAsync(h + o_tag, d + o_tag, o_in - o_tag + len, hipMemcpyDeviceToHost, s) ==
+            hipSuccess;
   ok &= hipStreamSynchronize(s) == hipSuccess;
   if (!ok) {
     PUT_ERROR(ERR_R_INTERNAL_ERROR);
     return 0;
   }
-  if (!status) {
+  if (len) memcpy(out, h + o_in, len);
+  if (!open && tag_len) memcpy(tag, h + o_tag, tag_len);
+  if (!h[o_status]) {
     PUT_ERROR(open ? CIPHER_R_BAD_DECRYPT : CIPHER_R_TOO_LARGE);
     return 0;
   }
