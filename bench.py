@@ -437,8 +437,11 @@ def main():
 
     d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
     d_lens = torch.from_numpy(lens.astype(np.int64)).to(dev)
-    d_pt = torch.empty(max(1, sh.total_pad), dtype=torch.uint8, device=dev)
-    d_ct = torch.empty(max(1, sh.total_pad), dtype=torch.uint8, device=dev)
+    # Base offset of the record buffers within their allocation (bytes;
+    # BSSL_AMD_BASE_OFFSET, diagnostic): shifts every record's cache-line phase.
+    boff = int(os.environ.get("BSSL_AMD_BASE_OFFSET", 0))
+    d_pt = torch.empty(max(1, sh.total_pad) + boff, dtype=torch.uint8, device=dev)[boff:]
+    d_ct = torch.empty(max(1, sh.total_pad) + boff, dtype=torch.uint8, device=dev)[boff:]
     d_nonce = torch.empty(max(1, 12 * nrec), dtype=torch.uint8, device=dev)
     d_ad = torch.empty(max(1, 13 * nrec), dtype=torch.uint8, device=dev)
     d_tags = torch.empty(max(1, 16 * nrec), dtype=torch.uint8, device=dev)
@@ -475,7 +478,7 @@ def main():
         # Seal once, then time opens of the sealed records into a third buffer
         # (tags verified every step).
         ctx.seal_batch_device(batch, stream)
-        d_back = torch.empty_like(d_pt)
+        d_back = torch.empty(d_pt.numel() + boff, dtype=torch.uint8, device=dev)[boff:]
         batch = ba.make_batch(nrec, d_ct, d_back, d_tags, d_nonce, nonce_len, d_ad,
                               offsets=None if uniform else d_offs,
                               lengths=None if uniform else d_lens,

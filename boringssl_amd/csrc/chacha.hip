@@ -416,12 +416,18 @@ __device__ __forceinline__ void crypt_block_x(const uint8_t *src, uint8_t *dst, 
 #ifndef BSSL_AMD_CHACHA_COAL
 #define BSSL_AMD_CHACHA_COAL 1
 #endif
+// Slot shift for 128-byte-aligned records (see `sh` in chacha_group).
+#ifndef BSSL_AMD_CHACHA_SHIFT
+#define BSSL_AMD_CHACHA_SHIFT 1
+#endif
 #ifndef BSSL_AMD_CHACHA_STAMPS
 #define BSSL_AMD_CHACHA_STAMPS 0
 #endif
 // Diagnostic ablations (wrong output; selected builds only): 1 = no input
 // loads in the block loop, 2 = no Poly1305 absorb in the loop, 3 = no ChaCha
-// rounds in the loop, 4 = no stores in the loop.
+// rounds in the loop, 4 = no stores in the loop (lane-per-block I/O); with
+// the record-contiguous I/O: 7 = no loads, 8 = no global stores in the loop
+// (the staged values are still read back).
 #ifndef BSSL_AMD_CHACHA_ABLATE
 #define BSSL_AMD_CHACHA_ABLATE 0
 #endif
@@ -511,6 +517,21 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   uint8_t *dst = b.out + m.off;
   const bool aligned = ((reinterpret_cast<uintptr_t>(src) |
                          reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+  // Slot u of the record (lane u mod L, iteration u / L) holds the Poly1305
+  // key block for u = 0 and data block d = u - 1 - sh for u >= 1 + sh (ChaCha
+  // counter d + 1).  sh = 1 leaves slot 1 idle so that, for a record on a
+  // 128-byte boundary, each iteration's 256-byte run (data blocks
+  // 4 it - 1 - sh ..) covers whole 128-byte lines instead of half lines at
+  // both ends (the other half written one iteration later); the Poly1305
+  // element order then starts with a zero element (Y_A at v = sh).
+  constexpr bool kCoalSh = BSSL_AMD_CHACHA_COAL && BSSL_AMD_CHACHA_SHIFT && L == 4;
+  // (Wave-uniform: 1 only if every live record of the wave is 128-byte
+  // aligned, so the slot arithmetic stays scalar.)
+  const uint64_t live_mask = __ballot(live);
+  const uint32_t sh =
+      kCoalSh && live_mask &&
+              __ballot(live && ((reinterpret_cast<uintptr_t>(dst) & 127) == 0)) == live_mask
+          ? 1u : 0u;
   // LDS: one 64-byte block per thread (the first ciphertext block while the
   // powers of r are built, then the staging area of the coalesced record
   // I/O: record slot r of the wave at r * 256, block q at + 64 q, its 16-byte
@@ -526,7 +547,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   const int rslot = lane / L;
   if (kCoal && q == 0) {
     const uint32_t nfull = live && aligned ? (uint32_t)(m.len / 64) : 0u;
-    s_rinfo[threadIdx.x / L] = make_uint4((uint32_t)m.off, (uint32_t)(m.off >> 32), nfull, 0u);
+    s_rinfo[threadIdx.x / L] = make_uint4((uint32_t)m.off, (uint32_t)(m.off >> 32), nfull, sh);
   }
   auto saddr = [](int r, int qq, int j) { return r * 256 + qq * 64 + ((j + qq + r) & 3) * 16; };
 
@@ -535,8 +556,8 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   // Input of data block d = u-1 when it is a full aligned 64-byte block
   // (issued before the ChaCha rounds so the HBM latency hides under them).
   auto prefetch = [&](uint64_t u, uint4 pre[4]) {
-    const uint64_t d = u - 1;
-    if (u >= 1 && u <= nblk && aligned && m.len >= 64 * d + 64) {
+    const uint64_t d = u - 1 - sh;
+    if (u >= 1 + sh && d < nblk && aligned && m.len >= 64 * d + 64) {
 #if BSSL_AMD_CHACHA_ABLATE == 1
       if (u >= (uint64_t)L) {
 #pragma unroll
@@ -551,7 +572,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   };
   auto crypt_block = [&](uint64_t u, const uint32_t ks[16], const uint4 pre[4], uint32_t c[16],
                          bool staged) {
-    const uint64_t d = u - 1;
+    const uint64_t d = u - 1 - sh;
     const uint64_t rem = vlen - 64 * d;
     uint32_t x[16], y[16];
     if (kCoal && staged && m.len >= 64 * d + 64 && aligned) {
@@ -625,13 +646,13 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   };
 
   // Iteration 0: lane 0 computes the Poly1305 key block (counter 0,
-  // e_chacha20poly1305.cc:89-93), lanes 1..L-1 the data blocks 0..L-2.
-  const int iters = wave_max((int)((nblk + 1 + L - 1) / L));
+  // e_chacha20poly1305.cc:89-93), lanes 1+sh..L-1 the data blocks 0..L-2-sh.
+  const int iters = wave_max((int)((nblk + 1 + sh + L - 1) / L));
   uint32_t ks[16], c0[16];
   uint4 pre[4];
   prefetch((uint64_t)q, pre);
-  chacha_block(key, (uint32_t)q, nonce, ks);
-  const bool have0 = q >= 1 && (uint64_t)q <= nblk;
+  chacha_block(key, (uint32_t)q >= 1 + sh ? (uint32_t)q - sh : 0u, nonce, ks);
+  const bool have0 = (uint32_t)q >= 1 + sh && (uint64_t)q - sh <= nblk;
   if (have0) crypt_block((uint64_t)q, ks, pre, c0, false);
   CSTAMP(1);
   if (BSSL_AMD_CHACHA_PRIO) __builtin_amdgcn_s_setprio(0);
@@ -717,6 +738,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     };
     if (wmax <= 1) {
       if (nab == 1) ya = pblock(adw[0], adw[1], adw[2], adw[3]);  // block 0 (lane 0's)
+      if (kCoalSh) ya = pshfl(ya, 0, L);  // lane sh takes Y_A
     } else {
       P acc = pzero();
       for (uint64_t k = q; k < nab; k += L)
@@ -736,10 +758,10 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
 
   // Absorb data block d = u-1: a full unit folds into acc (acc*R^L + U with
   // lazy reduction), the trailing partial unit is kept in `tail`.
-  P acc = (q == 0 && live) ? ya : pzero();
+  P acc = ((uint32_t)q == sh && live) ? ya : pzero();
   P tail = pzero();
   auto absorb = [&](uint64_t u, const uint32_t c[16]) {
-    const uint64_t d = u - 1;
+    const uint64_t d = u - 1 - sh;
     if (d < nunits) {
       PAcc t = pacc_zero();
       uint32_t ap[36];
@@ -786,7 +808,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     uint32_t slot = wbase / L + 4 * k + (lane >> 4);
     asm volatile("" : "+v"(slot));  // re-read per use, not hoisted (registers)
     const uint4 inf = s_rinfo[slot];
-    const uint64_t dd = (uint64_t)it * 4 + cq - 1;
+    const uint64_t dd = (uint64_t)it * 4 + cq - 1 - inf.w;  // (it >= 1: no wrap)
     addr = ((uint64_t)inf.y << 32 | inf.x) + 64 * dd + 16 * cj;
     return dd < inf.z;
   };
@@ -808,7 +830,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
         uint64_t a;
         const int r = 4 * k + (lane >> 4);
         const int j = (cj - cq - r) & 3;
-        if (coal_addr(k, it, a))
+        if (BSSL_AMD_CHACHA_ABLATE != 7 && coal_addr(k, it, a))
           __builtin_amdgcn_global_load_lds(
               reinterpret_cast<const void *>(b.in + a - 16 * cj + 16 * j),
               reinterpret_cast<__attribute__((address_space(3))) void *>(
@@ -822,7 +844,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
 #pragma unroll
     for (int i = 0; i < 16; i++) ks[i] = key[i & 7] ^ (uint32_t)u ^ nonce[i % 3];
 #else
-    chacha_block_raw(kl, (uint32_t)u, nonce, ks);
+    chacha_block_raw(kl, (uint32_t)(u - sh), nonce, ks);
 #endif
     if constexpr (kCoal) {
       // vmcnt(0): the LDS-DMA loads have landed.  The keystream words are
@@ -833,7 +855,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
                    "v"(ks[10]), "v"(ks[11]), "v"(ks[12]), "v"(ks[13]), "v"(ks[14]), "v"(ks[15])
                    : "memory");
     }
-    if (u <= nblk) {
+    if (u - sh <= nblk) {
       uint32_t c[16];
       crypt_block(u, ks, pre, c, true);
 #if BSSL_AMD_CHACHA_ABLATE == 2
@@ -846,9 +868,13 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         uint64_t a;
-        if (coal_addr(k, it, a))
-          *reinterpret_cast<uint4 *>(b.out + a) =
-              *reinterpret_cast<const uint4 *>(stage + saddr(4 * k + (lane >> 4), cq, cj));
+        if (coal_addr(k, it, a)) {
+          const uint4 v = *reinterpret_cast<const uint4 *>(stage + saddr(4 * k + (lane >> 4), cq, cj));
+          if (BSSL_AMD_CHACHA_ABLATE == 8)
+            asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+          else
+            *reinterpret_cast<uint4 *>(b.out + a) = v;
+        }
       }
     }
   }
@@ -857,7 +883,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   // Combine the lanes: M = nunits + 1 virtual elements; lane p takes the
   // accumulator of lane (p + M mod L) and the tree weights position p by
   // R^(L-1-p).
-  P z = pshfl(acc, (q + (int)((nunits + 1) % L)) & (L - 1), L);
+  P z = pshfl(acc, (q + (int)((nunits + 1 + sh) % L)) & (L - 1), L);
 #pragma unroll
   for (int t = 0; t < kLog; t++) {
     const int sh = 1 << t;
@@ -866,7 +892,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     if ((q & (2 * sh - 1)) == 0) z = padd(mm, o);
   }
   // Z = X * r^t + tail (tail held by the lane of unit `nunits`).
-  tail = pshfl(tail, (int)((nunits + 1) % L), L);
+  tail = pshfl(tail, (int)((nunits + 1 + sh) % L), L);
   const int tmax = wave_max((int)tail_blocks);
   for (int k = 0; k < tmax; k++)
     if ((uint32_t)k < tail_blocks) z = pmul(z, pwr(0));
