@@ -423,8 +423,17 @@ def main():
     import boringssl_amd as ba  # fails loudly without the HIP library
 
     dist = _dist()
+    # Rehearsal on fewer GPUs than ranks (diagnostic; BSSL_AMD_REHEARSE_DEVICES
+    # = k): rank r uses GPU r mod k, and the timing collectives run over gloo
+    # (RCCL does not put two ranks of one communicator on one GPU).
+    rehearse = int(os.environ.get("BSSL_AMD_REHEARSE_DEVICES", "0"))
+    if rehearse:
+        local %= rehearse
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     torch.cuda.set_device(local)
     ba.set_device(local)
     dev = torch.device(f"cuda:{local}")
