@@ -420,6 +420,14 @@ __device__ __forceinline__ void crypt_block_x(const uint8_t *src, uint8_t *dst, 
 #ifndef BSSL_AMD_CHACHA_SHIFT
 #define BSSL_AMD_CHACHA_SHIFT 1
 #endif
+// Ciphertext stores with the non-temporal hint: +2.3 % on config 3 (same-box
+// A/B); NT_LOAD sets the non-temporal cache policy on the LDS-DMA loads.
+#ifndef BSSL_AMD_CHACHA_NT_STORE
+#define BSSL_AMD_CHACHA_NT_STORE 1
+#endif
+#ifndef BSSL_AMD_CHACHA_NT_LOAD
+#define BSSL_AMD_CHACHA_NT_LOAD 0
+#endif
 #ifndef BSSL_AMD_CHACHA_STAMPS
 #define BSSL_AMD_CHACHA_STAMPS 0
 #endif
@@ -835,7 +843,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
               reinterpret_cast<const void *>(b.in + a - 16 * cj + 16 * j),
               reinterpret_cast<__attribute__((address_space(3))) void *>(
                   reinterpret_cast<uintptr_t>(stage + 1024 * k)),
-              16, 0, 0);
+              16, 0, BSSL_AMD_CHACHA_NT_LOAD ? 2 : 0);  // aux 2: nt (gfx950 CPol)
       }
     } else {
       prefetch(u, pre);
@@ -873,7 +881,17 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
           if (BSSL_AMD_CHACHA_ABLATE == 8)
             asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
           else
+          {
+#if BSSL_AMD_CHACHA_NT_STORE  // non-temporal ciphertext stores
+            uint4 *o = reinterpret_cast<uint4 *>(b.out + a);
+            __builtin_nontemporal_store(v.x, &o->x);
+            __builtin_nontemporal_store(v.y, &o->y);
+            __builtin_nontemporal_store(v.z, &o->z);
+            __builtin_nontemporal_store(v.w, &o->w);
+#else
             *reinterpret_cast<uint4 *>(b.out + a) = v;
+#endif
+          }
         }
       }
     }

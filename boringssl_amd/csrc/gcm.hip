@@ -57,6 +57,14 @@ constexpr int kWaves = BSSL_AMD_GCM_WAVES;
 #ifndef BSSL_AMD_GCM_STAMPS
 #define BSSL_AMD_GCM_STAMPS 0
 #endif
+// Plaintext loads and ciphertext stores with the non-temporal hint (each byte
+// is touched once): +1.7 % on config 2 (same-box A/B, 3 rounds).
+#ifndef BSSL_AMD_GCM_NT_STORE
+#define BSSL_AMD_GCM_NT_STORE 1
+#endif
+#ifndef BSSL_AMD_GCM_NT_LOAD
+#define BSSL_AMD_GCM_NT_LOAD 1
+#endif
 #if BSSL_AMD_GCM_STAMPS
 // Diagnostic build: per-wave cycle counts of the T-table kernel's loop and
 // AES rounds (s_memtime, with its own lgkmcnt wait), printed per wave 0.
@@ -922,7 +930,15 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
 #if BSSL_AMD_ABLATE == 3 || BSSL_AMD_ABLATE == 4  // diagnostic: no plaintext loads
     v = make_uint4((uint32_t)j, 1, 2, 3);
 #else
-    if (j < nfull) v = *reinterpret_cast<const uint4 *>(src + j * 16);
+    if (j < nfull) {
+#if BSSL_AMD_GCM_NT_LOAD  // non-temporal plaintext loads
+      const uint4 *ip = reinterpret_cast<const uint4 *>(src + j * 16);
+      v = make_uint4(__builtin_nontemporal_load(&ip->x), __builtin_nontemporal_load(&ip->y),
+                     __builtin_nontemporal_load(&ip->z), __builtin_nontemporal_load(&ip->w));
+#else
+      v = *reinterpret_cast<const uint4 *>(src + j * 16);
+#endif
+    }
 #endif
     return v;
   };
@@ -985,7 +1001,17 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
       asm volatile("" ::"v"(y.x), "v"(y.y), "v"(y.z), "v"(y.w));
 #else
     if (j < nfull) {
+#if BSSL_AMD_GCM_NT_STORE  // non-temporal ciphertext stores
+      {
+        uint4 *o = reinterpret_cast<uint4 *>(dst + j * 16);
+        __builtin_nontemporal_store(y.x, &o->x);
+        __builtin_nontemporal_store(y.y, &o->y);
+        __builtin_nontemporal_store(y.z, &o->z);
+        __builtin_nontemporal_store(y.w, &o->w);
+      }
+#else
       *reinterpret_cast<uint4 *>(dst + j * 16) = y;
+#endif
 #endif
     } else if (j < nb) {
       const uint32_t n = (uint32_t)min<uint64_t>(m.len + m.xlen - j * 16, 16);
