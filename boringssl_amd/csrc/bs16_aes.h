@@ -1,0 +1,112 @@
+// bs16_aes.h -- bitsliced AES on 16 blocks per lane, two state columns per
+// register (gfx950 VALU).  Register (r, h, b) holds bit b of state row r for
+// column h in its low 16 bits (block n in bit n) and for column h + 2 in its
+// high 16 bits (block n in bit 16 + n): 64 VGPRs of state, and every SubBytes
+// / MixColumns operation still works on 32 bit-slots.  See gcm.hip
+// (gcm_mix_kernel) and DESIGN.md §4.2c.
+#pragma once
+#include "bs_aes.h"
+
+namespace bssl_amd {
+
+__device__ __forceinline__ uint32_t swap16(uint32_t v) {
+  return __builtin_amdgcn_perm(v, v, 0x01000302u);
+}
+
+// Round-key mask of register (r, h, b): bit b of row r of round-key columns h
+// (low half) and h + 2 (high half), spread to 0 / 0xffff per half.
+__device__ __forceinline__ uint32_t bs16_kmask(const uint32_t w[4], int r, int h, int b) {
+  const uint32_t lo = (w[h] >> (8 * r + b)) & 1u, hi = (w[h + 2] >> (8 * r + b)) & 1u;
+  return (lo | (hi << 16)) * 0xffffu;
+}
+
+// MixColumns + AddRoundKey of column pair h (bs_mix_column's network).
+// km[r][b]: the round key's masks of this pair (bs16_kmask, or the key's
+// precomputed GcmKeyDev::rk_bs16 row).
+__device__ __forceinline__ void bs16_mix(const uint32_t a[4][8], uint32_t o[4][8],
+                                         const uint32_t km[4][8]) {
+  uint32_t t[8];
+#pragma unroll
+  for (int b = 0; b < 8; b++) t[b] = bs_xor3(a[0][b], a[1][b], a[2][b]) ^ a[3][b];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const uint32_t *x = a[r], *y = a[(r + 1) & 3];
+    uint32_t v[8];
+#pragma unroll
+    for (int b = 0; b < 8; b++) v[b] = bs_xor3(t[b], x[b], km[r][b]);
+    const uint32_t u7 = x[7] ^ y[7];
+    o[r][0] = u7 ^ v[0];
+    o[r][1] = bs_xor3(x[0], y[0], u7) ^ v[1];
+    o[r][2] = bs_xor3(x[1], y[1], v[2]);
+    o[r][3] = bs_xor3(x[2], y[2], u7) ^ v[3];
+    o[r][4] = bs_xor3(x[3], y[3], u7) ^ v[4];
+    o[r][5] = bs_xor3(x[4], y[4], v[5]);
+    o[r][6] = bs_xor3(x[5], y[5], v[6]);
+    o[r][7] = bs_xor3(x[6], y[6], v[7]);
+  }
+}
+
+// AES rounds 1..NR on the 16-block register pairs (round 0 is in p already).
+// Row r of new pair h comes from old pair (h + r) & 1, half-swapped when
+// ((h + r) >> 1) & 1 (ShiftRows on the column pairs {h, h + 2}).
+// MT: round-key masks read from the key's precomputed table `mk`
+// (GcmKeyDev::rk_bs16, scalar loads) instead of derived from the round-key
+// words `rkp` on the scalar unit (~10 SALU operations per mask).
+template <int NR, bool MT>
+__device__ __forceinline__ void bs16_cipher(uint32_t (&p)[4][2][8],
+                                            const uint32_t *__restrict__ rkp,
+                                            const uint32_t *__restrict__ mk) {
+#pragma unroll 1
+  for (int rd = 1; rd <= NR; rd++) {
+    uint32_t w[4] = {0, 0, 0, 0};
+    if constexpr (!MT) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) w[i] = (uint32_t)__builtin_amdgcn_readfirstlane(rkp[4 * rd + i]);
+    }
+    auto kmask = [&](int r, int h, int b) -> uint32_t {
+      if constexpr (MT)
+        return (uint32_t)__builtin_amdgcn_readfirstlane(mk[64 * rd + (r * 2 + h) * 8 + b]);
+      else
+        return bs16_kmask(w, r, h, b);
+    };
+    const bool last = rd == NR;
+    uint32_t np[4][2][8];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      uint32_t a[4][8];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        sbox_planes(p[r][(h + r) & 1], a[r]);
+        if (((h + r) >> 1) & 1) {
+#pragma unroll
+          for (int b = 0; b < 8; b++) a[r][b] = swap16(a[r][b]);
+        }
+      }
+      if (!last) {
+        uint32_t km[4][8], o[4][8];
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+          for (int b = 0; b < 8; b++) km[r][b] = kmask(r, h, b);
+        bs16_mix(a, o, km);
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+          for (int b = 0; b < 8; b++) np[r][h][b] = o[r][b];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+          for (int b = 0; b < 8; b++) np[r][h][b] = a[r][b] ^ kmask(r, h, b);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int b = 0; b < 8; b++) p[r][h][b] = np[r][h][b];
+  }
+}
+
+}  // namespace bssl_amd

@@ -34,6 +34,7 @@
 
 #include "internal.h"
 #include "bs_aes.h"
+#include "bs16_aes.h"
 
 #ifndef BSSL_AMD_ABLATE
 #define BSSL_AMD_ABLATE 0
@@ -83,6 +84,14 @@ struct StampVec {
 };
 constexpr int kRecPerWave = 4;
 // Tiled (multi-key) path: rotating wave priorities (process_records RP).
+// Mixed-role kernel: raise the T-table waves' issue priority (knob).
+// bs16 round-key masks from the key's table (1) or the SALU (0).
+#ifndef BSSL_AMD_BS16_MASKTAB
+#define BSSL_AMD_BS16_MASKTAB 1
+#endif
+#ifndef BSSL_AMD_GCM_MIX_PRIO
+#define BSSL_AMD_GCM_MIX_PRIO 0
+#endif
 #ifndef BSSL_AMD_GCM_TILE_RP
 #define BSSL_AMD_GCM_TILE_RP 1
 #endif
@@ -1577,6 +1586,229 @@ __global__ __launch_bounds__(512, 2) void gcm_hy_kernel(const GcmKeyDev *__restr
   }
 }
 
+// ---------------------------------------------------------------------------
+// Mixed-role one-key kernel: the T-table role and a
+// bitsliced role that fits the T-table kernel's 128-VGPR allocation, so both
+// share each SIMD at 4 waves.  The bitsliced role (bs16) encrypts 16 blocks
+// per lane with two state columns per register: register (r, h, b) holds bit
+// b of state row r for column h in its low 16 bits (block n in bit n) and for
+// column h + 2 in its high 16 bits (block n in bit 16 + n) -- 64 VGPRs of
+// state instead of 128, and every SubBytes / MixColumns operation still works
+// on 32 bit-slots.  ShiftRows maps row r of column c to column c - r: for the
+// register pairs that is a renaming plus a swap of the two halves (rot16) of
+// 4 of the 8 (row, pair) groups per round.
+
+// Keystream words of pair h: word n (< 16) = column h of block n, word
+// 16 + n = column h + 2 of block n.
+__device__ __forceinline__ v32u bs16_words(const uint32_t (&p)[4][2][8], int h) {
+  uint32_t o[32];
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+#pragma unroll
+    for (int b = 0; b < 8; b++) o[8 * r + b] = p[r][h][b];
+  transpose32_fast(o);
+  v32u v;
+#pragma unroll
+  for (int n = 0; n < 32; n++) v[n] = o[n];
+  return v;
+}
+
+__device__ __forceinline__ uint4 load_blk_nt(const uint8_t *p) {
+#if BSSL_AMD_GCM_NT_LOAD
+  const uint4 *ip = reinterpret_cast<const uint4 *>(p);
+  return make_uint4(__builtin_nontemporal_load(&ip->x), __builtin_nontemporal_load(&ip->y),
+                    __builtin_nontemporal_load(&ip->z), __builtin_nontemporal_load(&ip->w));
+#else
+  return *reinterpret_cast<const uint4 *>(p);
+#endif
+}
+
+__device__ __forceinline__ void store_blk_nt(uint8_t *p, uint4 y) {
+#if BSSL_AMD_GCM_NT_STORE
+  uint4 *o = reinterpret_cast<uint4 *>(p);
+  __builtin_nontemporal_store(y.x, &o->x);
+  __builtin_nontemporal_store(y.y, &o->y);
+  __builtin_nontemporal_store(y.z, &o->z);
+  __builtin_nontemporal_store(y.w, &o->w);
+#else
+  *reinterpret_cast<uint4 *>(p) = y;
+#endif
+}
+
+// The (up to) 4 records of a wave with the bs16 engine.  Lane q owns blocks
+// j = 256*c + 16*n + q (n = 0..15) of chunk c -- the T-table role's lane
+// algebra, so GHASH (multiplier H^16, the LDS byte table) and finish_record
+// are shared.  Records must be 16-byte aligned multiples of 16 bytes (the
+// caller checks; no extra bytes).
+template <int NR, bool OPEN>
+__device__ __forceinline__ void process_records_bs16(const uint32_t *__restrict__ rkp,
+                                                     const uint32_t *__restrict__ mk,
+                                                     const BatchDesc &b,
+                                                     const RecState *__restrict__ st, uint64_t rec,
+                                                     bool active, const RecordMeta &m0,
+                                                     const uint8_t *smem, const uint8_t *gtab,
+                                                     uint32_t mf0) {
+  // Register budget: the rounds need ~100 VGPRs, so little else may stay live
+  // across them -- the per-lane GHASH constants, J0 and the record metadata
+  // are re-derived (laundered through empty asm so they are not hoisted)
+  // after the rounds and at the end of the record.
+  RecState s;
+  s.j0 = s.ya = make_uint4(0, 0, 0, 0);
+  s.live = 0;
+  if (active) {
+    s.j0 = st[rec].j0;
+    s.ya = st[rec].ya;
+    s.live = st[rec].live;
+  }
+  const bool live = active && s.live;
+  const uint32_t nb = live ? (uint32_t)(m0.len / 16) : 0u;  // nb < 2^32 (GCM length limit)
+  const uint8_t *src = b.in + m0.off;
+  uint8_t *dst = b.out + m0.off;
+  uint4 acc = ((threadIdx.x & 15) == 15 && live) ? s.ya : make_uint4(0, 0, 0, 0);
+  const int nchunks = wave_max((int)((nb + 255) / 256));
+#pragma unroll 1
+  for (int c = 0; c < nchunks; c++) {
+    uint32_t p[4][2][8];
+    {
+      // Round 0.  Pair 0 = columns 0 and 2 of J0 ^ rk0 (per-lane constants:
+      // 0 / 0xffff per half); pair 1 = column 1 (constant, low half) and the
+      // counter words of column 3 (high half), both out of one transpose:
+      // t[n] = column 1, t[16 + n] = word 3 of block n.
+      uint64_t rr = rec;
+      asm volatile("" : "+v"(rr));
+      const uint4 j0 = active ? st[rr].j0 : make_uint4(0, 0, 0, 0);
+      uint32_t rk0[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) rk0[i] = (uint32_t)__builtin_amdgcn_readfirstlane(rkp[i]);
+      const uint32_t w0 = j0.x ^ rk0[0], w1 = j0.y ^ rk0[1], w2 = j0.z ^ rk0[2];
+#pragma unroll
+      for (int k = 0; k < 32; k++)
+        p[k / 8][0][k % 8] = (bit_mask(w0, k) & 0xffffu) | (bit_mask(w2, k) & 0xffff0000u);
+      const uint32_t jc = 256u * (uint32_t)c + (threadIdx.x & 15u);
+      const uint32_t cb = bswap32(j0.w) + 1u + jc;  // inc32: mod 2^32
+      uint32_t t[32];
+#pragma unroll
+      for (int n = 0; n < 16; n++) {
+        t[n] = w1;
+        t[16 + n] = bswap32(cb + 16u * (uint32_t)n) ^ rk0[3];
+      }
+      transpose32_fast(t);
+#pragma unroll
+      for (int k = 0; k < 32; k++) p[k / 8][1][k % 8] = t[k];
+    }
+    bs16_cipher<NR, BSSL_AMD_BS16_MASKTAB != 0>(p, rkp, mk);
+    uint32_t q = threadIdx.x & 15u;
+    asm volatile("" : "+v"(q));
+    const uint32_t jc = 256u * (uint32_t)c + q;
+    const bool rs1 = (q >> 2) & 1, rs2 = (q >> 3) & 1;
+    const uint32_t rbs = q & 3u;
+    uint32_t P[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) v |= (((4u * k + i + q) & 15u) << 4) << (8 * i);
+      P[k] = v;
+    }
+    auto load_blk = [&](uint32_t j) {
+      return load_blk_nt(src + (uint64_t)(j < nb ? j : 0u) * 16);
+    };
+    uint4 x0 = load_blk(jc);
+    v32u KA = bs16_words(p, 0), KB = bs16_words(p, 1);
+    const int nv = (int)min(16u, jc < nb ? (nb - jc + 15u) / 16u : 0u);
+    // Pass 1 (memory): out = in ^ keystream, input one block ahead; the
+    // ciphertext (the output when sealing, the input when opening) replaces
+    // the keystream in KA/KB.
+#pragma unroll 1
+    for (int n = 0; n < 16; n++) {
+      const uint32_t j = jc + 16u * (uint32_t)n;
+      const uint4 x1 = load_blk(j + 16u);  // (past the chunk: clamped, unused)
+      const uint4 y = xor4(x0, make_uint4(KA[n], KB[n], KA[16 + n], KB[16 + n]));
+      if (j < nb) store_blk_nt(dst + (uint64_t)j * 16, y);
+      const uint4 cb = OPEN ? x0 : y;
+      KA[n] = cb.x;
+      KB[n] = cb.y;
+      KA[16 + n] = cb.z;
+      KB[16 + n] = cb.w;
+      x0 = x1;
+    }
+    // Pass 2 (LDS): acc = acc * H^16 ^ C over the lane's valid blocks.
+#pragma unroll 1
+    for (int n = 0; n < 16; n++) {
+      const uint4 hm = g8_mul(acc, rs1, rs2, rbs, P, smem);
+      if (n < nv) acc = xor4(hm, make_uint4(KA[n], KB[n], KA[16 + n], KB[16 + n]));
+    }
+  }
+  uint64_t rr = rec;
+  asm volatile("" : "+v"(rr));
+  RecordMeta m = {0, 0, 0, 0, 0};
+  if (active) {
+    m = record_meta(b, rr);
+    s = st[rr];
+  }
+  finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, gtab, mf0);
+}
+
+// One-key kernel with NB bs16 waves (the last NB of 16; waves w, w+4, ...
+// share a SIMD, so NB = 4 puts one on each SIMD) beside 16 - NB T-table
+// waves, all at 128 VGPRs.  Every wave takes 4-record units from one grid-wide
+// counter; a bs16 wave hands a unit to the T-table engine when any of its
+// records is unaligned, not a multiple of 16 bytes, or shorter than 4 KiB.
+template <int NR, bool OPEN, int NB>
+__global__ __launch_bounds__(1024) void gcm_mix_kernel(const GcmKeyDev *__restrict__ keys,
+                                                        BatchDesc b,
+                                                        const RecState *__restrict__ st,
+                                                        uint32_t *__restrict__ units) {
+  constexpr int kThreads = 1024;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsPlan];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  for (int e = tid; e < 256 * 64; e += kThreads) {
+    const int idx = e >> 6, slot = (e >> 5) & 1;
+    const uint32_t v = kTables.te0[idx];
+    reinterpret_cast<uint32_t *>(smem + kLdsAes)[e] = slot ? rotl(v, 8) : v;
+  }
+  build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab[4]), tid);
+  __syncthreads();
+  const uint8_t *gtab = reinterpret_cast<const uint8_t *>(keys[0].htab);
+  const uint32_t *rkp = &keys[0].rk_plain[0][0];
+  const uint64_t n = b.num_records;
+  const bool role_b = wave >= 16 - NB;
+#if BSSL_AMD_GCM_MIX_PRIO
+  if (!role_b) __builtin_amdgcn_s_setprio(1);
+#endif
+  RoundKeys rk;
+#pragma unroll
+  for (int r = 0; r <= NR; r++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) rk.w[r][c] = keys[0].rk[r][c];
+  const uint32_t lc0 = kLdsAes + (uint32_t)(lane & 31) * 4u, lc1 = lc0 + 128u;
+  StampVec stamps = {{0, 0, 0, 0, 0, 0, 0, 0}};
+  for (;;) {
+    uint32_t u = 0;
+    if (lane == 0) u = atomicAdd(units, 1u);
+    u = __builtin_amdgcn_readfirstlane(__shfl(u, 0, 64));
+    const uint64_t first = (uint64_t)u * kRecPerWave;
+    if (first >= n) break;
+    const uint64_t i = first + g;
+    const bool active = i < n;
+    const uint64_t rec = active ? rec_at(b, i) : 0;
+    bool bs = false;
+    RecordMeta m = {0, 0, 0, 0, 0};
+    if (role_b) {
+      if (active) m = record_meta(b, rec);
+      const bool ok = !active || (((reinterpret_cast<uintptr_t>(b.in + m.off) |
+                                    reinterpret_cast<uintptr_t>(b.out + m.off) | m.len) & 15) == 0 &&
+                                  m.len >= 4096);
+      bs = __ballot(!ok) == 0;
+    }
+    if (bs)
+      process_records_bs16<NR, OPEN>(rkp, &keys[0].rk_bs16[0][0], b, st, rec, active, m, smem, gtab, 0xf0u);
+    else
+      process_records<NR, OPEN, false>(rk, b, st, rec, active, smem, gtab, lc0, lc1, 0xf0u,
+                                       stamps);
+  }
+}
+
 int g_num_cus = 0;
 
 
@@ -1589,6 +1821,12 @@ int gcm_mode(const BatchDesc &b) {
   int mode = 0;
   if (e && !strcmp(e, "bs")) mode = 1;
   if (e && !strcmp(e, "hybrid")) mode = 2;
+  // Mixed-role kernel (gcm_mix_kernel): its bs16 waves check their units'
+  // records themselves, so any one-key batch without extra bytes qualifies.
+  if (e && !strcmp(e, "mix4")) mode = 3;
+  if (e && !strcmp(e, "mix8")) mode = 4;
+  if (e && !strcmp(e, "bs16")) mode = 5;  // every wave bs16 (no T-tables on eligible units)
+  if (mode >= 3) return (b.extra_len || b.key_index) ? 0 : mode;
   if (!mode || b.lengths || b.offsets || b.extra_len || b.tag_stride || b.key_index) return 0;
   if ((b.record_len | b.record_stride | reinterpret_cast<uintptr_t>(b.in) |
        reinterpret_cast<uintptr_t>(b.out)) & 15)
@@ -1637,7 +1875,20 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
   const int mode = gcm_mode(b);
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
   const RecState *cst = st;
-  if (mode) {
+  if (mode >= 3) {
+    const uint64_t units_needed = (b.num_records + 4 * 16 - 1) / (4 * 16);
+    const unsigned grid = (unsigned)(units_needed < (uint64_t)g_num_cus ? units_needed
+                                                                       : (uint64_t)g_num_cus);
+    if (mode == 3)
+      hipLaunchKernelGGL((gcm_mix_kernel<NR, OPEN, 4>), dim3(grid), dim3(1024), 0, s, keys, bo,
+                         cst, units);
+    else if (mode == 4)
+      hipLaunchKernelGGL((gcm_mix_kernel<NR, OPEN, 8>), dim3(grid), dim3(1024), 0, s, keys, bo,
+                         cst, units);
+    else
+      hipLaunchKernelGGL((gcm_mix_kernel<NR, OPEN, 16>), dim3(grid), dim3(1024), 0, s, keys, bo,
+                         cst, units);
+  } else if (mode) {
     const uint64_t units_needed = (b.num_records + 4 * 8 - 1) / (4 * 8);
     const unsigned grid = (unsigned)(units_needed < (uint64_t)g_num_cus ? units_needed
                                                                        : (uint64_t)g_num_cus);

@@ -230,7 +230,7 @@ def test_batch_large_ragged_reordered(aead, multikey):
     assert st.all() and back == ins
 
 
-@pytest.mark.parametrize("mode", ["bs", "hybrid"])
+@pytest.mark.parametrize("mode", ["bs", "hybrid", "mix4", "mix8", "bs16"])
 @pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-192-gcm", "aes-256-gcm"])
 @pytest.mark.parametrize("rlen", [4096, 16384, 17408, 32768])
 def test_bitsliced_gcm_path(aead, rlen, mode, monkeypatch):
@@ -271,6 +271,35 @@ def test_bitsliced_gcm_path(aead, rlen, mode, monkeypatch):
     back = d_back.cpu().numpy()
     assert not back[7 * rlen:8 * rlen].any()
     assert np.array_equal(np.delete(back.reshape(n, rlen), 7, 0), np.delete(pt.reshape(n, rlen), 7, 0))
+
+
+@pytest.mark.parametrize("mode", ["mix4", "mix8", "bs16"])
+@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm"])
+def test_mix_kernel_ragged(aead, mode, monkeypatch):
+    """The mixed-role kernel (gcm_mix_kernel) on a ragged one-key batch: its
+    bitsliced waves take only units whose 4 records are 16-byte-aligned
+    multiples of 16 bytes of >= 4 KiB and hand the rest to the T-table engine
+    -- every record must match the oracle either way, sealed and opened."""
+    monkeypatch.setenv("BSSL_AMD_GCM_MODE", mode)
+    rng = random.Random(len(mode) * 7 + len(aead))
+    key = bytes(rng.getrandbits(8) for _ in range(AEAD_KEYLEN[aead]))
+    n = 600
+    lens = []
+    for i in range(n):
+        k = rng.randrange(4)
+        lens.append(16 * rng.randrange(256, 1200) if k < 3 else rng.randrange(0, 9000))
+    ins = [rng.randbytes(L) for L in lens]
+    nonces = [rng.randbytes(12) for _ in range(n)]
+    ads = [rng.randbytes(rng.randrange(0, 40)) for _ in range(n)]
+    for odd in (0, 4):
+        outs, tags, st = run_batch(aead, [key], None, ins, nonces, ads, 16, odd=odd)
+        assert st.all()
+        for i in range(n):
+            ok, ct, tag = o.seal(ORACLE_ID[aead], key, nonces[i], ins[i], ads[i])
+            assert ok and outs[i] == ct and tags[i] == tag, (odd, i, lens[i])
+        back, _, st = run_batch(aead, [key], None, outs, nonces, ads, 16, open_=True, tags=tags,
+                                odd=odd)
+        assert st.all() and back == ins
 
 
 def test_batch_gcm_nonce_lengths_and_truncated_tags():

@@ -19,7 +19,7 @@ def main():
     n = int(os.environ.get("N", 1 << 20))
     L = int(os.environ.get("LEN", 16384))
     aead = os.environ.get("AEAD", "aes-128-gcm")
-    modes = sys.argv[1:] or ["table", "bs", "hybrid"]
+    modes = sys.argv[1:] or ["table", "mix4", "mix8", "bs", "hybrid"]
     dev = torch.device("cuda:0")
     torch.cuda.set_device(0)
     offs = torch.from_numpy(np.arange(n, dtype=np.int64) * L).to(dev)
