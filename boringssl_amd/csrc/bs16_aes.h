@@ -21,8 +21,7 @@ __device__ __forceinline__ uint32_t bs16_kmask(const uint32_t w[4], int r, int h
 }
 
 // MixColumns + AddRoundKey of column pair h (bs_mix_column's network).
-// km[r][b]: the round key's masks of this pair (bs16_kmask, or the key's
-// precomputed GcmKeyDev::rk_bs16 row).
+// km[r][b]: the round key's masks of this pair (bs16_kmask).
 __device__ __forceinline__ void bs16_mix(const uint32_t a[4][8], uint32_t o[4][8],
                                          const uint32_t km[4][8]) {
   uint32_t t[8];
@@ -49,26 +48,18 @@ __device__ __forceinline__ void bs16_mix(const uint32_t a[4][8], uint32_t o[4][8
 // AES rounds 1..NR on the 16-block register pairs (round 0 is in p already).
 // Row r of new pair h comes from old pair (h + r) & 1, half-swapped when
 // ((h + r) >> 1) & 1 (ShiftRows on the column pairs {h, h + 2}).
-// MT: round-key masks read from the key's precomputed table `mk`
-// (GcmKeyDev::rk_bs16, scalar loads) instead of derived from the round-key
-// words `rkp` on the scalar unit (~10 SALU operations per mask).
-template <int NR, bool MT>
+// Round keys: the FIPS-197 words of round rd (wave-uniform), spread into the
+// per-register masks on the scalar unit.  (A per-key table of the 64 masks
+// per round, read by scalar loads, measured the same.)
+template <int NR>
 __device__ __forceinline__ void bs16_cipher(uint32_t (&p)[4][2][8],
-                                            const uint32_t *__restrict__ rkp,
-                                            const uint32_t *__restrict__ mk) {
+                                            const uint32_t *__restrict__ rkp) {
 #pragma unroll 1
   for (int rd = 1; rd <= NR; rd++) {
-    uint32_t w[4] = {0, 0, 0, 0};
-    if constexpr (!MT) {
+    uint32_t w[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++) w[i] = (uint32_t)__builtin_amdgcn_readfirstlane(rkp[4 * rd + i]);
-    }
-    auto kmask = [&](int r, int h, int b) -> uint32_t {
-      if constexpr (MT)
-        return (uint32_t)__builtin_amdgcn_readfirstlane(mk[64 * rd + (r * 2 + h) * 8 + b]);
-      else
-        return bs16_kmask(w, r, h, b);
-    };
+    for (int i = 0; i < 4; i++) w[i] = (uint32_t)__builtin_amdgcn_readfirstlane(rkp[4 * rd + i]);
+    auto kmask = [&](int r, int h, int b) { return bs16_kmask(w, r, h, b); };
     const bool last = rd == NR;
     uint32_t np[4][2][8];
 #pragma unroll

@@ -85,10 +85,6 @@ struct StampVec {
 constexpr int kRecPerWave = 4;
 // Tiled (multi-key) path: rotating wave priorities (process_records RP).
 // Mixed-role kernel: raise the T-table waves' issue priority (knob).
-// bs16 round-key masks from the key's table (1) or the SALU (0).
-#ifndef BSSL_AMD_BS16_MASKTAB
-#define BSSL_AMD_BS16_MASKTAB 1
-#endif
 #ifndef BSSL_AMD_GCM_MIX_PRIO
 #define BSSL_AMD_GCM_MIX_PRIO 0
 #endif
@@ -1642,7 +1638,6 @@ __device__ __forceinline__ void store_blk_nt(uint8_t *p, uint4 y) {
 // caller checks; no extra bytes).
 template <int NR, bool OPEN>
 __device__ __forceinline__ void process_records_bs16(const uint32_t *__restrict__ rkp,
-                                                     const uint32_t *__restrict__ mk,
                                                      const BatchDesc &b,
                                                      const RecState *__restrict__ st, uint64_t rec,
                                                      bool active, const RecordMeta &m0,
@@ -1696,7 +1691,7 @@ __device__ __forceinline__ void process_records_bs16(const uint32_t *__restrict_
 #pragma unroll
       for (int k = 0; k < 32; k++) p[k / 8][1][k % 8] = t[k];
     }
-    bs16_cipher<NR, BSSL_AMD_BS16_MASKTAB != 0>(p, rkp, mk);
+    bs16_cipher<NR>(p, rkp);
     uint32_t q = threadIdx.x & 15u;
     asm volatile("" : "+v"(q));
     const uint32_t jc = 256u * (uint32_t)c + q;
@@ -1802,7 +1797,7 @@ __global__ __launch_bounds__(1024) void gcm_mix_kernel(const GcmKeyDev *__restri
       bs = __ballot(!ok) == 0;
     }
     if (bs)
-      process_records_bs16<NR, OPEN>(rkp, &keys[0].rk_bs16[0][0], b, st, rec, active, m, smem, gtab, 0xf0u);
+      process_records_bs16<NR, OPEN>(rkp, b, st, rec, active, m, smem, gtab, 0xf0u);
     else
       process_records<NR, OPEN, false>(rk, b, st, rec, active, smem, gtab, lc0, lc1, 0xf0u,
                                        stamps);

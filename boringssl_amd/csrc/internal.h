@@ -2,8 +2,8 @@
 //
 // Device data layout (all resident in HBM, 16-byte aligned):
 //
-//   GcmKeyDev   one per AES-GCM key (53,488 bytes): the AES round keys (T-table,
-//               plain and bs16-mask forms) and the GHASH multiplication tables for
+//   GcmKeyDev   one per AES-GCM key (49,648 bytes): the AES round keys (T-table
+//               and plain forms) and the GHASH multiplication tables for
 //               H, H^2, H^4, H^8, H^16, H^32.
 //               Equivalent of the reference's GCM128_KEY
 //               (crypto/fipsmodule/aes/internal.h:325-334), re-laid-out for the
@@ -36,12 +36,8 @@ struct alignas(16) GcmKeyDev {
   // little-endian words of the 16 GCM-order bytes.  Nibble position
   // pos = 2*k + 0 is the high nibble of byte k, 2*k + 1 the low nibble.
   uint32_t htab[kGhashPowers][32][16][4];
-  // Round-key masks of the bs16 engine (gcm.hip gcm_mix_kernel, bs16_aes.h):
-  // rk_bs16[r][(row * 2 + h) * 8 + b] = bit b of round key r's byte (row, h)
-  // spread over the low 16 bits | that of byte (row, h + 2) over the high 16.
-  uint32_t rk_bs16[15][64];
 };
-static_assert(sizeof(GcmKeyDev) == 240 + 16 + 240 + kGhashPowers * 8192 + 15 * 256, "layout");
+static_assert(sizeof(GcmKeyDev) == 240 + 16 + 240 + kGhashPowers * 8192, "layout");
 
 struct alignas(16) ChaChaKeyDev {
   uint32_t k[8];

@@ -172,14 +172,6 @@ bool gcm_key_setup(const uint8_t *key, size_t key_len, GcmKeyDev *out) {
       out->rk[r][c] = (r == 0 || r == nr) ? v : rotl32(v, 16);
       out->rk_plain[r][c] = v;
     }
-  for (int r = 0; r <= nr; r++)
-    for (int row = 0; row < 4; row++)
-      for (int h = 0; h < 2; h++)
-        for (int b = 0; b < 8; b++) {
-          const uint32_t lo = (w[16 * r + 4 * h + row] >> b) & 1u;
-          const uint32_t hi = (w[16 * r + 4 * (h + 2) + row] >> b) & 1u;
-          out->rk_bs16[r][(row * 2 + h) * 8 + b] = (lo | (hi << 16)) * 0xffffu;
-        }
   uint8_t hb[16] = {0};
   encrypt_block(w, nr, hb, hb);  // H = E_K(0^128), gcm.cc.inc:270-272
   U128 p = load_u128(hb);
