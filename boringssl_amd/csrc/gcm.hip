@@ -66,6 +66,13 @@ constexpr int kWaves = BSSL_AMD_GCM_WAVES;
 #ifndef BSSL_AMD_GCM_NT_LOAD
 #define BSSL_AMD_GCM_NT_LOAD 1
 #endif
+// Plaintext loads under the block's branch (1) or unconditional with a
+// clamped address (0, which lets hipcc count the outstanding memory
+// operations instead of draining them with vmcnt(0) once per iteration pair;
+// measured 0.6 % slower on config 2 -- the drain is not what binds).
+#ifndef BSSL_AMD_GCM_COND_LOAD
+#define BSSL_AMD_GCM_COND_LOAD 1
+#endif
 #if BSSL_AMD_GCM_STAMPS
 // Diagnostic build: per-wave cycle counts of the T-table kernel's loop and
 // AES rounds (s_memtime, with its own lgkmcnt wait), printed per wave 0.
@@ -571,6 +578,46 @@ __device__ __forceinline__ uint4 gmul(uint4 x, const uint8_t *tab, uint32_t mf0)
   return r;
 }
 
+// x * (the power whose nibble tables start at `tab`) with the tables in
+// GLOBAL memory (the record-end tree and tag of finish_record, which read the
+// key's L2-resident copy): the 16 lookups of two words are issued back to back
+// and XORed after one wait -- two memory round trips per product.  (Through
+// gmul, whose grouping targets LDS reads, hipcc issued them two at a time with
+// a vmcnt(0) after each pair: 16 round trips per product, 6 products per
+// record.)
+template <int W0>
+__device__ __forceinline__ uint4 gmul_gwords(uint4 r, uint32_t v0, uint32_t v1, const uint8_t *tab,
+                                             uint32_t mf0) {
+  uint4 t[16];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint32_t v = h ? v1 : v0, l = v << 4;
+    const uint8_t *tw = tab + (8 * (W0 + h)) * 256;
+    t[8 * h + 0] = tab128<0 * 256>(tw, nib<0>(v, mf0));
+    t[8 * h + 1] = tab128<1 * 256>(tw, nib<0>(l, mf0));
+    t[8 * h + 2] = tab128<2 * 256>(tw, nib<1>(v, mf0));
+    t[8 * h + 3] = tab128<3 * 256>(tw, nib<1>(l, mf0));
+    t[8 * h + 4] = tab128<4 * 256>(tw, nib<2>(v, mf0));
+    t[8 * h + 5] = tab128<5 * 256>(tw, nib<2>(l, mf0));
+    t[8 * h + 6] = tab128<6 * 256>(tw, nib<3>(v, mf0));
+    t[8 * h + 7] = tab128<7 * 256>(tw, nib<3>(l, mf0));
+  }
+  __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);  // address VALU
+  __builtin_amdgcn_sched_group_barrier(0x020, 16, 0);  // the 16 VMEM reads
+#pragma unroll
+  for (int i = 0; i < 16; i += 2) r = xor4_3(r, t[i], t[i + 1]);
+  return r;
+}
+
+__device__ __forceinline__ uint4 gmul_global(uint4 x, const uint8_t *tab, uint32_t mf0) {
+  uint4 r = make_uint4(0, 0, 0, 0);
+  r = gmul_gwords<0>(r, x.x, x.y, tab, mf0);
+  __builtin_amdgcn_sched_barrier(0);
+  r = gmul_gwords<2>(r, x.z, x.w, tab, mf0);
+  __builtin_amdgcn_sched_barrier(0);
+  return r;
+}
+
 // Runtime power index (prologue, tree).
 __device__ __forceinline__ uint4 gmul_pow(uint4 x, const uint8_t *tab, int p, uint32_t mf0) {
   return gmul<0>(x, tab + p * 8192, mf0);
@@ -714,6 +761,28 @@ __device__ __forceinline__ uint4 crypt_partial_x(const uint8_t *src, uint8_t *ds
   return y;
 }
 
+__device__ __forceinline__ uint4 load_blk_nt(const uint8_t *p) {
+#if BSSL_AMD_GCM_NT_LOAD
+  const uint4 *ip = reinterpret_cast<const uint4 *>(p);
+  return make_uint4(__builtin_nontemporal_load(&ip->x), __builtin_nontemporal_load(&ip->y),
+                    __builtin_nontemporal_load(&ip->z), __builtin_nontemporal_load(&ip->w));
+#else
+  return *reinterpret_cast<const uint4 *>(p);
+#endif
+}
+
+__device__ __forceinline__ void store_blk_nt(uint8_t *p, uint4 y) {
+#if BSSL_AMD_GCM_NT_STORE
+  uint4 *o = reinterpret_cast<uint4 *>(p);
+  __builtin_nontemporal_store(y.x, &o->x);
+  __builtin_nontemporal_store(y.y, &o->y);
+  __builtin_nontemporal_store(y.z, &o->z);
+  __builtin_nontemporal_store(y.w, &o->w);
+#else
+  *reinterpret_cast<uint4 *>(p) = y;
+#endif
+}
+
 // Record at processing position i (sched.hip's length order, if any).
 __device__ __forceinline__ uint64_t rec_at(const BatchDesc &b, uint64_t i) {
   return b.order ? b.order[i] : i;
@@ -800,6 +869,17 @@ __global__ __launch_bounds__(256) void gcm_prologue(const GcmKeyDev *__restrict_
 // p holds the lane whose weight is H^(L-1-p), then tree-combine with
 // H, H^2, ..., H^(L/2) (nibble tables 0..log2(L)-1 at `tab`: LDS or the key's
 // global copy).
+// The record-end products: `tab` is the key's global copy of the nibble
+// tables (gmul_global; gmul in the
+// round-1 path for A/B (BSSL_AMD_GCM_FIN_GMUL=0).
+#ifndef BSSL_AMD_GCM_FIN_GMUL
+#define BSSL_AMD_GCM_FIN_GMUL 1
+#endif
+#if BSSL_AMD_GCM_FIN_GMUL
+#define GMUL_FIN(x, tab, mf0) gmul_global(x, tab, mf0)
+#else
+#define GMUL_FIN(x, tab, mf0) gmul<0>(x, tab, mf0)
+#endif
 template <bool OPEN, int L>
 __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const RecordMeta &m,
                                               const RecState &s, const BatchDesc &b, uint64_t rec,
@@ -816,7 +896,7 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
   for (int t = 0; t < kLevels; t++) {
     const int sh = 1 << t;
     const uint4 o = shfl_down4(a, sh, L);
-    const uint4 mlt = gmul<0>(a, tab + t * 8192, mf0);
+    const uint4 mlt = GMUL_FIN(a, tab + t * 8192, mf0);
     if ((q & (2 * sh - 1)) == 0) a = xor4(mlt, o);
   }
   // Tag (gcm.cc.inc:576-604): ((Z*H) ^ len block) * H ^ E_K(J0), in lane 0.
@@ -825,7 +905,7 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
                          bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits));
 #pragma unroll 1
   for (int t = 0; t < 2; t++) {
-    a = xor4(gmul<0>(a, tab, mf0), add);
+    a = xor4(GMUL_FIN(a, tab, mf0), add);
     add = s.ek0;
   }
   const uint4 tag = a;
@@ -930,20 +1010,17 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   // (Left undefined when not loaded: such a block is never stored or hashed
   // from this value, and a zero-fill would be a VALU write that the waitcnt
   // pass orders after the previous store.)
+  // BSSL_AMD_GCM_COND_LOAD=0 issues the load unconditionally (a block past
+  // the record's full blocks reads the batch's RecState array instead, a
+  // valid 16-byte-aligned address whose value is never used).
   auto load_full = [&](uint64_t j) {
     uint4 v;
 #if BSSL_AMD_ABLATE == 3 || BSSL_AMD_ABLATE == 4  // diagnostic: no plaintext loads
     v = make_uint4((uint32_t)j, 1, 2, 3);
+#elif BSSL_AMD_GCM_COND_LOAD
+    if (j < nfull) v = load_blk_nt(src + j * 16);
 #else
-    if (j < nfull) {
-#if BSSL_AMD_GCM_NT_LOAD  // non-temporal plaintext loads
-      const uint4 *ip = reinterpret_cast<const uint4 *>(src + j * 16);
-      v = make_uint4(__builtin_nontemporal_load(&ip->x), __builtin_nontemporal_load(&ip->y),
-                     __builtin_nontemporal_load(&ip->z), __builtin_nontemporal_load(&ip->w));
-#else
-      v = *reinterpret_cast<const uint4 *>(src + j * 16);
-#endif
-    }
+    v = load_blk_nt(j < nfull ? src + j * 16 : reinterpret_cast<const uint8_t *>(st));
 #endif
     return v;
   };
@@ -1607,28 +1684,6 @@ __device__ __forceinline__ v32u bs16_words(const uint32_t (&p)[4][2][8], int h) 
 #pragma unroll
   for (int n = 0; n < 32; n++) v[n] = o[n];
   return v;
-}
-
-__device__ __forceinline__ uint4 load_blk_nt(const uint8_t *p) {
-#if BSSL_AMD_GCM_NT_LOAD
-  const uint4 *ip = reinterpret_cast<const uint4 *>(p);
-  return make_uint4(__builtin_nontemporal_load(&ip->x), __builtin_nontemporal_load(&ip->y),
-                    __builtin_nontemporal_load(&ip->z), __builtin_nontemporal_load(&ip->w));
-#else
-  return *reinterpret_cast<const uint4 *>(p);
-#endif
-}
-
-__device__ __forceinline__ void store_blk_nt(uint8_t *p, uint4 y) {
-#if BSSL_AMD_GCM_NT_STORE
-  uint4 *o = reinterpret_cast<uint4 *>(p);
-  __builtin_nontemporal_store(y.x, &o->x);
-  __builtin_nontemporal_store(y.y, &o->y);
-  __builtin_nontemporal_store(y.z, &o->z);
-  __builtin_nontemporal_store(y.w, &o->w);
-#else
-  *reinterpret_cast<uint4 *>(p) = y;
-#endif
 }
 
 // The (up to) 4 records of a wave with the bs16 engine.  Lane q owns blocks
