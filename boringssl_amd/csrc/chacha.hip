@@ -428,6 +428,9 @@ __device__ __forceinline__ void crypt_block_x(const uint8_t *src, uint8_t *dst, 
 #ifndef BSSL_AMD_CHACHA_NT_LOAD
 #define BSSL_AMD_CHACHA_NT_LOAD 0
 #endif
+#ifndef BSSL_AMD_CHACHA_META_BRANCH
+#define BSSL_AMD_CHACHA_META_BRANCH 0
+#endif
 #ifndef BSSL_AMD_CHACHA_STAMPS
 #define BSSL_AMD_CHACHA_STAMPS 0
 #endif
@@ -444,6 +447,19 @@ __device__ __forceinline__ void crypt_block_x(const uint8_t *src, uint8_t *dst, 
 #else
 #define CSTAMP(i)
 #endif
+// Per-record metadata without branches: a missing array (null pointer, the
+// uniform-layout fields apply) is read at kMetaZero instead, so every load is
+// issued unconditionally and they are all in flight together.  (Under the
+// null-pointer branches hipcc waited for each load before issuing the next:
+// ~8 serialized memory round trips per wave before its first block.)
+__device__ const uint64_t kMetaZero[2] = {0, 0};
+
+template <typename T>
+__device__ __forceinline__ T meta_load(const T *arr, uint64_t i, bool active) {
+  const T *p = arr && active ? arr + i : reinterpret_cast<const T *>(kMetaZero);
+  return *p;
+}
+
 // One wave group: records pos = grp * (64 / L) + lane / L.
 template <bool OPEN, int L, bool XT, bool XC>
 __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ keys,
@@ -459,6 +475,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   const int q = lane & (L - 1);
   const uint64_t pos = grp * (64 / L) + lane / L;
   const bool active = pos < b.num_records;
+#if BSSL_AMD_CHACHA_META_BRANCH  // (the round-1 form, for A/B)
   const uint64_t rec = active && b.order ? b.order[pos] : pos;  // sched.hip order
   RecordMeta m = {0, 0, 0, 0};
   uint32_t kidx = 0;
@@ -469,26 +486,51 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     m.ad_len = b.ad_lengths ? b.ad_lengths[rec] : b.ad_len;
     kidx = b.key_index ? b.key_index[rec] : 0u;
   }
+  const uint8_t vld = active && b.valid ? b.valid[rec] : 1;
+#else
+  uint8_t vld = 1;
+  const uint32_t ord = meta_load(b.order, pos, active);
+  const uint64_t rec = active && b.order ? (uint64_t)ord : pos;  // sched.hip order
+  RecordMeta m = {0, 0, 0, 0};
+  uint32_t kidx = 0;
+  {
+    const uint64_t off = meta_load(b.offsets, rec, active), len = meta_load(b.lengths, rec, active);
+    const uint64_t ado = meta_load(b.ad_offsets, rec, active);
+    const uint64_t adl = meta_load(b.ad_lengths, rec, active);
+    const uint32_t ki = meta_load(b.key_index, rec, active);
+    vld = meta_load(b.valid, rec, active);
+    if (active) {
+      m.off = b.offsets ? off : rec * b.record_stride;
+      m.len = b.lengths ? len : b.record_len;
+      m.ad_off = b.ad_offsets ? ado : rec * b.ad_stride;
+      m.ad_len = b.ad_lengths ? adl : b.ad_len;
+      kidx = b.key_index ? ki : 0u;
+    }
+  }
+#endif
   // e_chacha20poly1305.cc:127-142: 12-byte nonce, < 2^32 - 1 blocks
   // (XChaCha20-Poly1305: 24-byte nonce, :241-244).
   constexpr uint32_t kNonceLen = XC ? 24 : 12;
   const bool bad = active && (kidx >= b.num_keys || b.nonce_len != kNonceLen ||
                               m.len + b.extra_len >= (uint64_t(1) << 32) * 64 - 64 ||
-                              (b.valid && !b.valid[rec]));
+                              (b.valid && !vld));
   const bool live = active && !bad;
   uint32_t key[8], nonce[3];
   {
     const ChaChaKeyDev *kp = keys + (live ? kidx : 0u);
 #pragma unroll
     for (int i = 0; i < 8; i++) key[i] = kp->k[i];
-    const uint8_t *np = b.nonces + (live ? rec * kNonceLen : 0);
+    // (Addressed as soon as the record index is known, not after the
+    // validity checks: any in-range record's nonce is readable.)
+    const bool nok = active && b.nonce_len == kNonceLen;
+    const uint8_t *np = b.nonces + (nok ? rec * kNonceLen : 0);
     constexpr int kWords = kNonceLen / 4;
     uint32_t nw[kWords];
 #pragma unroll
     for (int i = 0; i < kWords; i++)
-      nw[i] = live && (reinterpret_cast<uintptr_t>(np) & 3) == 0
+      nw[i] = nok && (reinterpret_cast<uintptr_t>(np) & 3) == 0
                   ? reinterpret_cast<const uint32_t *>(np)[i]
-                  : load_le32_bytes(np + 4 * i, live ? 4 : 0);
+                  : load_le32_bytes(np + 4 * i, nok ? 4 : 0);
     if constexpr (XC) {
       // key' = HChaCha20(key, nonce[0:16]), nonce' = 0^4 || nonce[16:24]
       // (e_chacha20poly1305.cc:248-252).

@@ -714,12 +714,37 @@ struct RecordMeta {
   uint32_t xlen;
 };
 
+// Per-record arrays read without branches: a missing array (null pointer,
+// the uniform-layout field applies) is read at kMetaZero instead, so the
+// loads are issued together.  (Under the null-pointer branches hipcc waited
+// for each load before issuing the next.)
+__device__ const uint64_t kMetaZero[2] = {0, 0};
+
+template <typename T>
+__device__ __forceinline__ T meta_load(const T *arr, uint64_t i) {
+  const T *p = arr ? arr + i : reinterpret_cast<const T *>(kMetaZero);
+  return *p;
+}
+
+#ifndef BSSL_AMD_GCM_META_BRANCH
+#define BSSL_AMD_GCM_META_BRANCH 0
+#endif
 __device__ __forceinline__ RecordMeta record_meta(const BatchDesc &b, uint64_t i) {
   RecordMeta m;
+#if BSSL_AMD_GCM_META_BRANCH  // (the round-1 form, for A/B)
   m.off = b.offsets ? b.offsets[i] : i * b.record_stride;
   m.len = b.lengths ? b.lengths[i] : b.record_len;
   m.ad_off = b.ad_offsets ? b.ad_offsets[i] : i * b.ad_stride;
   m.ad_len = b.ad_lengths ? b.ad_lengths[i] : b.ad_len;
+  m.xlen = b.extra_len;
+  return m;
+#endif
+  const uint64_t off = meta_load(b.offsets, i), len = meta_load(b.lengths, i);
+  const uint64_t ado = meta_load(b.ad_offsets, i), adl = meta_load(b.ad_lengths, i);
+  m.off = b.offsets ? off : i * b.record_stride;
+  m.len = b.lengths ? len : b.record_len;
+  m.ad_off = b.ad_offsets ? ado : i * b.ad_stride;
+  m.ad_len = b.ad_lengths ? adl : b.ad_len;
   m.xlen = b.extra_len;
   return m;
 }
@@ -785,7 +810,8 @@ __device__ __forceinline__ void store_blk_nt(uint8_t *p, uint4 y) {
 
 // Record at processing position i (sched.hip's length order, if any).
 __device__ __forceinline__ uint64_t rec_at(const BatchDesc &b, uint64_t i) {
-  return b.order ? b.order[i] : i;
+  const uint32_t o = meta_load(b.order, i);
+  return b.order ? (uint64_t)o : i;
 }
 
 
