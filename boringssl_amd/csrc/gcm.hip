@@ -824,12 +824,65 @@ struct alignas(16) RecState {
 };
 
 // ---------------------------------------------------------------------------
+// One AES block with a compact T-table (prologue): tab[2*x] = T0[x],
+// tab[2*x + 1] = T1[x] = rotl8(T0[x]) in 2 KiB of LDS -- the round algebra of
+// aes_round / aes_rounds (middle round keys pre-rotated by 16), addressed by
+// byte * 8 + slot * 4 instead of the bank-replicated layout of the bulk
+// kernel, so the one-thread-per-record prologue is not held to two
+// workgroups per CU by a 64 KiB LDS declaration.
+template <int K, int SLOT>
+__device__ __forceinline__ uint32_t ctl(const uint32_t *tab, uint32_t s) {
+  return tab[2 * __builtin_amdgcn_ubfe(s, 8 * K, 8) + SLOT];
+}
+
+template <int NR>
+__device__ __forceinline__ uint4 aes_block_compact(uint4 in, const RoundKeys &rk,
+                                                   const uint32_t *tab) {
+  uint32_t s0 = in.x ^ rk.w[0][0], s1 = in.y ^ rk.w[0][1], s2 = in.z ^ rk.w[0][2],
+           s3 = in.w ^ rk.w[0][3];
+#pragma unroll
+  for (int r = 1; r < NR; r++) {
+    const uint32_t *rkx = rk.w[r];
+    const uint32_t t0 = xor3(ctl<0, 0>(tab, s0), ctl<1, 1>(tab, s1),
+                             rotl(xor3(ctl<2, 0>(tab, s2), ctl<3, 1>(tab, s3), rkx[0]), 16));
+    const uint32_t t1 = xor3(ctl<0, 0>(tab, s1), ctl<1, 1>(tab, s2),
+                             rotl(xor3(ctl<2, 0>(tab, s3), ctl<3, 1>(tab, s0), rkx[1]), 16));
+    const uint32_t t2 = xor3(ctl<0, 0>(tab, s2), ctl<1, 1>(tab, s3),
+                             rotl(xor3(ctl<2, 0>(tab, s0), ctl<3, 1>(tab, s1), rkx[2]), 16));
+    const uint32_t t3 = xor3(ctl<0, 0>(tab, s3), ctl<1, 1>(tab, s0),
+                             rotl(xor3(ctl<2, 0>(tab, s1), ctl<3, 1>(tab, s2), rkx[3]), 16));
+    s0 = t0;
+    s1 = t1;
+    s2 = t2;
+    s3 = t3;
+  }
+  // Last round: S[x] is byte 1 (and byte 2) of Te0[x].
+  auto last = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+    return xor3(__builtin_amdgcn_perm(ctl<1, 0>(tab, b), ctl<0, 0>(tab, a), 0x0c0c0501u),
+                __builtin_amdgcn_perm(ctl<3, 0>(tab, d), ctl<2, 0>(tab, c), 0x06020c0cu), k);
+  };
+  return make_uint4(last(s0, s1, s2, s3, rk.w[NR][0]), last(s1, s2, s3, s0, rk.w[NR][1]),
+                    last(s2, s3, s0, s1, rk.w[NR][2]), last(s3, s0, s1, s2, rk.w[NR][3]));
+}
+
+#ifndef BSSL_AMD_GCM_PRO_COMPACT
+#define BSSL_AMD_GCM_PRO_COMPACT 1
+#endif
+
+// ---------------------------------------------------------------------------
 // Prologue: one thread per record.  J0 (incl. the GHASH-derived J0 of a
 // non-96-bit nonce), E_K(J0) and the AD hash -- the per-record constant work
 // of CRYPTO_gcm128_init_ctx / _aad (gcm.cc.inc:298-398).
 template <int NR>
 __global__ __launch_bounds__(256) void gcm_prologue(const GcmKeyDev *__restrict__ keys,
                                                     BatchDesc b, RecState *__restrict__ st) {
+#if BSSL_AMD_GCM_PRO_COMPACT
+  __shared__ uint32_t ctab[512];
+  for (int e = threadIdx.x; e < 512; e += blockDim.x) {
+    const uint32_t v = kTables.te0[e >> 1];
+    ctab[e] = (e & 1) ? rotl(v, 8) : v;
+  }
+#else
   __shared__ __attribute__((aligned(16))) uint8_t smem[kAesLdsBytes];
   // Only replica 0 of T0/T1 (lane constant 0 / 128): conflicts do not matter here.
   for (int e = threadIdx.x; e < 512; e += blockDim.x) {
@@ -837,6 +890,7 @@ __global__ __launch_bounds__(256) void gcm_prologue(const GcmKeyDev *__restrict_
     const uint32_t v = kTables.te0[idx];
     reinterpret_cast<uint32_t *>(smem)[idx * 64 + (e & 1) * 32] = (e & 1) ? rotl(v, 8) : v;
   }
+#endif
   __syncthreads();
   const uint64_t rec = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (rec >= b.num_records) return;
@@ -875,8 +929,12 @@ __global__ __launch_bounds__(256) void gcm_prologue(const GcmKeyDev *__restrict_
                     htab, 0, mf0);
     }
     s.j0 = j0;
+#if BSSL_AMD_GCM_PRO_COMPACT
+    s.ek0 = aes_block_compact<NR>(j0, rk, ctab);
+#else
     s.ek0 = aes_rounds<NR, 0>(j0.x ^ rk.w[0][0], j0.y ^ rk.w[0][1], j0.z ^ rk.w[0][2],
                               j0.w ^ rk.w[0][3], rk, smem, 0u, 128u);
+#endif
     const uint8_t *ad = b.ad + m.ad_off;
     uint4 ya = make_uint4(0, 0, 0, 0);
     for (uint64_t o = 0; o < m.ad_len; o += 16) {
