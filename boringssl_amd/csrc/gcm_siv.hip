@@ -423,6 +423,17 @@ __device__ __forceinline__ uint4 rev(uint4 x) { return make_uint4(x.w, x.z, x.y,
 #else
 #define SIV_OCC
 #endif
+#ifndef BSSL_AMD_SIV_META_BRANCH
+#define BSSL_AMD_SIV_META_BRANCH 0
+#endif
+__device__ const uint64_t kSivMetaZero[2] = {0, 0};
+
+template <typename T>
+__device__ __forceinline__ T siv_meta(const T *arr, uint64_t i, bool active) {
+  const T *p = arr && active ? arr + i : reinterpret_cast<const T *>(kSivMetaZero);
+  return *p;
+}
+
 template <int NR, bool OPEN>
 __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyDev *__restrict__ keys,
                                                            BatchDesc b) {
@@ -449,6 +460,7 @@ __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyD
   const bool active = rec < b.num_records;
   uint64_t off = 0, len = 0, ad_off = 0, ad_len = 0;
   uint32_t kidx = 0;
+#if BSSL_AMD_SIV_META_BRANCH  // (the round-1 form, for A/B)
   if (active) {
     off = b.offsets ? b.offsets[rec] : rec * b.record_stride;
     len = b.lengths ? b.lengths[rec] : b.record_len;
@@ -456,12 +468,36 @@ __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyD
     ad_len = b.ad_lengths ? b.ad_lengths[rec] : b.ad_len;
     kidx = b.key_index ? b.key_index[rec] : 0u;
   }
+  const uint8_t vld = active && b.valid ? b.valid[rec] : 1;
+#else
+  // Branch-free: a missing array is read at kSivMetaZero, so these loads and
+  // the nonce's are in flight together (under the null-pointer branches hipcc
+  // waited for each before issuing the next).
+  {
+    const uint64_t o = siv_meta(b.offsets, rec, active), l = siv_meta(b.lengths, rec, active);
+    const uint64_t ao = siv_meta(b.ad_offsets, rec, active);
+    const uint64_t al = siv_meta(b.ad_lengths, rec, active);
+    const uint32_t ki = siv_meta(b.key_index, rec, active);
+    if (active) {
+      off = b.offsets ? o : rec * b.record_stride;
+      len = b.lengths ? l : b.record_len;
+      ad_off = b.ad_offsets ? ao : rec * b.ad_stride;
+      ad_len = b.ad_lengths ? al : b.ad_len;
+      kidx = b.key_index ? ki : 0u;
+    }
+  }
+  const uint8_t vld = siv_meta(b.valid, rec, active);
+#endif
   // e_aesgcmsiv.cc:794-808, 830-846.
   const bool live = active && kidx < b.num_keys && b.nonce_len == 12 && b.tag_len == 16 &&
                     len <= (uint64_t(1) << 36) && ad_len < (uint64_t(1) << 61) &&
-                    (!b.valid || b.valid[rec]);
-  const uint8_t *np = b.nonces + (live ? rec * 12 : 0);
-  const uint4 nw = live ? load_block(np, 12) : make_uint4(0, 0, 0, 0);
+                    (!b.valid || vld);
+  // (Addressed once the record index is known: any in-range record's nonce
+  // is readable when nonce_len is 12.)
+  const bool nok = active && b.nonce_len == 12;
+  const uint8_t *np = b.nonces + (nok ? rec * 12 : 0);
+  uint4 nw = nok ? load_block(np, 12) : make_uint4(0, 0, 0, 0);
+  if (!live) nw = make_uint4(0, 0, 0, 0);
 
   // gcm_siv_keys (e_aesgcmsiv.cc:750-780): AES_K(le32(i) || nonce)[0:8].
   constexpr int kKeyBlocks = NR == 14 ? 6 : 4;
