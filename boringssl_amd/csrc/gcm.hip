@@ -1101,6 +1101,17 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     uint4 v;
 #if BSSL_AMD_ABLATE == 3 || BSSL_AMD_ABLATE == 4  // diagnostic: no plaintext loads
     v = make_uint4((uint32_t)j, 1, 2, 3);
+#elif BSSL_AMD_ABLATE == 7
+    // Diagnostic cost probe (wrong output): the plaintext goes to a per-wave
+    // LDS slot by LDS-DMA issued in asm (no wait) and is read back with
+    // ds_read_b128 -- the instruction cost of LDS-DMA staging.
+    {
+      const uint32_t slot = kLdsBytes + (threadIdx.x >> 6) * 1024u;
+      const uint8_t *gp = j < nfull ? src + j * 16 : reinterpret_cast<const uint8_t *>(st);
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off nt"
+                   :: "s"(__builtin_amdgcn_readfirstlane(slot)), "v"(gp) : "memory", "m0");
+      v = *reinterpret_cast<const uint4 *>(smem + slot + (threadIdx.x & 63) * 16);
+    }
 #elif BSSL_AMD_GCM_COND_LOAD
     if (j < nfull) v = load_blk_nt(src + j * 16);
 #else
@@ -1269,7 +1280,11 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
   constexpr int kThreads = W * 64;
   constexpr int kRecPerTile = W * kRecPerWave;
   static_assert(kRecPerTile <= 64, "one wave plans a tile with ballots");
+#if BSSL_AMD_ABLATE == 7
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes + 16 * 1024];
+#else
   __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
+#endif
   // Pass list of the current tile: key and 64-bit record mask per pass.
   uint32_t *s_pass_key = reinterpret_cast<uint32_t *>(smem + kLdsPlan);
   uint64_t *s_pass_mask = reinterpret_cast<uint64_t *>(smem + kLdsPlan + 64 * 4);
