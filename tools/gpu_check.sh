@@ -22,7 +22,7 @@ for s in $STEPS; do
     smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
     pytest) run pytest 1500 python -u -m pytest tests/ -v -m gpu -rf --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
-    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} ;;
     pmc)
       PB="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --records ${PMC_RECORDS:-262144} ${BENCH_ARGS:-}"
       run pmc_a 600 rocprofv3 --kernel-include-regex "${PMC_KERNEL:-gcm_kernel}" --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmc_a -o run --output-format csv -- $PB
