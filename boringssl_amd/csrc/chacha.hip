@@ -489,11 +489,18 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   const uint8_t vld = active && b.valid ? b.valid[rec] : 1;
 #else
   uint8_t vld = 1;
-  const uint32_t ord = meta_load(b.order, pos, active);
-  const uint64_t rec = active && b.order ? (uint64_t)ord : pos;  // sched.hip order
+  const uint64_t rec = active && b.order ? (uint64_t)b.order[pos] : pos;  // sched.hip order
   RecordMeta m = {0, 0, 0, 0};
   uint32_t kidx = 0;
-  {
+  if (!(b.offsets || b.lengths || b.ad_offsets || b.ad_lengths || b.key_index || b.valid)) {
+    // Uniform layout, one key: no per-record loads.
+    if (active) {
+      m.off = rec * b.record_stride;
+      m.len = b.record_len;
+      m.ad_off = rec * b.ad_stride;
+      m.ad_len = b.ad_len;
+    }
+  } else {
     const uint64_t off = meta_load(b.offsets, rec, active), len = meta_load(b.lengths, rec, active);
     const uint64_t ado = meta_load(b.ad_offsets, rec, active);
     const uint64_t adl = meta_load(b.ad_lengths, rec, active);

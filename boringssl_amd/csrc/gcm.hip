@@ -714,10 +714,11 @@ struct RecordMeta {
   uint32_t xlen;
 };
 
-// Per-record arrays read without branches: a missing array (null pointer,
-// the uniform-layout field applies) is read at kMetaZero instead, so the
-// loads are issued together.  (Under the null-pointer branches hipcc waited
-// for each load before issuing the next.)
+// Per-record arrays read without branches when the batch has any: a missing
+// array (null pointer, the uniform-layout field applies) is read at kMetaZero
+// instead, so the loads are issued together (under per-array null-pointer
+// branches hipcc waited for each load before issuing the next).  A batch with
+// none of them takes the uniform layout with no loads at all.
 __device__ const uint64_t kMetaZero[2] = {0, 0};
 
 template <typename T>
@@ -739,6 +740,14 @@ __device__ __forceinline__ RecordMeta record_meta(const BatchDesc &b, uint64_t i
   m.xlen = b.extra_len;
   return m;
 #endif
+  if (!(b.offsets || b.lengths || b.ad_offsets || b.ad_lengths)) {  // uniform layout: no loads
+    m.off = i * b.record_stride;
+    m.len = b.record_len;
+    m.ad_off = i * b.ad_stride;
+    m.ad_len = b.ad_len;
+    m.xlen = b.extra_len;
+    return m;
+  }
   const uint64_t off = meta_load(b.offsets, i), len = meta_load(b.lengths, i);
   const uint64_t ado = meta_load(b.ad_offsets, i), adl = meta_load(b.ad_lengths, i);
   m.off = b.offsets ? off : i * b.record_stride;
@@ -810,8 +819,7 @@ __device__ __forceinline__ void store_blk_nt(uint8_t *p, uint4 y) {
 
 // Record at processing position i (sched.hip's length order, if any).
 __device__ __forceinline__ uint64_t rec_at(const BatchDesc &b, uint64_t i) {
-  const uint32_t o = meta_load(b.order, i);
-  return b.order ? (uint64_t)o : i;
+  return b.order ? (uint64_t)b.order[i] : i;  // (one load; no order array: none)
 }
 
 

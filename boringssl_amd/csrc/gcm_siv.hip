@@ -473,7 +473,15 @@ __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyD
   // Branch-free: a missing array is read at kSivMetaZero, so these loads and
   // the nonce's are in flight together (under the null-pointer branches hipcc
   // waited for each before issuing the next).
-  {
+  uint8_t vld = 1;
+  if (!(b.offsets || b.lengths || b.ad_offsets || b.ad_lengths || b.key_index || b.valid)) {
+    if (active) {  // uniform layout, one key: no per-record loads
+      off = rec * b.record_stride;
+      len = b.record_len;
+      ad_off = rec * b.ad_stride;
+      ad_len = b.ad_len;
+    }
+  } else {
     const uint64_t o = siv_meta(b.offsets, rec, active), l = siv_meta(b.lengths, rec, active);
     const uint64_t ao = siv_meta(b.ad_offsets, rec, active);
     const uint64_t al = siv_meta(b.ad_lengths, rec, active);
@@ -485,8 +493,8 @@ __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyD
       ad_len = b.ad_lengths ? al : b.ad_len;
       kidx = b.key_index ? ki : 0u;
     }
+    vld = siv_meta(b.valid, rec, active);
   }
-  const uint8_t vld = siv_meta(b.valid, rec, active);
 #endif
   // e_aesgcmsiv.cc:794-808, 830-846.
   const bool live = active && kidx < b.num_keys && b.nonce_len == 12 && b.tag_len == 16 &&
