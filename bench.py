@@ -187,20 +187,41 @@ def _free_port():
     return port
 
 
-def launch_ranks(n, argv):
+def launch_ranks(n, argv, timeout=None):
     """Start n rank processes of this script (one per GPU) and wait for them.
     Runs before anything in this process touches a GPU; the children are
-    fresh processes (never exec).  Rank 0's stdout is passed through; if a
-    rank fails, the others are stopped.  Returns the exit code."""
+    fresh processes (never exec).  Rank 0's stdout is passed through; the other
+    ranks' stdout goes to temporary files whose last line is echoed to stderr
+    when the rank ends.  If a rank fails, or the whole launch exceeds `timeout`
+    seconds (BSSL_AMD_RANK_TIMEOUT, default 1800), every remaining rank is
+    terminated (then killed) and the exit code is non-zero (124 on timeout).
+    Returns the exit code."""
+    import tempfile
+    if timeout is None:
+        timeout = float(os.environ.get("BSSL_AMD_RANK_TIMEOUT", "1800"))
     port = _free_port()
-    procs = []
+    procs, logs = [], []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        log = None if r == 0 else tempfile.TemporaryFile(mode="w+")
+        logs.append(log)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
-                                      stdout=None if r == 0 else subprocess.DEVNULL))
+                                      stdout=log))
+
+    def stop_all(live):
+        for q in live:
+            q.terminate()
+        t_end = time.time() + 10
+        for q in live:
+            try:
+                q.wait(timeout=max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                q.kill()
+
     rc = 0
     live = list(procs)
+    deadline = time.time() + timeout
     while live:
         for p in list(live):
             code = p.poll()
@@ -209,12 +230,27 @@ def launch_ranks(n, argv):
             live.remove(p)
             if code != 0:
                 rc = rc or code
-                for q in live:
-                    q.terminate()
+                stop_all(live)
+                live = []
+                break
+        if live and time.time() > deadline:
+            print(f"bench.py: ranks still running after {timeout:.0f} s; stopping them",
+                  file=sys.stderr)
+            rc = 124
+            stop_all(live)
+            live = []
         time.sleep(0.05)
-    for p in procs:
+    for r, (p, log) in enumerate(zip(procs, logs)):
         p.wait()
-    return rc
+        if log is not None:
+            log.seek(0)
+            lines = [x for x in log.read().splitlines() if x.strip()]
+            log.close()
+            print(f"bench.py: rank {r} exit {p.returncode}; last line: "
+                  f"{lines[-1] if lines else '(none)'}", file=sys.stderr)
+        if p.returncode not in (0, None) and rc == 0:
+            rc = p.returncode
+    return rc if rc >= 0 else 128 - rc
 
 
 # ---------------------------------------------------------------------------
@@ -367,6 +403,155 @@ def load_profile(config, kernel_prefix):
 
 # ---------------------------------------------------------------------------
 
+class Workload:
+    """Device buffers and the batch descriptor of one rank's bench batch."""
+
+
+def build_workload(config, rank, world, records, dev, open_op=False):
+    """The rank's batch exactly as the bench times it: synthetic records
+    (oracle/synth.h) generated in HBM, uniform configs as a uniform layout
+    (record_stride / record_len, no per-record arrays), records aligned to
+    record_align() bytes; config 4 with per-record offsets/lengths; config 5 a
+    keyset with key_index.  open_op: seal once, then time opens of the sealed
+    batch into a third buffer.  Used by main() and by the parity tests
+    (tests/test_bench_layout.py), so the timed layout is the tested one."""
+    import torch
+    import boringssl_amd as ba
+    aead, key_len, _, length, scaling, _ = CONFIGS[config]
+    sh = shard_plan(config, rank, world, records)
+    first, lens, offs, nrec = sh.first, sh.lens, sh.offs, sh.n
+    padded = _pad16(lens, record_align(config))
+    w = Workload()
+    w.config, w.aead, w.shard, w.nrec, w.lens, w.offs = config, aead, sh, nrec, lens, offs
+    w.pt_bytes = int(lens.sum())
+    w.world = world
+    d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.astype(np.int64)).to(dev)
+    # Base offset of the record buffers within their allocation (bytes;
+    # BSSL_AMD_BASE_OFFSET, diagnostic): shifts every record's cache-line phase.
+    boff = int(os.environ.get("BSSL_AMD_BASE_OFFSET", 0))
+    # Zero-filled, so the padding between records is defined (the kernels never
+    # write it; the open check compares whole buffers).
+    w.d_pt = torch.zeros(max(1, sh.total_pad) + boff, dtype=torch.uint8, device=dev)[boff:]
+    w.d_ct = torch.zeros(max(1, sh.total_pad) + boff, dtype=torch.uint8, device=dev)[boff:]
+    d_nonce = torch.empty(max(1, 12 * nrec), dtype=torch.uint8, device=dev)
+    d_ad = torch.empty(max(1, 13 * nrec), dtype=torch.uint8, device=dev)
+    w.d_tags = torch.empty(max(1, 16 * nrec), dtype=torch.uint8, device=dev)
+    w.d_status = torch.zeros(max(1, nrec), dtype=torch.uint8, device=dev)
+    ba.synth_fill_device(first, nrec, d_offs, d_lens, w.d_pt, d_nonce, d_ad)
+    nonce_len = 12
+    if aead == "xchacha20-poly1305":  # 24-byte nonces (ref_tool.cc make_nonce)
+        a = d_nonce.view(-1, 12)
+        b = a.clone()
+        b[:, 4:] ^= 0xff
+        d_nonce, nonce_len = torch.cat([a, b], dim=1).contiguous().view(-1), 24
+    w.nonce_len = nonce_len
+    w.uniform = uniform = length != "mixed"
+    rpk = RECORDS_PER_KEY.get(config)
+    d_kidx = None
+    w.nkeys = 1
+    if rpk:
+        # The rank's keys: global key ids key_first .. (synth_key).
+        w.nkeys = sh.nkeys
+        ctx = ba.Keyset(aead, b"".join(synth_key(sh.key_first + k, key_len)
+                                       for k in range(sh.nkeys)), sh.nkeys, 16)
+        d_kidx = torch.from_numpy((np.arange(nrec) // rpk).astype(np.int32)).to(dev)
+    else:
+        ctx = ba.AEADCtx(aead, synth_key(0, key_len), 16)
+    w.ctx = ctx
+    w.stride = stride = int(padded[0]) if nrec else 16
+
+    def mk(src, dst):
+        return ba.make_batch(nrec, src, dst, w.d_tags, d_nonce, nonce_len, d_ad,
+                             offsets=None if uniform else d_offs,
+                             lengths=None if uniform else d_lens,
+                             record_stride=stride if uniform else 0,
+                             record_len=int(length) if uniform else 0,
+                             ad_stride=13, ad_len=13, status=w.d_status, key_index=d_kidx)
+    w.batch = mk(w.d_pt, w.d_ct)
+    w.op = ctx.seal_batch_device
+    torch.cuda.synchronize()
+    if open_op:
+        ctx.seal_batch_device(w.batch, torch.cuda.current_stream())
+        w.d_back = torch.zeros(w.d_pt.numel() + boff, dtype=torch.uint8, device=dev)[boff:]
+        w.batch = mk(w.d_ct, w.d_back)
+        w.op = ctx.open_batch_device
+        torch.cuda.synchronize()
+    return w
+
+
+def golden_entry(w):
+    """The reference digest entry (tests/golden/ref_digests.json) of the
+    rank's batch, or None: the batch must be the whole synthetic sequence of
+    some entry (same AEAD, key count, records per key, length), starting at
+    record 0."""
+    if w.shard.first != 0 or w.shard.key_first != 0:
+        return None
+    path = os.path.join(ROOT, "tests", "golden", "ref_digests.json")
+    try:
+        with open(path) as f:
+            golden = json.load(f)
+    except OSError:
+        return None
+    length = CONFIGS[w.config][3]
+    rpk = RECORDS_PER_KEY.get(w.config, w.nrec)
+    for name, g in sorted(golden.items()):
+        if (g["aead"] == w.aead and int(g["records"]) == w.nrec and int(g["nkeys"]) == w.nkeys
+                and int(g["records_per_key"]) == rpk and str(g["len"]) == str(length)):
+            return name, g
+    return None
+
+
+def device_digests(d_out, offs, lens, d_tags, uniform_stride=0, chunk=1024, threads=16):
+    """(tags_sha256, ct_sha256) of sealed records on the device, with the
+    reference tool's definition (oracle/ref/ref_tool.cc cmd_digest; as
+    tests/golden_util.batch_digests): SHA-256 over all tags in record order,
+    and SHA-256 over the per-1024-record SHA-256 of the concatenated
+    ciphertexts.  Streams the records to the host chunk by chunk."""
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
+    n = len(lens)
+    L = int(lens[0]) if n else 0
+
+    def part(c):
+        lo, hi = c * chunk, min(n, (c + 1) * chunk)
+        lo_b, hi_b = int(offs[lo]), int(offs[hi - 1] + lens[hi - 1])
+        host = d_out[lo_b:hi_b].cpu().numpy()
+        if uniform_stride:
+            if uniform_stride == L:
+                data = host.tobytes()
+            else:
+                full = np.zeros((hi - lo) * uniform_stride, dtype=np.uint8)
+                full[:host.size] = host
+                data = full.reshape(hi - lo, uniform_stride)[:, :L].tobytes()
+        else:
+            data = b"".join(host[int(offs[i]) - lo_b:int(offs[i]) - lo_b + int(lens[i])].tobytes()
+                            for i in range(lo, hi))
+        return hashlib.sha256(data).digest()
+
+    with ThreadPoolExecutor(threads) as ex:
+        parts = list(ex.map(part, range((n + chunk - 1) // chunk)))
+    tags = d_tags[:16 * n].cpu().numpy().tobytes()
+    return hashlib.sha256(tags).hexdigest(), hashlib.sha256(b"".join(parts)).hexdigest()
+
+
+def verify_workload(w):
+    """Compare the rank's sealed batch with the reference digest: returns
+    "ref_digest_ok:<entry>" or "not_checked:<reason>"; raises SystemExit on a
+    mismatch (the measured output is wrong)."""
+    ge = golden_entry(w)
+    if ge is None:
+        return "not_checked:no reference digest for this shard"
+    name, g = ge
+    tags_d, ct_d = device_digests(w.d_ct, w.offs, w.lens, w.d_tags,
+                                  uniform_stride=w.stride if w.uniform else 0)
+    if tags_d != g["tags_sha256"] or ct_d != g["ct_sha256"]:
+        raise SystemExit(f"bench.py: sealed output differs from the reference digest {name} "
+                         f"(tags {tags_d[:16]} vs {g['tags_sha256'][:16]}, "
+                         f"ct {ct_d[:16]} vs {g['ct_sha256'][:16]})")
+    return f"ref_digest_ok:{name}"
+
+
 def plan_only(args, world, rank):
     """The launcher/plan/reduction path without a GPU (gloo)."""
     dist = _dist()
@@ -401,6 +586,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=5.0,
                     help="seconds per CPU-baseline measurement (seal, then open)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the digest check of the sealed output after the timed steps")
     ap.add_argument("--plan-only", action="store_true",
                     help="launcher + shard plan + reductions on CPU (gloo), no GPU")
     ap.add_argument("--op", default="seal", choices=["seal", "open"],
@@ -439,62 +626,10 @@ def main():
     dev = torch.device(f"cuda:{local}")
 
     aead, key_len, _, length, scaling, desc = CONFIGS[args.config]
-    sh = shard_plan(args.config, rank, world, args.records)
-    first, lens, offs, nrec = sh.first, sh.lens, sh.offs, sh.n
-    padded = _pad16(lens, record_align(args.config))
-    pt_bytes = int(lens.sum())
-
-    d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
-    d_lens = torch.from_numpy(lens.astype(np.int64)).to(dev)
-    # Base offset of the record buffers within their allocation (bytes;
-    # BSSL_AMD_BASE_OFFSET, diagnostic): shifts every record's cache-line phase.
-    boff = int(os.environ.get("BSSL_AMD_BASE_OFFSET", 0))
-    d_pt = torch.empty(max(1, sh.total_pad) + boff, dtype=torch.uint8, device=dev)[boff:]
-    d_ct = torch.empty(max(1, sh.total_pad) + boff, dtype=torch.uint8, device=dev)[boff:]
-    d_nonce = torch.empty(max(1, 12 * nrec), dtype=torch.uint8, device=dev)
-    d_ad = torch.empty(max(1, 13 * nrec), dtype=torch.uint8, device=dev)
-    d_tags = torch.empty(max(1, 16 * nrec), dtype=torch.uint8, device=dev)
-    d_status = torch.zeros(max(1, nrec), dtype=torch.uint8, device=dev)
-    ba.synth_fill_device(first, nrec, d_offs, d_lens, d_pt, d_nonce, d_ad)
-    nonce_len = 12
-    if aead == "xchacha20-poly1305":  # 24-byte nonces (ref_tool.cc make_nonce)
-        a = d_nonce.view(-1, 12)
-        b = a.clone()
-        b[:, 4:] ^= 0xff
-        d_nonce, nonce_len = torch.cat([a, b], dim=1).contiguous().view(-1), 24
-    uniform = length != "mixed"
-    rpk = RECORDS_PER_KEY.get(args.config)
-    d_kidx = None
-    if rpk:
-        # The rank's keys: global key ids key_first .. (synth_key).
-        nkeys = sh.nkeys
-        ctx = ba.Keyset(aead, b"".join(synth_key(sh.key_first + k, key_len)
-                                       for k in range(nkeys)), nkeys, 16)
-        d_kidx = torch.from_numpy((np.arange(nrec) // rpk).astype(np.int32)).to(dev)
-    else:
-        ctx = ba.AEADCtx(aead, synth_key(0, key_len), 16)
-    stride = int(padded[0]) if nrec else 16
-    batch = ba.make_batch(nrec, d_pt, d_ct, d_tags, d_nonce, nonce_len, d_ad,
-                          offsets=None if uniform else d_offs,
-                          lengths=None if uniform else d_lens,
-                          record_stride=stride if uniform else 0,
-                          record_len=int(length) if uniform else 0,
-                          ad_stride=13, ad_len=13, status=d_status, key_index=d_kidx)
+    wl = build_workload(args.config, rank, world, args.records, dev, open_op=args.op == "open")
+    sh, nrec, pt_bytes, nonce_len = wl.shard, wl.nrec, wl.pt_bytes, wl.nonce_len
+    d_status, batch, op = wl.d_status, wl.batch, wl.op
     stream = torch.cuda.current_stream()
-    torch.cuda.synchronize()
-    op = ctx.seal_batch_device
-    if args.op == "open":
-        # Seal once, then time opens of the sealed records into a third buffer
-        # (tags verified every step).
-        ctx.seal_batch_device(batch, stream)
-        d_back = torch.empty(d_pt.numel() + boff, dtype=torch.uint8, device=dev)[boff:]
-        batch = ba.make_batch(nrec, d_ct, d_back, d_tags, d_nonce, nonce_len, d_ad,
-                              offsets=None if uniform else d_offs,
-                              lengths=None if uniform else d_lens,
-                              record_stride=stride if uniform else 0,
-                              record_len=int(length) if uniform else 0,
-                              ad_stride=13, ad_len=13, status=d_status, key_index=d_kidx)
-        op = ctx.open_batch_device
 
     for _ in range(args.warmup):
         op(batch, stream)
@@ -520,8 +655,12 @@ def main():
     ba.set_kernel_timing(False)
     if nrec and not bool(d_status[:nrec].all()):
         raise SystemExit(f"{args.op} reported failed records")
-    if args.op == "open" and not torch.equal(d_back[:16 << 10], d_pt[:16 << 10]):
+    if args.op == "open" and not torch.equal(wl.d_back, wl.d_pt):
         raise SystemExit("open did not return the plaintext")
+    # Bit-exact check of the timed output (seal): the digest of the sealed
+    # records and tags against the reference library's digest of the same
+    # synthetic batch (tests/golden/ref_digests.json), where one exists.
+    parity = verify_workload(wl) if args.op == "seal" and not args.no_parity else "not_checked"
     assert len(kernel_ms) == args.steps, kernel_ms
     avg_kernel_ms = float(np.mean(kernel_ms))
     kname = ba.last_kernel_name()
@@ -555,6 +694,7 @@ def main():
                    "record_bytes": length, "plaintext_bytes_rank0": pt_bytes,
                    "plaintext_bytes_all_ranks": int(total_bytes),
                    "parallelism": f"dp{world} (independent record shards, no collective)"},
+        "parity": parity,
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "algorithmic_bytes_per_launch": algo_bytes,

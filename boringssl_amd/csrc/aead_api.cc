@@ -179,7 +179,12 @@ void free_keys(KeyMaterial *km) {
   if (!km) return;
   if (km->dev) {
     DeviceGuard g(km->device);
-    hipMemset(km->dev, 0, km->bytes);  // wipe the device copy (OPENSSL_cleanse)
+    // Batches may still be reading the keys on any stream of the device,
+    // including non-blocking ones the null-stream memset does not order
+    // against (seal/open_batch_device are asynchronous to the host): drain the
+    // device first, then wipe the device copy (OPENSSL_cleanse) and free it.
+    hipDeviceSynchronize();
+    hipMemset(km->dev, 0, km->bytes);
     hipDeviceSynchronize();
     hipFree(km->dev);
   }
@@ -309,7 +314,14 @@ struct Scratch {
   uint8_t *host = nullptr;
   size_t cap = 0;
   hipStream_t stream = nullptr;
+  int device = -1;  // the device that owns dev/stream (set on first use)
   ~Scratch() {
+    if (device < 0) return;  // never used
+    // Thread exit (or process teardown for the main thread): free on the
+    // owning device.  If the HIP runtime is already shut down the calls fail
+    // and the process is exiting anyway.
+    DeviceGuard g(device);
+    if (!g.ok) return;
     if (dev) hipFree(dev);
     if (host) hipHostFree(host);
     if (stream) hipStreamDestroy(stream);
@@ -323,6 +335,7 @@ Scratch *scratch(size_t bytes) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
   Scratch &sc = t_scratch[dev];
+  sc.device = dev;
   if (!sc.stream && hipStreamCreateWithFlags(&sc.stream, hipStreamNonBlocking) != hipSuccess)
     return nullptr;
   if (sc.cap < bytes) {

@@ -168,6 +168,8 @@ DIGESTS = [
     ("config3_chacha_1350", "chacha20-poly1305", 1, 1048576, "1350"),
     ("config3x_xchacha_1350", "xchacha20-poly1305", 1, 1048576, "1350"),
     ("configs_siv128_16k", "aes-128-gcm-siv", 1, 262144, "16384"),
+    # bench.py --config configS's own batch (1M records; round 3)
+    ("configS_siv128_16k_1m", "aes-128-gcm-siv", 1, 1048576, "16384"),
     ("config4_aes256_mixed", "aes-256-gcm", 1, 4194304, "mixed"),
     ("config5_multikey_aes128", "aes-128-gcm", 65536, 64, "16384"),
 ]
@@ -176,7 +178,10 @@ DIGESTS = [
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true")
+    ap.add_argument("--only", default="", help="regenerate just this digest entry")
     args = ap.parse_args()
+    if args.only:
+        return digest_entries(lambda name: name == args.only)
     aead = convert_aead()
     # attach Wycheproof tcIds (comment lines precede each record in file order)
     for rel in ("third_party/wycheproof_testvectors/aes_gcm_test.txt",
@@ -203,13 +208,19 @@ def main():
         json.dump(edge, f, indent=0)
     print(f"ref_edge.json: {len(edge)} cases")
 
+    return digest_entries(lambda name: not (args.skip_full and name.startswith("config")))
+
+
+def digest_entries(want):
+    if not os.path.exists(REF_TOOL):
+        subprocess.check_call(["make", "-j8", "-C", os.path.join(ROOT, "oracle", "ref")])
     path = os.path.join(HERE, "ref_digests.json")
     digests = {}
     if os.path.exists(path):
         with open(path) as f:
             digests = json.load(f)
     for name, aead_name, nkeys, rpk, length in DIGESTS:
-        if args.skip_full and name.startswith("config"):
+        if not want(name):
             continue
         res = json.loads(subprocess.check_output(
             [REF_TOOL, "digest", aead_name, str(nkeys), str(rpk), length, "8"]))

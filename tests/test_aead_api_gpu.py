@@ -614,3 +614,66 @@ def test_keyset_tag_len_rules():
     assert e.value.reason == ba.CIPHER_R_TAG_TOO_LARGE
     ba.Keyset("aes-128-gcm-siv", key, 1, 16).close()
     ba.Keyset("aes-128-gcm", key, 1, 8).close()
+
+
+@pytest.mark.parametrize("which", ["ctx", "keyset"])
+def test_cleanup_while_batch_in_flight(which):
+    """EVP_AEAD_CTX_cleanup / BSSL_AMD_KEYSET_free right after enqueueing a
+    large device batch on a NON-BLOCKING stream (seal_batch_device is
+    asynchronous to the host): the key wipe must not land while the kernel
+    still reads the round keys (the null-stream memset does not
+    order against such streams).  Sampled records and every status must
+    match the oracle after the stream completes."""
+    import numpy as np
+    import oracle_lib as o
+    n, rlen = 1 << 17, 16384  # 2 GiB: several ms of kernel time
+    key = bytes(range(7, 23))
+    dev = torch.device("cuda:0")
+    d_pt = torch.randint(0, 256, (n * rlen,), dtype=torch.uint8, device=dev)
+    d_ct = torch.zeros_like(d_pt)
+    d_tags = torch.zeros(16 * n, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(n, dtype=torch.uint8, device=dev)
+    d_n = torch.randint(0, 256, (12 * n,), dtype=torch.uint8, device=dev)
+    d_ad = torch.randint(0, 256, (13 * n,), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()  # pool stream: created non-blocking by PyTorch
+    b = ba.make_batch(n, d_pt, d_ct, d_tags, d_n, 12, d_ad, record_stride=rlen, record_len=rlen,
+                      ad_stride=13, ad_len=13, status=d_st)
+    if which == "ctx":
+        obj = ba.AEADCtx("aes-128-gcm", key, 16)
+    else:
+        obj = ba.Keyset("aes-128-gcm", key, 1, 16)
+    obj.seal_batch_device(b, s)
+    obj.close()  # cleanup with the batch in flight
+    s.synchronize()
+    assert bool(d_st.all())
+    pt, ct, tags = d_pt.cpu().numpy(), d_ct.cpu().numpy(), d_tags.cpu().numpy()
+    nn, aa = d_n.cpu().numpy(), d_ad.cpu().numpy()
+    for i in list(range(0, 32)) + list(range(n - 32, n)) + list(range(n // 2, n // 2 + 8)):
+        ok, c, t = o.seal(o.AES_GCM, key, nn[12 * i:12 * i + 12].tobytes(),
+                          pt[rlen * i:rlen * (i + 1)].tobytes(), aa[13 * i:13 * i + 13].tobytes())
+        assert ok and ct[rlen * i:rlen * (i + 1)].tobytes() == c and \
+            tags[16 * i:16 * i + 16].tobytes() == t, i
+
+
+def test_device_guard_one_gpu():
+    """Single-GPU check of the device guard (the two-GPU test is deselected on
+    one-GPU boxes): host-buffer calls leave the caller's current device as
+    it was, and a rejected device-batch call reports the same error every
+    time and leaves the context usable."""
+    key, nonce = bytes(range(16)), bytes(12)
+    ctx = ba.AEADCtx("aes-128-gcm", key, 16)
+    before = torch.cuda.current_device()
+    sealed = ctx.seal(nonce, b"hello", b"ad")
+    assert ctx.open(nonce, sealed, b"ad") == b"hello"
+    assert torch.cuda.current_device() == before
+    d = torch.zeros(64, dtype=torch.uint8, device="cuda:0")
+    reasons = []
+    for _ in range(3):
+        with pytest.raises(ba.AEADError) as e:  # no nonces: rejected before any launch
+            ctx.seal_batch_device(ba.make_batch(1, d, d, d, None, 12, d, record_len=16,
+                                                record_stride=16))
+        reasons.append(e.value.reason)
+    assert len(set(reasons)) == 1 and reasons[0] == 66  # ERR_R_SHOULD_NOT_HAVE_BEEN_CALLED
+    assert ctx.seal(nonce, b"hello", b"ad") == sealed
+    assert torch.cuda.current_device() == before

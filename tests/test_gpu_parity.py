@@ -366,13 +366,14 @@ def test_device_synth_matches_host_definition():
 # ---------------------------------------------------------------------------
 # synthetic workloads vs the reference library's digests
 
-def synth_device_batch(aead, nkeys, rpk, length, first=0):
+def synth_device_batch(aead, nkeys, rpk, length, first=0, align=16):
     n = nkeys * rpk
     if length == "mixed":
         lens = np.array([o.synth_mixed_len(first + i) for i in range(n)], dtype=np.uint64)
     else:
         lens = np.full(n, int(length), dtype=np.uint64)
-    padded = (lens + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+    a = np.uint64(align)
+    padded = (lens + a - np.uint64(1)) // a * a
     offs = np.zeros(n, dtype=np.uint64)
     offs[1:] = np.cumsum(padded[:-1])
     total = int(padded.sum())
@@ -411,11 +412,12 @@ def xchacha_nonces_device(d_n12):
     return torch.cat([a, b], dim=1).contiguous().view(-1)
 
 
-def _run_synth_digest(name):
+def _run_synth_digest(name, align=16):
     g = load("ref_digests.json")[name]
     aead, nkeys, rpk, length = g["aead"], g["nkeys"], g["records_per_key"], g["len"]
     n = nkeys * rpk
-    lens, offs, d_offs, d_lens, d_pt, d_n, d_a = synth_device_batch(aead, nkeys, rpk, length)
+    lens, offs, d_offs, d_lens, d_pt, d_n, d_a = synth_device_batch(aead, nkeys, rpk, length,
+                                                                    align=align)
     d_out = torch.zeros_like(d_pt)
     d_tags = torch.zeros(16 * n, dtype=torch.uint8, device=DEV)
     d_st = torch.zeros(n, dtype=torch.uint8, device=DEV)
@@ -454,6 +456,15 @@ def _run_synth_digest(name):
                                   "parity_siv128_multikey"])
 def test_synth_parity_digest(name):
     _run_synth_digest(name)
+
+
+@pytest.mark.parametrize("name", ["parity_chacha_1350", "parity_xchacha_1350",
+                                  "parity_aes256_mixed", "config3_chacha_1350"])
+def test_synth_parity_digest_align128(name):
+    """The same digests with records 128-byte aligned (bench.py's alignment;
+    per-record offsets/lengths arrays): ChaCha's 128-byte slot shift (sh = 1)
+    with the per-record metadata path."""
+    _run_synth_digest(name, align=128)
 
 
 @pytest.mark.parametrize("name", ["config2_aes128_16k", "config3_chacha_1350",

@@ -19,6 +19,7 @@ run() {
 }
 for s in $STEPS; do
   case $s in
+    micro) run micro 300 tools/micro/${MICRO:-bs16_rate} ;;
     smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
     pytest) run pytest 1500 python -u -m pytest tests/ -v -m gpu -rf --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
