@@ -33,8 +33,8 @@
 #include <string.h>
 
 #include "internal.h"
-#include "bs_aes.h"
 #include "bs16_aes.h"
+#include "gf128_ct.h"
 
 #ifndef BSSL_AMD_ABLATE
 #define BSSL_AMD_ABLATE 0
@@ -91,12 +91,12 @@ struct StampVec {
 };
 constexpr int kRecPerWave = 4;
 // Tiled (multi-key) path: rotating wave priorities (process_records RP).
-// Mixed-role kernel: raise the T-table waves' issue priority (knob).
-#ifndef BSSL_AMD_GCM_MIX_PRIO
-#define BSSL_AMD_GCM_MIX_PRIO 0
-#endif
 #ifndef BSSL_AMD_GCM_TILE_RP
 #define BSSL_AMD_GCM_TILE_RP 1
+#endif
+// Tiled path: workgroup barrier every N iterations (0 = off; even N).
+#ifndef BSSL_AMD_GCM_TILE_SYNC
+#define BSSL_AMD_GCM_TILE_SYNC 0
 #endif
 
 // ---------------------------------------------------------------------------
@@ -149,14 +149,12 @@ __constant__ Tables kTables = make_tables();
 //   [65536, 131072)  AES T0/T1, replicated per bank (see header comment); the
 //                    lookup address carries bit 16 (lane constants lc0/lc1)
 //   [131072, ...)    tile plan (keys and record masks of the passes)
-// The bitsliced kernel keeps the nibble tables (kLdsGhash, 8 KiB per power).
-constexpr uint32_t kLdsGhash = 0;
 constexpr uint32_t kLdsG8 = 0;
 constexpr uint32_t kG8Bytes = 256 * 256;
 constexpr uint32_t kLdsAes = kG8Bytes;
 constexpr uint32_t kAesLdsBytes = 256 * 256;
 constexpr uint32_t kLdsPlan = kLdsAes + kAesLdsBytes;
-constexpr uint32_t kLdsBytes = kLdsPlan + 64 * 16 + 16;
+constexpr uint32_t kLdsBytes = kLdsPlan + 64 * 16 + 16;  // (+4: TILE_SYNC minimum)
 
 __device__ __forceinline__ uint32_t rotl(uint32_t v, int n) {
   return __builtin_amdgcn_alignbit(v, v, 32 - n);
@@ -173,29 +171,6 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 __device__ __forceinline__ uint4 xor4_3(uint4 a, uint4 b, uint4 c) {
   return make_uint4(xor3(a.x, b.x, c.x), xor3(a.y, b.y, c.y), xor3(a.z, b.z, c.z),
                     xor3(a.w, b.w, c.w));
-}
-
-// (byte B of v) & 0xf0 in one VALU op (SDWA byte select).
-#define DEFINE_NIB(B)                                                          \
-  __device__ __forceinline__ uint32_t nib_b##B(uint32_t v, uint32_t mf0) {     \
-    uint32_t r;                                                                \
-    asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD "       \
-        "src0_sel:BYTE_" #B " src1_sel:DWORD"                                  \
-        : "=v"(r)                                                              \
-        : "v"(v), "v"(mf0));                                                   \
-    return r;                                                                  \
-  }
-DEFINE_NIB(1)
-DEFINE_NIB(2)
-DEFINE_NIB(3)
-#undef DEFINE_NIB
-
-template <int B>
-__device__ __forceinline__ uint32_t nib(uint32_t v, uint32_t mf0) {
-  if constexpr (B == 0) return v & 0xf0u;
-  if constexpr (B == 1) return nib_b1(v, mf0);
-  if constexpr (B == 2) return nib_b2(v, mf0);
-  return nib_b3(v, mf0);
 }
 
 // ---------------------------------------------------------------------------
@@ -342,59 +317,7 @@ __device__ __forceinline__ uint4 g8_load(const Gh8 &h, const uint32_t (&P)[4],
   return *reinterpret_cast<const uint4 *>(smem + kLdsG8 + a);
 }
 
-// ---------------------------------------------------------------------------
-// GHASH: x * H^(2^p); the tables of power p start at byte TB of `tab`
-// (LDS in the main kernel, global memory in the prologue).
-template <uint32_t TB>
-__device__ __forceinline__ uint4 tab128(const uint8_t *tab, uint32_t a) {
-  return *reinterpret_cast<const uint4 *>(tab + TB + a);
-}
-
-template <uint32_t TB, int W>
-__device__ __forceinline__ uint4 gmul_word(uint4 r, uint32_t v, const uint8_t *tab,
-                                           uint32_t mf0) {
-  const uint32_t l = v << 4;  // low nibble of byte k -> high nibble of byte k of l
-  r = xor4_3(r, tab128<TB + (8 * W + 0) * 256>(tab, nib<0>(v, mf0)),
-             tab128<TB + (8 * W + 1) * 256>(tab, nib<0>(l, mf0)));
-  r = xor4_3(r, tab128<TB + (8 * W + 2) * 256>(tab, nib<1>(v, mf0)),
-             tab128<TB + (8 * W + 3) * 256>(tab, nib<1>(l, mf0)));
-  r = xor4_3(r, tab128<TB + (8 * W + 4) * 256>(tab, nib<2>(v, mf0)),
-             tab128<TB + (8 * W + 5) * 256>(tab, nib<2>(l, mf0)));
-  r = xor4_3(r, tab128<TB + (8 * W + 6) * 256>(tab, nib<3>(v, mf0)),
-             tab128<TB + (8 * W + 7) * 256>(tab, nib<3>(l, mf0)));
-#if BSSL_AMD_GHASH_GROUP
-  // Keep the word's 8 lookups in flight together (hipcc otherwise issues
-  // them two at a time under register pressure).
-  __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-  __builtin_amdgcn_sched_group_barrier(0x2, 16, 0);
-#endif
-  return r;
-}
-
-// Hot-loop form: the word's 8 lookups are issued back to back by one asm
-// block (hipcc's scheduler otherwise issues them two at a time, one LDS round
-// trip per pair).  `base` is the LDS byte address of the power's tables.
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-
-template <uint32_t OFF>
-__device__ __forceinline__ void lds_read8(const uint32_t a[8], v4u d[8]) {
-  static_assert(OFF + 7 * 256 < 65536, "ds_read offset field");
-  asm volatile(
-      "ds_read_b128 %0, %8 offset:%16\n\t"
-      "ds_read_b128 %1, %9 offset:%17\n\t"
-      "ds_read_b128 %2, %10 offset:%18\n\t"
-      "ds_read_b128 %3, %11 offset:%19\n\t"
-      "ds_read_b128 %4, %12 offset:%20\n\t"
-      "ds_read_b128 %5, %13 offset:%21\n\t"
-      "ds_read_b128 %6, %14 offset:%22\n\t"
-      "ds_read_b128 %7, %15 offset:%23\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]), "=&v"(d[5]),
-        "=&v"(d[6]), "=&v"(d[7])
-      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]),
-        "i"(OFF), "i"(OFF + 256), "i"(OFF + 512), "i"(OFF + 768), "i"(OFF + 1024),
-        "i"(OFF + 1280), "i"(OFF + 1536), "i"(OFF + 1792));
-}
 
 // Counter-mode cache of one AES stream (see process_records).
 struct WindowCache {
@@ -456,6 +379,9 @@ constexpr uint32_t g8_sel() {
 // AES-192/256 spread 2 per round over the first 8.
 template <int NR>
 constexpr int g_steps(int i) {
+#if BSSL_AMD_ABLATE == 8  // diagnostic: no GHASH lookups at all (wrong tags)
+  return 0 * i;
+#endif
   if (NR == 10) return i < 2 ? 3 : 2;
   return i < 8 ? 2 : 0;
 }
@@ -537,90 +463,6 @@ __device__ __forceinline__ void rounds_s1(uint32_t (&a)[4], const RoundKeys &rk,
     }
     rounds_s1<I + 1, NR>(a, rk, lc0, lc1, h, P, xs, wc, k0, nx);
   }
-}
-
-template <uint32_t TB, int W>
-__device__ __forceinline__ uint4 gmul_word_batched(uint4 r, uint32_t v, uint32_t base,
-                                                   uint32_t mf0) {
-  const uint32_t l = v << 4;
-  const uint32_t a[8] = {base + nib<0>(v, mf0), base + nib<0>(l, mf0), base + nib<1>(v, mf0),
-                         base + nib<1>(l, mf0), base + nib<2>(v, mf0), base + nib<2>(l, mf0),
-                         base + nib<3>(v, mf0), base + nib<3>(l, mf0)};
-  v4u d[8];
-  lds_read8<TB + 8 * W * 256>(a, d);
-  const v4u t = (d[0] ^ d[1] ^ d[2]) ^ (d[3] ^ d[4] ^ d[5]) ^ (d[6] ^ d[7]);
-  return make_uint4(r.x ^ t.x, r.y ^ t.y, r.z ^ t.z, r.w ^ t.w);
-}
-
-template <uint32_t TB>
-__device__ __forceinline__ uint4 gmul_batched(uint4 x, uint32_t base, uint32_t mf0) {
-  uint4 r = make_uint4(0, 0, 0, 0);
-  r = gmul_word_batched<TB, 0>(r, x.x, base, mf0);
-  r = gmul_word_batched<TB, 1>(r, x.y, base, mf0);
-  r = gmul_word_batched<TB, 2>(r, x.z, base, mf0);
-  r = gmul_word_batched<TB, 3>(r, x.w, base, mf0);
-  return r;
-}
-
-template <uint32_t TB>
-__device__ __forceinline__ uint4 gmul(uint4 x, const uint8_t *tab, uint32_t mf0) {
-  // The scheduling barriers keep at most one word's lookups (8 x 16 B) in
-  // flight; without them hipcc hoists all 32 loads and needs 128 VGPRs.
-  uint4 r = make_uint4(0, 0, 0, 0);
-  r = gmul_word<TB, 0>(r, x.x, tab, mf0);
-  __builtin_amdgcn_sched_barrier(0);
-  r = gmul_word<TB, 1>(r, x.y, tab, mf0);
-  __builtin_amdgcn_sched_barrier(0);
-  r = gmul_word<TB, 2>(r, x.z, tab, mf0);
-  __builtin_amdgcn_sched_barrier(0);
-  r = gmul_word<TB, 3>(r, x.w, tab, mf0);
-  __builtin_amdgcn_sched_barrier(0);
-  return r;
-}
-
-// x * (the power whose nibble tables start at `tab`) with the tables in
-// GLOBAL memory (the record-end tree and tag of finish_record, which read the
-// key's L2-resident copy): the 16 lookups of two words are issued back to back
-// and XORed after one wait -- two memory round trips per product.  (Through
-// gmul, whose grouping targets LDS reads, hipcc issued them two at a time with
-// a vmcnt(0) after each pair: 16 round trips per product, 6 products per
-// record.)
-template <int W0>
-__device__ __forceinline__ uint4 gmul_gwords(uint4 r, uint32_t v0, uint32_t v1, const uint8_t *tab,
-                                             uint32_t mf0) {
-  uint4 t[16];
-#pragma unroll
-  for (int h = 0; h < 2; h++) {
-    const uint32_t v = h ? v1 : v0, l = v << 4;
-    const uint8_t *tw = tab + (8 * (W0 + h)) * 256;
-    t[8 * h + 0] = tab128<0 * 256>(tw, nib<0>(v, mf0));
-    t[8 * h + 1] = tab128<1 * 256>(tw, nib<0>(l, mf0));
-    t[8 * h + 2] = tab128<2 * 256>(tw, nib<1>(v, mf0));
-    t[8 * h + 3] = tab128<3 * 256>(tw, nib<1>(l, mf0));
-    t[8 * h + 4] = tab128<4 * 256>(tw, nib<2>(v, mf0));
-    t[8 * h + 5] = tab128<5 * 256>(tw, nib<2>(l, mf0));
-    t[8 * h + 6] = tab128<6 * 256>(tw, nib<3>(v, mf0));
-    t[8 * h + 7] = tab128<7 * 256>(tw, nib<3>(l, mf0));
-  }
-  __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);  // address VALU
-  __builtin_amdgcn_sched_group_barrier(0x020, 16, 0);  // the 16 VMEM reads
-#pragma unroll
-  for (int i = 0; i < 16; i += 2) r = xor4_3(r, t[i], t[i + 1]);
-  return r;
-}
-
-__device__ __forceinline__ uint4 gmul_global(uint4 x, const uint8_t *tab, uint32_t mf0) {
-  uint4 r = make_uint4(0, 0, 0, 0);
-  r = gmul_gwords<0>(r, x.x, x.y, tab, mf0);
-  __builtin_amdgcn_sched_barrier(0);
-  r = gmul_gwords<2>(r, x.z, x.w, tab, mf0);
-  __builtin_amdgcn_sched_barrier(0);
-  return r;
-}
-
-// Runtime power index (prologue, tree).
-__device__ __forceinline__ uint4 gmul_pow(uint4 x, const uint8_t *tab, int p, uint32_t mf0) {
-  return gmul<0>(x, tab + p * 8192, mf0);
 }
 
 __device__ __forceinline__ uint4 shfl4(uint4 v, int src, int width) {
@@ -727,19 +569,8 @@ __device__ __forceinline__ T meta_load(const T *arr, uint64_t i) {
   return *p;
 }
 
-#ifndef BSSL_AMD_GCM_META_BRANCH
-#define BSSL_AMD_GCM_META_BRANCH 0
-#endif
 __device__ __forceinline__ RecordMeta record_meta(const BatchDesc &b, uint64_t i) {
   RecordMeta m;
-#if BSSL_AMD_GCM_META_BRANCH  // (the round-1 form, for A/B)
-  m.off = b.offsets ? b.offsets[i] : i * b.record_stride;
-  m.len = b.lengths ? b.lengths[i] : b.record_len;
-  m.ad_off = b.ad_offsets ? b.ad_offsets[i] : i * b.ad_stride;
-  m.ad_len = b.ad_lengths ? b.ad_lengths[i] : b.ad_len;
-  m.xlen = b.extra_len;
-  return m;
-#endif
   if (!(b.offsets || b.lengths || b.ad_offsets || b.ad_lengths)) {  // uniform layout: no loads
     m.off = i * b.record_stride;
     m.len = b.record_len;
@@ -831,34 +662,60 @@ struct alignas(16) RecState {
   uint32_t live, pad[3];
 };
 
+// Kernel block words (the 16 block bytes as 4 little-endian words) <-> the
+// reversed domain of gf128_ct.h (the big-endian integer of the bytes).
+__device__ __forceinline__ Gf128 to_gf(uint4 v) {
+  Gf128 g;
+  g.w[3] = bswap32(v.x);
+  g.w[2] = bswap32(v.y);
+  g.w[1] = bswap32(v.z);
+  g.w[0] = bswap32(v.w);
+  return g;
+}
+__device__ __forceinline__ uint4 from_gf(Gf128 g) {
+  return make_uint4(bswap32(g.w[3]), bswap32(g.w[2]), bswap32(g.w[1]), bswap32(g.w[0]));
+}
+__device__ __forceinline__ Gf128 gf_load(const uint32_t *p) {
+  const uint4 v = *reinterpret_cast<const uint4 *>(p);
+  Gf128 g;
+  g.w[0] = v.x;
+  g.w[1] = v.y;
+  g.w[2] = v.z;
+  g.w[3] = v.w;
+  return g;
+}
+__device__ __forceinline__ Gf128 gf_xor(Gf128 a, Gf128 b) {
+  for (int i = 0; i < 4; i++) a.w[i] ^= b.w[i];
+  return a;
+}
+
 // ---------------------------------------------------------------------------
-// One AES block with a compact T-table (prologue): tab[2*x] = T0[x],
-// tab[2*x + 1] = T1[x] = rotl8(T0[x]) in 2 KiB of LDS -- the round algebra of
-// aes_round / aes_rounds (middle round keys pre-rotated by 16), addressed by
-// byte * 8 + slot * 4 instead of the bank-replicated layout of the bulk
-// kernel, so the one-thread-per-record prologue is not held to two
-// workgroups per CU by a 64 KiB LDS declaration.
-template <int K, int SLOT>
-__device__ __forceinline__ uint32_t ctl(const uint32_t *tab, uint32_t s) {
-  return tab[2 * __builtin_amdgcn_ubfe(s, 8 * K, 8) + SLOT];
+// One AES block with T0 alone, replicated once per LDS bank (prologue):
+// entry x for lane l at tab[x * 32 + (l & 31)] (32 KiB), so every lookup of a
+// wave is bank-conflict free whatever the index -- the same constant-time
+// argument as the bulk kernel's tables, at half their size
+// so more prologue workgroups fit per CU.  T1..T3 are rotations of T0; the
+// middle round keys arrive pre-rotated by 16 (GcmKeyDev::rk).
+template <int K>
+__device__ __forceinline__ uint32_t t0r(const uint32_t *tab, uint32_t s, uint32_t lane) {
+  return tab[__builtin_amdgcn_ubfe(s, 8 * K, 8) * 32 + lane];
 }
 
 template <int NR>
-__device__ __forceinline__ uint4 aes_block_compact(uint4 in, const RoundKeys &rk,
-                                                   const uint32_t *tab) {
+__device__ __forceinline__ uint4 aes_block_rep(uint4 in, const RoundKeys &rk, const uint32_t *tab) {
+  const uint32_t l = threadIdx.x & 31;
   uint32_t s0 = in.x ^ rk.w[0][0], s1 = in.y ^ rk.w[0][1], s2 = in.z ^ rk.w[0][2],
            s3 = in.w ^ rk.w[0][3];
+  auto col = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t kx) {
+    // T0[a] ^ T1[b] ^ rotl16(T0[c] ^ T1[d] ^ kx), T1 = rotl8(T0)
+    return xor3(t0r<0>(tab, a, l), rotl(t0r<1>(tab, b, l), 8),
+                rotl(xor3(t0r<2>(tab, c, l), rotl(t0r<3>(tab, d, l), 8), kx), 16));
+  };
 #pragma unroll
   for (int r = 1; r < NR; r++) {
-    const uint32_t *rkx = rk.w[r];
-    const uint32_t t0 = xor3(ctl<0, 0>(tab, s0), ctl<1, 1>(tab, s1),
-                             rotl(xor3(ctl<2, 0>(tab, s2), ctl<3, 1>(tab, s3), rkx[0]), 16));
-    const uint32_t t1 = xor3(ctl<0, 0>(tab, s1), ctl<1, 1>(tab, s2),
-                             rotl(xor3(ctl<2, 0>(tab, s3), ctl<3, 1>(tab, s0), rkx[1]), 16));
-    const uint32_t t2 = xor3(ctl<0, 0>(tab, s2), ctl<1, 1>(tab, s3),
-                             rotl(xor3(ctl<2, 0>(tab, s0), ctl<3, 1>(tab, s1), rkx[2]), 16));
-    const uint32_t t3 = xor3(ctl<0, 0>(tab, s3), ctl<1, 1>(tab, s0),
-                             rotl(xor3(ctl<2, 0>(tab, s1), ctl<3, 1>(tab, s2), rkx[3]), 16));
+    const uint32_t *kx = rk.w[r];
+    const uint32_t t0 = col(s0, s1, s2, s3, kx[0]), t1 = col(s1, s2, s3, s0, kx[1]),
+                   t2 = col(s2, s3, s0, s1, kx[2]), t3 = col(s3, s0, s1, s2, kx[3]);
     s0 = t0;
     s1 = t1;
     s2 = t2;
@@ -866,39 +723,23 @@ __device__ __forceinline__ uint4 aes_block_compact(uint4 in, const RoundKeys &rk
   }
   // Last round: S[x] is byte 1 (and byte 2) of Te0[x].
   auto last = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
-    return xor3(__builtin_amdgcn_perm(ctl<1, 0>(tab, b), ctl<0, 0>(tab, a), 0x0c0c0501u),
-                __builtin_amdgcn_perm(ctl<3, 0>(tab, d), ctl<2, 0>(tab, c), 0x06020c0cu), k);
+    return xor3(__builtin_amdgcn_perm(t0r<1>(tab, b, l), t0r<0>(tab, a, l), 0x0c0c0501u),
+                __builtin_amdgcn_perm(t0r<3>(tab, d, l), t0r<2>(tab, c, l), 0x06020c0cu), k);
   };
   return make_uint4(last(s0, s1, s2, s3, rk.w[NR][0]), last(s1, s2, s3, s0, rk.w[NR][1]),
                     last(s2, s3, s0, s1, rk.w[NR][2]), last(s3, s0, s1, s2, rk.w[NR][3]));
 }
 
-#ifndef BSSL_AMD_GCM_PRO_COMPACT
-#define BSSL_AMD_GCM_PRO_COMPACT 1
-#endif
-
 // ---------------------------------------------------------------------------
 // Prologue: one thread per record.  J0 (incl. the GHASH-derived J0 of a
 // non-96-bit nonce), E_K(J0) and the AD hash -- the per-record constant work
-// of CRYPTO_gcm128_init_ctx / _aad (gcm.cc.inc:298-398).
+// of CRYPTO_gcm128_init_ctx / _aad (gcm.cc.inc:298-398).  Constant time: AES
+// from the bank-replicated T0, GHASH products by gf_mul (gf128_ct.h).
 template <int NR>
 __global__ __launch_bounds__(256) void gcm_prologue(const GcmKeyDev *__restrict__ keys,
                                                     BatchDesc b, RecState *__restrict__ st) {
-#if BSSL_AMD_GCM_PRO_COMPACT
-  __shared__ uint32_t ctab[512];
-  for (int e = threadIdx.x; e < 512; e += blockDim.x) {
-    const uint32_t v = kTables.te0[e >> 1];
-    ctab[e] = (e & 1) ? rotl(v, 8) : v;
-  }
-#else
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kAesLdsBytes];
-  // Only replica 0 of T0/T1 (lane constant 0 / 128): conflicts do not matter here.
-  for (int e = threadIdx.x; e < 512; e += blockDim.x) {
-    const int idx = e >> 1;
-    const uint32_t v = kTables.te0[idx];
-    reinterpret_cast<uint32_t *>(smem)[idx * 64 + (e & 1) * 32] = (e & 1) ? rotl(v, 8) : v;
-  }
-#endif
+  __shared__ uint32_t t0tab[256 * 32];
+  for (int e = threadIdx.x; e < 256 * 32; e += blockDim.x) t0tab[e] = kTables.te0[e >> 5];
   __syncthreads();
   const uint64_t rec = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (rec >= b.num_records) return;
@@ -915,8 +756,7 @@ __global__ __launch_bounds__(256) void gcm_prologue(const GcmKeyDev *__restrict_
   s.j0 = s.ek0 = s.ya = make_uint4(0, 0, 0, 0);
   if (live) {
     const GcmKeyDev *kp = keys + k;
-    const uint8_t *htab = reinterpret_cast<const uint8_t *>(kp->htab);
-    const uint32_t mf0 = 0xf0;
+    const Gf128 h1 = gf_load(kp->hpow_ct[1]);
     RoundKeys rk;
 #pragma unroll
     for (int r = 0; r <= NR; r++)
@@ -928,79 +768,65 @@ __global__ __launch_bounds__(256) void gcm_prologue(const GcmKeyDev *__restrict_
       j0 = load_partial(nonce, 12);
       j0.w = 0x01000000u;  // be32(1)
     } else {
-      j0 = make_uint4(0, 0, 0, 0);
+      // GHASH(N || 0^s || [len(N)]_64) (gcm.cc.inc:320-338).
+      Gf128 y = {{0, 0, 0, 0}};
       for (uint64_t o = 0; o < b.nonce_len; o += 16)
-        j0 = gmul_pow(xor4(j0, load_partial(nonce + o, (uint32_t)min<uint64_t>(b.nonce_len - o, 16))),
-                      htab, 0, mf0);
+        y = gf_mul(gf_xor(y, to_gf(load_partial(nonce + o,
+                                                (uint32_t)min<uint64_t>(b.nonce_len - o, 16)))),
+                   h1);
       const uint64_t bits = b.nonce_len << 3;
-      j0 = gmul_pow(xor4(j0, make_uint4(0, 0, bswap32((uint32_t)(bits >> 32)), bswap32((uint32_t)bits))),
-                    htab, 0, mf0);
+      y.w[0] ^= (uint32_t)bits;
+      y.w[1] ^= (uint32_t)(bits >> 32);
+      j0 = from_gf(gf_mul(y, h1));
     }
     s.j0 = j0;
-#if BSSL_AMD_GCM_PRO_COMPACT
-    s.ek0 = aes_block_compact<NR>(j0, rk, ctab);
-#else
-    s.ek0 = aes_rounds<NR, 0>(j0.x ^ rk.w[0][0], j0.y ^ rk.w[0][1], j0.z ^ rk.w[0][2],
-                              j0.w ^ rk.w[0][3], rk, smem, 0u, 128u);
-#endif
+    s.ek0 = aes_block_rep<NR>(j0, rk, t0tab);
+    // Exclusive GHASH of the AD, sum A_k H^(m-1-k) (the lanes' element 0).
     const uint8_t *ad = b.ad + m.ad_off;
-    uint4 ya = make_uint4(0, 0, 0, 0);
+    Gf128 ya = {{0, 0, 0, 0}};
     for (uint64_t o = 0; o < m.ad_len; o += 16) {
-      const uint4 blk = load_partial(ad + o, (uint32_t)min<uint64_t>(m.ad_len - o, 16));
-      ya = o ? xor4(gmul_pow(ya, htab, 0, mf0), blk) : blk;
+      const Gf128 blk = to_gf(load_partial(ad + o, (uint32_t)min<uint64_t>(m.ad_len - o, 16)));
+      ya = o ? gf_xor(gf_mul(ya, h1), blk) : blk;
     }
-    s.ya = ya;
+    s.ya = from_gf(ya);
   }
   st[rec] = s;
 }
 
-// End of a record (both bulk kernels): combine the L lanes' GHASH
+// End of a record (all bulk kernels): combine the 16 lanes' GHASH
 // accumulators, form the tag, check it (open), write tag/status, and zero the
-// output of a failed record.  Lane algebra (DESIGN.md): lane q holds the
-// virtual elements v = q+1+L*i of [Y_A, C_0, ..., C_{nb-1}]; rotate so position
-// p holds the lane whose weight is H^(L-1-p), then tree-combine with
-// H, H^2, ..., H^(L/2) (nibble tables 0..log2(L)-1 at `tab`: LDS or the key's
-// global copy).
-// The record-end products: `tab` is the key's global copy of the nibble
-// tables (gmul_global; gmul in the
-// round-1 path for A/B (BSSL_AMD_GCM_FIN_GMUL=0).
-#ifndef BSSL_AMD_GCM_FIN_GMUL
-#define BSSL_AMD_GCM_FIN_GMUL 1
-#endif
-#if BSSL_AMD_GCM_FIN_GMUL
-#define GMUL_FIN(x, tab, mf0) gmul_global(x, tab, mf0)
-#else
-#define GMUL_FIN(x, tab, mf0) gmul<0>(x, tab, mf0)
-#endif
+// output of a failed record.  Lane algebra (DESIGN.md §4.2): lane q holds the
+// virtual elements v = q+1+16i of [Y_A, C_0, ..., C_{nb-1}], Horner'd at
+// stride 16, so its accumulator needs weight H^(15-p), p = (q - r + 1) mod 16
+// with r = (nb + 1) mod 16 (the lane holding the last element gets H^0).
+// Each lane multiplies its accumulator by H^(16-p) -- its weight times the
+// tag's first H -- and the 16 products are XOR-reduced:
+//   tag = ((Z*H) ^ len block) * H ^ E_K(J0)  (gcm.cc.inc:576-604).
+// Both products are constant-time VALU multiplications (gf128_ct.h) by the
+// key's prepared powers H^1..H^16 (key->hpow_ct), indexed by lane position
+// and record length only; no table is indexed by a secret.
 template <bool OPEN, int L>
 __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const RecordMeta &m,
                                               const RecState &s, const BatchDesc &b, uint64_t rec,
                                               bool active, bool live, uint8_t *dst,
-                                              const uint8_t *tab, uint32_t mf0) {
-  constexpr int kLevels = L == 32 ? 5 : L == 16 ? 4 : L == 8 ? 3 : L == 4 ? 2 : -1;
-  static_assert(kLevels > 0, "lanes per record");
+                                              const GcmKeyDev *key) {
+  static_assert(L == 16, "lanes per record");
   const int q = threadIdx.x & (L - 1);
   const int r = (int)((nb + 1) & (L - 1));
-  uint4 a = shfl4(acc, (q + r + L - 1) & (L - 1), L);
-  // Kept as a rolled loop so hipcc does not interleave the dependent
-  // multiplications (which costs ~120 VGPRs when unrolled).
-#pragma unroll 1
-  for (int t = 0; t < kLevels; t++) {
-    const int sh = 1 << t;
-    const uint4 o = shfl_down4(a, sh, L);
-    const uint4 mlt = GMUL_FIN(a, tab + t * 8192, mf0);
-    if ((q & (2 * sh - 1)) == 0) a = xor4(mlt, o);
-  }
-  // Tag (gcm.cc.inc:576-604): ((Z*H) ^ len block) * H ^ E_K(J0), in lane 0.
+  const int p = (q - r + 1) & (L - 1);
+  Gf128 z = gf_mul(to_gf(acc), gf_load(key->hpow_ct[L - p]));
+#pragma unroll
+  for (int o = L / 2; o >= 1; o >>= 1)
+#pragma unroll
+    for (int i = 0; i < 4; i++) z.w[i] ^= __shfl_xor(z.w[i], o, L);
+  // Length block be64(AD bits) || be64(message bits) in the reversed domain.
   const uint64_t abits = m.ad_len << 3, cbits = (m.len + m.xlen) << 3;
-  uint4 add = make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
-                         bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits));
-#pragma unroll 1
-  for (int t = 0; t < 2; t++) {
-    a = xor4(GMUL_FIN(a, tab, mf0), add);
-    add = s.ek0;
-  }
-  const uint4 tag = a;
+  z.w[0] ^= (uint32_t)cbits;
+  z.w[1] ^= (uint32_t)(cbits >> 32);
+  z.w[2] ^= (uint32_t)abits;
+  z.w[3] ^= (uint32_t)(abits >> 32);
+  z = gf_mul(z, gf_load(key->hpow_ct[1]));
+  const uint4 tag = xor4(from_gf(z), s.ek0);
 
   uint8_t *tagp = batch_tag(b, rec);
   int ok = live;
@@ -1034,7 +860,7 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
 // ---------------------------------------------------------------------------
 // Bulk kernel: CTR keystream + GHASH + tag for the (up to) 4 records of a
 // wave, 16 lanes per record.  `active` is per group (record in this key pass).
-// `gtab` = the key's nibble tables in global memory (record-end tree only).
+// `key` = the batch key (record-end products, finish_record).
 // L = lanes per record (16: 4 records per wave, GHASH stride H^16; 32: 2
 // records per wave, stride H^32 -- the byte table in LDS must be of H^L).
 // RP: rotate the wave's issue priority every iteration ((prio_base + it) mod
@@ -1045,9 +871,8 @@ template <int NR, bool OPEN, bool XT, int L = 16, bool RP = false>
 __device__ __forceinline__ void process_records(const RoundKeys &rk, const BatchDesc &b,
                                                 const RecState *__restrict__ st, uint64_t rec,
                                                 bool active, const uint8_t *smem,
-                                                const uint8_t *gtab, uint32_t lc0, uint32_t lc1,
-                                                uint32_t mf0, StampVec &stamps,
-                                                int prio_base = 0) {
+                                                const GcmKeyDev *key, uint32_t lc0, uint32_t lc1,
+                                                StampVec &stamps, int prio_base = 0) {
   (void)stamps;
 #if BSSL_AMD_GCM_STAMPS
   uint64_t *stv = stamps.v;
@@ -1240,9 +1065,31 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   if (it < iters) step(it, x0);
   if (it + 1 < iters) step(it + 1, x1);
 #else
+  int sync_limit = 0;
+#if BSSL_AMD_GCM_TILE_SYNC
+  if constexpr (RP) {  // (RP: the tiled path, where every wave of the workgroup is here)
+    // The tile's minimum iteration count; every wave executes the same
+    // barriers below (those at it + 1 < sync_limit).
+    uint32_t *s_min = const_cast<uint32_t *>(reinterpret_cast<const uint32_t *>(smem + kLdsPlan + 64 * 16 + 4));
+    if (threadIdx.x == 0) *s_min = 0x7fffffffu;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) atomicMin(s_min, (uint32_t)iters);
+    __syncthreads();
+    sync_limit = (int)*s_min;
+    __syncthreads();
+  }
+#endif
   uint4 x0 = load_full(q);
   int it = 0;
   for (; it + 1 < iters; it += 2) {
+#if BSSL_AMD_GCM_TILE_SYNC
+    // Tiled path (diagnostic knob): a workgroup barrier every TILE_SYNC
+    // iterations while every wave of the tile still has iterations left
+    // (sync_limit = the tile's minimum), so the SIMD arbiter's favoured waves
+    // cannot run ahead and idle at the end of the tile.  Every wave executes
+    // the same number of barriers.
+    if (RP && it > 0 && it + 1 < sync_limit && it % BSSL_AMD_GCM_TILE_SYNC == 0) __syncthreads();
+#endif
     const uint4 x1 = load_full((uint64_t)(it + 1) * L + q);
     step(it, x0);
     x0 = load_full((uint64_t)(it + 2) * L + q);
@@ -1253,7 +1100,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
 #if BSSL_AMD_GCM_STAMPS
   g_stamp_loop += stamp() - sl0;
 #endif
-  finish_record<OPEN, L>(acc, nb, m, s, b, rec, active, live, dst, gtab, mf0);
+  finish_record<OPEN, L>(acc, nb, m, s, b, rec, active, live, dst, key);
 }
 
 // Byte table of H^16 from the key's nibble tables (power 4): entry (e, p) =
@@ -1330,7 +1177,6 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
     for (int r = 0; r <= NR; r++)
 #pragma unroll
       for (int c = 0; c < 4; c++) rk.w[r][c] = keys[0].rk[r][c];
-    const uint8_t *gtab = reinterpret_cast<const uint8_t *>(keys[0].htab);
     for (;;) {
       uint32_t u = 0;
       if (lane == 0) u = atomicAdd(units, 1u);
@@ -1339,8 +1185,8 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
       if (first >= n) break;
       const uint64_t i = first + g;
       const bool active = i < n;
-      process_records<NR, OPEN, XT>(rk, b, st, active ? rec_at(b, i) : 0, active, smem, gtab, lc0,
-                                lc1, mf0, stamps);
+      process_records<NR, OPEN, XT>(rk, b, st, active ? rec_at(b, i) : 0, active, smem, keys, lc0,
+                                    lc1, stamps);
     }
 #if BSSL_AMD_GCM_STAMPS
     if (blockIdx.x < 2 && (tid & 63) == 0)
@@ -1385,7 +1231,6 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
     for (int pi = 0; pi < npass; pi++) {
       const uint32_t k = __builtin_amdgcn_readfirstlane(s_pass_key[pi]);
       const uint64_t mask = s_pass_mask[pi];
-      const uint8_t *gtab = reinterpret_cast<const uint8_t *>(keys[k].htab);
 #if BSSL_AMD_GCM_STAMPS
       const uint64_t tb0 = stamp();
 #endif
@@ -1409,7 +1254,7 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
       const int t = wave * kRecPerWave + g;
       const bool active = (mask >> t) & 1;
       process_records<NR, OPEN, XT, 16, BSSL_AMD_GCM_TILE_RP != 0>(
-          rk, b, st, active ? rec_at(b, base + t) : 0, active, smem, gtab, lc0, lc1, mf0, stamps,
+          rk, b, st, active ? rec_at(b, base + t) : 0, active, smem, keys + k, lc0, lc1, stamps,
           wave >> 2);
       if (BSSL_AMD_GCM_TILE_RP) __builtin_amdgcn_s_setprio(0);
 #if BSSL_AMD_GCM_STAMPS
@@ -1429,70 +1274,14 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
 }
 
 // ---------------------------------------------------------------------------
-// Bitsliced AES engine: AES on the VALU only, no tables.
-// 16 lanes per record, as in process_records; lane q owns the record's
-// blocks j = 512*c + 16*n + q of chunk c, n = 0..31, and encrypts those 32
-// counter blocks together as 128 bit-planes (bs_aes.h: plane (i, b) = bit b
-// of state byte i, block n in bit n).  The plaintext of one n is a coalesced
-// 256-byte run per record.  GHASH runs per lane over its blocks in order
-// with multiplier H^16 -- exactly the lane algebra of process_records -- on
-// the same lane-rotated byte table of H^16 in LDS (kLdsG8), and the record
-// ends in the same finish_record<16>.
-//
-// Code size matters: the round loop is rolled (the last round reuses the
-// S-box code with the MixColumns step skipped), and the keystream of the 32
-// blocks is read back by a rolled loop through dynamic vector indexing
-// (s_set_gpr_idx), so the engine stays a small fraction of the 64 KiB
-// instruction cache it shares with the T-table role (gcm_hy_kernel).
+// Table-free engine (opt-in, BSSL_AMD_GCM_MODE=bs16): AES on
+// the VALU only, bitsliced 16 blocks per lane (bs16_aes.h), sharing the
+// T-table kernel's lane algebra, GHASH byte table and finish_record.
 typedef uint32_t v32u __attribute__((ext_vector_type(32)));
-
-// Diagnostic ablations of the bitsliced engine (csrc/Makefile `bsablate`;
-// never in the shipped library): 1 = no GHASH step, 2 = no AES rounds,
-// 3 = no output stores, 4 = no record-end tree/tag (finish_record).
-#ifndef BSSL_AMD_BS_ABLATE
-#define BSSL_AMD_BS_ABLATE 0
-#endif
 
 // 0 or 0xffffffff: bit `k` of w (v_bfe_i32 / s_bfe_i32).
 __device__ __forceinline__ uint32_t bit_mask(uint32_t w, int k) {
   return (uint32_t)(((int32_t)(w << (31 - k))) >> 31);
-}
-
-// AES rounds 1..NR on the bit-planes (round 0 is in the planes already).
-// rkp: the key's FIPS-197 round-key words (GcmKeyDev::rk_plain), wave-uniform.
-template <int NR>
-__device__ __forceinline__ void bs_cipher(uint32_t (&p)[16][8], const uint32_t *__restrict__ rkp) {
-#pragma unroll 1
-  for (int r = 1; r <= NR; r++) {
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) w[i] = (uint32_t)__builtin_amdgcn_readfirstlane(rkp[4 * r + i]);
-    const bool last = r == NR;
-    uint32_t np[16][8];
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      uint32_t a[4][8];
-#pragma unroll
-      for (int row = 0; row < 4; row++) sbox_planes(p[row + 4 * ((c + row) & 3)], a[row]);
-      if (!last) {
-        uint32_t o[4][8];
-        bs_mix_column(a, o, w, c);
-#pragma unroll
-        for (int row = 0; row < 4; row++)
-#pragma unroll
-          for (int k = 0; k < 8; k++) np[4 * c + row][k] = o[row][k];
-      } else {
-#pragma unroll
-        for (int row = 0; row < 4; row++)
-#pragma unroll
-          for (int k = 0; k < 8; k++) np[4 * c + row][k] = a[row][k] ^ bs_kmask(w, 4 * c + row, k);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 16; i++)
-#pragma unroll
-      for (int k = 0; k < 8; k++) p[i][k] = np[i][k];
-  }
 }
 
 // 32x32 bit transpose (the swap-move network of bs_transpose32): the 16- and
@@ -1526,21 +1315,6 @@ __device__ __forceinline__ void transpose32_fast(uint32_t m[32]) {
   tr_stage<1>(m);
 }
 
-// Keystream word c of the lane's 32 blocks (after the last round p[4c+row]
-// holds row `row` of output column c).
-__device__ __forceinline__ v32u bs_column_words(const uint32_t (&p)[16][8], int c) {
-  uint32_t o[32];
-#pragma unroll
-  for (int row = 0; row < 4; row++)
-#pragma unroll
-    for (int k = 0; k < 8; k++) o[8 * row + k] = p[4 * c + row][k];
-  transpose32_fast(o);
-  v32u v;
-#pragma unroll
-  for (int n = 0; n < 32; n++) v[n] = o[n];
-  return v;
-}
-
 // x * H^16 with the lane-rotated byte table (all 16 lookups in flight).
 __device__ __forceinline__ uint4 g8_mul(uint4 x, bool rs1, bool rs2, uint32_t rbs,
                                         const uint32_t (&P)[4], const uint8_t *smem) {
@@ -1554,230 +1328,12 @@ __device__ __forceinline__ uint4 g8_mul(uint4 x, bool rs1, bool rs2, uint32_t rb
   return xor4(xor4_3(t0, t1, t2), xor4_3(t3, t4, g8_load<15>(h, P, smem)));
 }
 
-// Role B: the (up to) 4 records of a wave with the bitsliced engine.
-// Eligible batches only (gcm_bs_eligible: uniform, 16-byte-multiple,
-// 16-byte-aligned records, no extra bytes, one key).
-template <int NR, bool OPEN>
-__device__ __forceinline__ void process_records_bs(const uint32_t *__restrict__ rkp,
-                                                   const BatchDesc &b,
-                                                   const RecState *__restrict__ st, uint64_t rec,
-                                                   bool active, const uint8_t *smem,
-                                                   const uint8_t *gtab, uint32_t mf0) {
-  const int q = threadIdx.x & 15;
-  RecordMeta m = {0, 0, 0, 0, 0};
-  RecState s;
-  s.j0 = s.ek0 = s.ya = make_uint4(0, 0, 0, 0);
-  s.live = 0;
-  if (active) {
-    m = record_meta(b, rec);
-    s = st[rec];
-  }
-  m.xlen = 0;
-  const bool live = active && s.live;
-  const uint32_t nb = live ? (uint32_t)(m.len / 16) : 0u;  // nb < 2^32 (GCM length limit)
-  const uint32_t ctr0 = bswap32(s.j0.w);
-  const uint8_t *src = b.in + m.off;
-  uint8_t *dst = b.out + m.off;
-  uint4 acc = (q == 15 && live) ? s.ya : make_uint4(0, 0, 0, 0);
-  const bool rs1 = (q >> 2) & 1, rs2 = (q >> 3) & 1;
-  const uint32_t rbs = (uint32_t)q & 3u;
-  uint32_t P[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) v |= (uint32_t)(((4 * k + i + q) & 15) << 4) << (8 * i);
-    P[k] = v;
-  }
-  uint32_t rk0[4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) rk0[i] = (uint32_t)__builtin_amdgcn_readfirstlane(rkp[i]);
-  const int nchunks = wave_max((int)((nb + 511) / 512));
-  auto load_blk = [&](uint32_t j) {
-    return *reinterpret_cast<const uint4 *>(src + (uint64_t)(j < nb ? j : 0u) * 16);
-  };
-#pragma unroll 1
-  for (int c = 0; c < nchunks; c++) {
-    const uint32_t jc = 512u * (uint32_t)c + (uint32_t)q;
-    uint32_t p[16][8];
-    {
-      // Round 0: bytes 0..11 of every counter block are the record's J0
-      // (per-lane constants: all-0 / all-1 planes); word 3 holds the 32
-      // counters inc32(J0, 1 + j), transposed into planes.
-      uint32_t w0 = s.j0.x ^ rk0[0], w1 = s.j0.y ^ rk0[1], w2 = s.j0.z ^ rk0[2];
-      asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2));  // rebuilt per chunk, not hoisted
-#pragma unroll
-      for (int k = 0; k < 32; k++) {
-        p[k / 8][k % 8] = bit_mask(w0, k);
-        p[4 + k / 8][k % 8] = bit_mask(w1, k);
-        p[8 + k / 8][k % 8] = bit_mask(w2, k);
-      }
-      const uint32_t cb = ctr0 + 1u + jc;  // inc32: mod 2^32
-      uint32_t t[32];
-#pragma unroll
-      for (int n = 0; n < 32; n++) t[n] = bswap32(cb + 16u * (uint32_t)n) ^ rk0[3];
-      transpose32_fast(t);
-#pragma unroll
-      for (int k = 0; k < 32; k++) p[12 + k / 8][k % 8] = t[k];
-    }
-#if BSSL_AMD_BS_ABLATE != 2
-    bs_cipher<NR>(p, rkp);
-#endif
-    // The chunk's first input blocks are requested before the transposes.
-    uint4 xa[4], xb[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      xa[i] = load_blk(jc + 16u * i);
-      xb[i] = load_blk(jc + 16u * (4 + i));
-    }
-    v32u K0 = bs_column_words(p, 0), K1 = bs_column_words(p, 1), K2 = bs_column_words(p, 2),
-         K3 = bs_column_words(p, 3);
-    // Pass 1 (memory): out = in ^ keystream for blocks n = 0..31, inputs
-    // loaded 8 blocks ahead; the ciphertext of block n (the output when
-    // sealing, the input when opening) replaces its keystream in K.
-#pragma unroll 1
-    for (int n0 = 0; n0 < 32; n0 += 4) {
-      uint4 xc[4];  // (past the chunk: a clamped, in-bounds load whose value is unused)
-#pragma unroll
-      for (int i = 0; i < 4; i++) xc[i] = load_blk(jc + 16u * (uint32_t)(n0 + 8 + i));
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const int n = n0 + i;
-        const uint32_t j = jc + 16u * (uint32_t)n;
-        const uint4 y = xor4(xa[i], make_uint4(K0[n], K1[n], K2[n], K3[n]));
-#if BSSL_AMD_BS_ABLATE == 3
-        if (j < nb) asm volatile("" ::"v"(y.x), "v"(y.y), "v"(y.z), "v"(y.w));
-#else
-        if (j < nb) *reinterpret_cast<uint4 *>(dst + (uint64_t)j * 16) = y;
-#endif
-        const uint4 cb = OPEN ? xa[i] : y;
-        K0[n] = cb.x;
-        K1[n] = cb.y;
-        K2[n] = cb.z;
-        K3[n] = cb.w;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        xa[i] = xb[i];
-        xb[i] = xc[i];
-      }
-    }
-    // Pass 2 (LDS): the GHASH chain acc = acc * H^16 ^ C over the lane's
-    // valid blocks of the chunk.
-    const int nv = (int)min(32u, jc < nb ? (nb - jc + 15u) / 16u : 0u);
-#pragma unroll 1
-    for (int n = 0; n < 32; n++) {
-#if BSSL_AMD_BS_ABLATE == 1
-      const uint4 h = acc;
-#else
-      const uint4 h = g8_mul(acc, rs1, rs2, rbs, P, smem);
-#endif
-      if (n < nv) acc = xor4(h, make_uint4(K0[n], K1[n], K2[n], K3[n]));
-    }
-  }
-#if BSSL_AMD_BS_ABLATE == 4
-  if (active && q == 0 && b.status) b.status[rec] = live;
-  asm volatile("" ::"v"(acc.x), "v"(acc.y), "v"(acc.z), "v"(acc.w));
-#else
-  finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, gtab, mf0);
-#endif
-}
-
-// Bitsliced-only kernel (BSSL_AMD_GCM_MODE=bs): 8 waves, one workgroup per
-// CU, every wave role B; one key.
-constexpr int kBsThreads = 512;
-
-template <int NR, bool OPEN>
-__global__ __launch_bounds__(kBsThreads, 2) void gcm_bs_kernel(const GcmKeyDev *__restrict__ keys,
-                                                              BatchDesc b,
-                                                              const RecState *__restrict__ st,
-                                                              uint32_t *__restrict__ units) {
-  // [0, 64 KiB) the GHASH byte table of H^16; then the nibble tables of
-  // H, H^2, H^4, H^8 for the record-end tree (32 KiB).
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kG8Bytes + 4 * 8192];
-  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
-  build_g8<kBsThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab[4]), tid);
-  for (int e = tid; e < 4 * 8192 / 16; e += kBsThreads)
-    reinterpret_cast<uint4 *>(smem + kG8Bytes)[e] = reinterpret_cast<const uint4 *>(keys[0].htab)[e];
-  __syncthreads();
-  const uint32_t *rkp = &keys[0].rk_plain[0][0];
-  const uint8_t *gtab = smem + kG8Bytes;
-  const uint64_t n = b.num_records;
-  for (;;) {
-    uint32_t u = 0;
-    if (lane == 0) u = atomicAdd(units, 1u);
-    u = __builtin_amdgcn_readfirstlane(__shfl(u, 0, 64));
-    const uint64_t first = (uint64_t)u * kRecPerWave;
-    if (first >= n) break;
-    const uint64_t i = first + g;
-    const bool active = i < n;
-    process_records_bs<NR, OPEN>(rkp, b, st, active ? rec_at(b, i) : 0, active, smem, gtab, 0xf0u);
-  }
-}
-
-// Hybrid kernel (BSSL_AMD_GCM_MODE=hybrid): 8 waves per CU, two per SIMD;
-// the first four (one per SIMD) are role A -- the T-table engine of
-// process_records, which keeps the LDS busy and uses under half of the
-// VALU -- and the other four role B, the bitsliced engine, which needs only
-// the VALU.  Both take units of 4 records from the same counter, so the
-// split follows whatever each role sustains; both read the same GHASH byte
-// table.  One key.
-template <int NR, bool OPEN>
-__global__ __launch_bounds__(512, 2) void gcm_hy_kernel(const GcmKeyDev *__restrict__ keys,
-                                                       BatchDesc b,
-                                                       const RecState *__restrict__ st,
-                                                       uint32_t *__restrict__ units) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsPlan];
-  constexpr int kThreads = 512;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  for (int e = tid; e < 256 * 64; e += kThreads) {
-    const int idx = e >> 6, slot = (e >> 5) & 1;
-    const uint32_t v = kTables.te0[idx];
-    reinterpret_cast<uint32_t *>(smem + kLdsAes)[e] = slot ? rotl(v, 8) : v;
-  }
-  build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab[4]), tid);
-  __syncthreads();
-  const uint8_t *gtab = reinterpret_cast<const uint8_t *>(keys[0].htab);
-  const uint64_t n = b.num_records;
-  const bool role_b = wave >= 4;
-  if (!role_b) __builtin_amdgcn_s_setprio(1);  // the LDS feeder wins VALU arbitration
-  RoundKeys rk;
-  if (!role_b) {
-#pragma unroll
-    for (int r = 0; r <= NR; r++)
-#pragma unroll
-      for (int c = 0; c < 4; c++) rk.w[r][c] = keys[0].rk[r][c];
-  }
-  const uint32_t lc0 = kLdsAes + (uint32_t)(lane & 31) * 4u, lc1 = lc0 + 128u;
-  StampVec stamps = {{0, 0, 0}};
-  for (;;) {
-    uint32_t u = 0;
-    if (lane == 0) u = atomicAdd(units, 1u);
-    u = __builtin_amdgcn_readfirstlane(__shfl(u, 0, 64));
-    const uint64_t first = (uint64_t)u * kRecPerWave;
-    if (first >= n) break;
-    const uint64_t i = first + g;
-    const bool active = i < n;
-    if (role_b)
-      process_records_bs<NR, OPEN>(&keys[0].rk_plain[0][0], b, st, active ? rec_at(b, i) : 0,
-                                   active, smem, gtab, 0xf0u);
-    else
-      process_records<NR, OPEN, false>(rk, b, st, active ? rec_at(b, i) : 0, active, smem, gtab,
-                                       lc0, lc1, 0xf0u, stamps);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Mixed-role one-key kernel: the T-table role and a
-// bitsliced role that fits the T-table kernel's 128-VGPR allocation, so both
-// share each SIMD at 4 waves.  The bitsliced role (bs16) encrypts 16 blocks
-// per lane with two state columns per register: register (r, h, b) holds bit
-// b of state row r for column h in its low 16 bits (block n in bit n) and for
-// column h + 2 in its high 16 bits (block n in bit 16 + n) -- 64 VGPRs of
-// state instead of 128, and every SubBytes / MixColumns operation still works
-// on 32 bit-slots.  ShiftRows maps row r of column c to column c - r: for the
-// register pairs that is a renaming plus a swap of the two halves (rot16) of
-// 4 of the 8 (row, pair) groups per round.
+// bs16 layout: register (r, h, b) holds bit b of state row r for column h in
+// its low 16 bits (block n in bit n) and for column h + 2 in its high 16 bits
+// (block n in bit 16 + n) -- 64 VGPRs of state, and every SubBytes /
+// MixColumns operation works on 32 bit-slots.  ShiftRows maps row r of column
+// c to column c - r: for the register pairs that is a renaming plus a swap of
+// the two halves (rot16) of 4 of the 8 (row, pair) groups per round.
 
 // Keystream words of pair h: word n (< 16) = column h of block n, word
 // 16 + n = column h + 2 of block n.
@@ -1804,8 +1360,7 @@ __device__ __forceinline__ void process_records_bs16(const uint32_t *__restrict_
                                                      const BatchDesc &b,
                                                      const RecState *__restrict__ st, uint64_t rec,
                                                      bool active, const RecordMeta &m0,
-                                                     const uint8_t *smem, const uint8_t *gtab,
-                                                     uint32_t mf0) {
+                                                     const uint8_t *smem, const GcmKeyDev *key) {
   // Register budget: the rounds need ~100 VGPRs, so little else may stay live
   // across them -- the per-lane GHASH constants, J0 and the record metadata
   // are re-derived (laundered through empty asm so they are not hoisted)
@@ -1904,22 +1459,22 @@ __device__ __forceinline__ void process_records_bs16(const uint32_t *__restrict_
     m = record_meta(b, rr);
     s = st[rr];
   }
-  finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, gtab, mf0);
+  finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, key);
 }
 
-// One-key kernel with NB bs16 waves (the last NB of 16; waves w, w+4, ...
-// share a SIMD, so NB = 4 puts one on each SIMD) beside 16 - NB T-table
-// waves, all at 128 VGPRs.  Every wave takes 4-record units from one grid-wide
-// counter; a bs16 wave hands a unit to the T-table engine when any of its
-// records is unaligned, not a multiple of 16 bytes, or shorter than 4 KiB.
-template <int NR, bool OPEN, int NB>
-__global__ __launch_bounds__(1024) void gcm_mix_kernel(const GcmKeyDev *__restrict__ keys,
+// Table-free one-key kernel (BSSL_AMD_GCM_MODE=bs16): 16 waves per CU at 128
+// VGPRs, 4-record units from one grid-wide counter.  A unit whose records are
+// all 16-byte-aligned multiples of 16 bytes of >= 4 KiB runs on the bs16
+// engine; any other unit (short, ragged or unaligned records) falls back to
+// the T-table engine, so the tables are still staged.
+template <int NR, bool OPEN>
+__global__ __launch_bounds__(1024) void gcm_bs16_kernel(const GcmKeyDev *__restrict__ keys,
                                                         BatchDesc b,
                                                         const RecState *__restrict__ st,
                                                         uint32_t *__restrict__ units) {
   constexpr int kThreads = 1024;
   __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsPlan];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   for (int e = tid; e < 256 * 64; e += kThreads) {
     const int idx = e >> 6, slot = (e >> 5) & 1;
     const uint32_t v = kTables.te0[idx];
@@ -1927,13 +1482,8 @@ __global__ __launch_bounds__(1024) void gcm_mix_kernel(const GcmKeyDev *__restri
   }
   build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab[4]), tid);
   __syncthreads();
-  const uint8_t *gtab = reinterpret_cast<const uint8_t *>(keys[0].htab);
   const uint32_t *rkp = &keys[0].rk_plain[0][0];
   const uint64_t n = b.num_records;
-  const bool role_b = wave >= 16 - NB;
-#if BSSL_AMD_GCM_MIX_PRIO
-  if (!role_b) __builtin_amdgcn_s_setprio(1);
-#endif
   RoundKeys rk;
 #pragma unroll
   for (int r = 0; r <= NR; r++)
@@ -1950,46 +1500,28 @@ __global__ __launch_bounds__(1024) void gcm_mix_kernel(const GcmKeyDev *__restri
     const uint64_t i = first + g;
     const bool active = i < n;
     const uint64_t rec = active ? rec_at(b, i) : 0;
-    bool bs = false;
     RecordMeta m = {0, 0, 0, 0, 0};
-    if (role_b) {
-      if (active) m = record_meta(b, rec);
-      const bool ok = !active || (((reinterpret_cast<uintptr_t>(b.in + m.off) |
-                                    reinterpret_cast<uintptr_t>(b.out + m.off) | m.len) & 15) == 0 &&
-                                  m.len >= 4096);
-      bs = __ballot(!ok) == 0;
-    }
-    if (bs)
-      process_records_bs16<NR, OPEN>(rkp, b, st, rec, active, m, smem, gtab, 0xf0u);
+    if (active) m = record_meta(b, rec);
+    const bool ok = !active || (((reinterpret_cast<uintptr_t>(b.in + m.off) |
+                                  reinterpret_cast<uintptr_t>(b.out + m.off) | m.len) & 15) == 0 &&
+                                m.len >= 4096);
+    if (__ballot(!ok) == 0)
+      process_records_bs16<NR, OPEN>(rkp, b, st, rec, active, m, smem, keys);
     else
-      process_records<NR, OPEN, false>(rk, b, st, rec, active, smem, gtab, lc0, lc1, 0xf0u,
-                                       stamps);
+      process_records<NR, OPEN, false>(rk, b, st, rec, active, smem, keys, lc0, lc1, stamps);
   }
 }
 
 int g_num_cus = 0;
 
 
-// 0 = T-table kernel, 1 = bitsliced-only, 2 = hybrid (BSSL_AMD_GCM_MODE =
-// table | bs | hybrid) for batches the bitsliced engine takes: uniform,
-// 16-byte-multiple, 16-byte-aligned records of >= 4 KiB, one key, no extra
-// bytes.
+// Engine for a batch: 0 = T-table kernel (default), 1 = the table-free bs16
+// kernel (BSSL_AMD_GCM_MODE=bs16; one-key batches without extra bytes -- its
+// waves check their units' records themselves).
 int gcm_mode(const BatchDesc &b) {
   const char *e = getenv("BSSL_AMD_GCM_MODE");
-  int mode = 0;
-  if (e && !strcmp(e, "bs")) mode = 1;
-  if (e && !strcmp(e, "hybrid")) mode = 2;
-  // Mixed-role kernel (gcm_mix_kernel): its bs16 waves check their units'
-  // records themselves, so any one-key batch without extra bytes qualifies.
-  if (e && !strcmp(e, "mix4")) mode = 3;
-  if (e && !strcmp(e, "mix8")) mode = 4;
-  if (e && !strcmp(e, "bs16")) mode = 5;  // every wave bs16 (no T-tables on eligible units)
-  if (mode >= 3) return (b.extra_len || b.key_index) ? 0 : mode;
-  if (!mode || b.lengths || b.offsets || b.extra_len || b.tag_stride || b.key_index) return 0;
-  if ((b.record_len | b.record_stride | reinterpret_cast<uintptr_t>(b.in) |
-       reinterpret_cast<uintptr_t>(b.out)) & 15)
-    return 0;
-  return b.record_len >= 4096 ? mode : 0;
+  if (!e || strcmp(e, "bs16") || b.extra_len || b.key_index) return 0;
+  return 1;
 }
 
 template <int NR, bool OPEN>
@@ -2033,29 +1565,12 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
   const int mode = gcm_mode(b);
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
   const RecState *cst = st;
-  if (mode >= 3) {
+  if (mode == 1) {
     const uint64_t units_needed = (b.num_records + 4 * 16 - 1) / (4 * 16);
     const unsigned grid = (unsigned)(units_needed < (uint64_t)g_num_cus ? units_needed
                                                                        : (uint64_t)g_num_cus);
-    if (mode == 3)
-      hipLaunchKernelGGL((gcm_mix_kernel<NR, OPEN, 4>), dim3(grid), dim3(1024), 0, s, keys, bo,
-                         cst, units);
-    else if (mode == 4)
-      hipLaunchKernelGGL((gcm_mix_kernel<NR, OPEN, 8>), dim3(grid), dim3(1024), 0, s, keys, bo,
-                         cst, units);
-    else
-      hipLaunchKernelGGL((gcm_mix_kernel<NR, OPEN, 16>), dim3(grid), dim3(1024), 0, s, keys, bo,
-                         cst, units);
-  } else if (mode) {
-    const uint64_t units_needed = (b.num_records + 4 * 8 - 1) / (4 * 8);
-    const unsigned grid = (unsigned)(units_needed < (uint64_t)g_num_cus ? units_needed
-                                                                       : (uint64_t)g_num_cus);
-    if (mode == 1)
-      hipLaunchKernelGGL((gcm_bs_kernel<NR, OPEN>), dim3(grid), dim3(kBsThreads), 0, s, keys, bo,
-                         cst, units);
-    else
-      hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN>), dim3(grid), dim3(512), 0, s, keys, bo, cst,
-                         units);
+    hipLaunchKernelGGL((gcm_bs16_kernel<NR, OPEN>), dim3(grid), dim3(1024), 0, s, keys, bo, cst,
+                       units);
   } else {
     const uint64_t tiles = (b.num_records + kWaves * kRecPerWave - 1) / (kWaves * kRecPerWave);
     const unsigned grid = (unsigned)(tiles < (uint64_t)g_num_cus ? tiles : (uint64_t)g_num_cus);

@@ -33,9 +33,11 @@
 namespace bssl_amd {
 namespace {
 
-// BSSL_AMD_SIV_REP = 1: T0/T1 replicated 32x in LDS (lane l reads bank l, as
-// gcm.hip) with T2/T3 = rot16(T0/T1); the 64 KiB table then takes one
-// 768-thread workgroup (48 records) per CU.  0 = four plain 1 KiB tables.
+// AES tables: T0 alone, replicated once per LDS bank (entry x for lane l at
+// t[x][l & 31], 32 KiB), so every lookup of a wave is bank-conflict free
+// whatever the (secret) index -- the constant-time argument of gcm.hip's
+// tables; T1..T3 are rotations of T0.  (Round 1/2 used
+// four plain 1 KiB tables, whose bank conflicts depend on the data.)
 // BSSL_AMD_SIV_SPLIT = 1: the per-block multiply by H^16 as four independent
 // Shoup chains (gmul4) instead of one 32-step chain.
 #ifndef BSSL_AMD_SIV_SPLIT
@@ -65,11 +67,10 @@ namespace {
 #ifndef BSSL_AMD_SIV_CTRCACHE
 #define BSSL_AMD_SIV_CTRCACHE 0
 #endif
-#ifndef BSSL_AMD_SIV_REP
-#define BSSL_AMD_SIV_REP 0
-#endif
 constexpr int kL = 16;                // lanes per record
-constexpr int kThreads = BSSL_AMD_SIV_REP ? 768 : 256;
+// 384 threads (24 records, 6 waves): two workgroups per CU fit the LDS
+// (2 x 68.5 KiB) and the 168-VGPR budget (3 waves per SIMD).
+constexpr int kThreads = 384;
 constexpr int kRecs = kThreads / kL;  // records per workgroup
 constexpr int kPows = 5;              // H, H^2, H^4, H^8, H^16
 
@@ -112,40 +113,26 @@ constexpr Tables make_tables() {
 __constant__ Tables kSivTables = make_tables();
 
 struct Lds {
-#if BSSL_AMD_SIV_REP
-  uint32_t t[256][2][32];      // entry, T0 / T1 = rotl(T0, 8), replica (lane & 31)
-#else
-  uint32_t t[4][256];          // T0..T3 (T_r = rotl(T0, 8r))
-#endif
+  uint32_t t[256][32];         // T0, replica (lane & 31)
   uint4 rk[kRecs][15];         // each record's encryption round keys
   uint4 m[kRecs][kPows][16];   // each record's Shoup tables
 };
-static_assert(sizeof(Lds) <= 160 * 1024, "LDS per workgroup");
+static_assert(2 * sizeof(Lds) <= 160 * 1024, "two workgroups per CU");
 
 __device__ __forceinline__ uint32_t rotl(uint32_t v, int n) {
   return __builtin_amdgcn_alignbit(v, v, 32 - n);
 }
 
-#if BSSL_AMD_SIV_REP
-__device__ __forceinline__ uint32_t tlook(const Lds &L, int t, uint32_t x) {
-  return L.t[x][t][threadIdx.x & 31];
+__device__ __forceinline__ uint32_t t0(const Lds &L, uint32_t x) {
+  return L.t[x][threadIdx.x & 31];
 }
 __device__ __forceinline__ uint32_t sbox(const Lds &L, uint32_t x) {
-  return (tlook(L, 0, x) >> 8) & 0xff;
+  return (t0(L, x) >> 8) & 0xff;
 }
-#else
-__device__ __forceinline__ uint32_t sbox(const Lds &L, uint32_t x) {
-  return (L.t[0][x] >> 8) & 0xff;
-}
-#endif
 
 // Table T_t[x] (T_t = rotl(T0, 8t)).
 __device__ __forceinline__ uint32_t tt(const Lds &L, int t, uint32_t x) {
-#if BSSL_AMD_SIV_REP
-  return t < 2 ? tlook(L, t, x) : rotl(tlook(L, t - 2, x), 16);
-#else
-  return L.t[t][x];
-#endif
+  return t ? rotl(t0(L, x), 8 * t) : t0(L, x);
 }
 
 // FIPS-197 cipher on little-endian column words, from round R0 on (s = the
@@ -156,25 +143,14 @@ __device__ __forceinline__ uint4 aes_enc_from(uint32_t s0, uint32_t s1, uint32_t
 #pragma unroll
   for (int r = R0; r < NR; r++) {
     const uint4 k = rk[r];
-#if BSSL_AMD_SIV_REP
-    // T2[c] ^ T3[d] = rot16(T0[c] ^ T1[d])
+    // T0[a] ^ T1[b] ^ T2[c] ^ T3[d] = T0[a] ^ rotl8(T0[b] ^ rotl8(T0[c] ^ rotl8(T0[d])))
     auto col = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t kk) {
-      return tlook(L, 0, a & 0xff) ^ tlook(L, 1, (b >> 8) & 0xff) ^
-             rotl(tlook(L, 0, (c >> 16) & 0xff) ^ tlook(L, 1, d >> 24), 16) ^ kk;
+      const uint32_t x = rotl(t0(L, (c >> 16) & 0xff) ^ rotl(t0(L, d >> 24), 8), 8);
+      return t0(L, a & 0xff) ^ rotl(t0(L, (b >> 8) & 0xff) ^ x, 8) ^ kk;
     };
-    const uint32_t t0 = col(s0, s1, s2, s3, k.x), t1 = col(s1, s2, s3, s0, k.y),
+    const uint32_t t0v = col(s0, s1, s2, s3, k.x), t1 = col(s1, s2, s3, s0, k.y),
                    t2 = col(s2, s3, s0, s1, k.z), t3 = col(s3, s0, s1, s2, k.w);
-#else
-    const uint32_t t0 = L.t[0][s0 & 0xff] ^ L.t[1][(s1 >> 8) & 0xff] ^
-                        L.t[2][(s2 >> 16) & 0xff] ^ L.t[3][s3 >> 24] ^ k.x;
-    const uint32_t t1 = L.t[0][s1 & 0xff] ^ L.t[1][(s2 >> 8) & 0xff] ^
-                        L.t[2][(s3 >> 16) & 0xff] ^ L.t[3][s0 >> 24] ^ k.y;
-    const uint32_t t2 = L.t[0][s2 & 0xff] ^ L.t[1][(s3 >> 8) & 0xff] ^
-                        L.t[2][(s0 >> 16) & 0xff] ^ L.t[3][s1 >> 24] ^ k.z;
-    const uint32_t t3 = L.t[0][s3 & 0xff] ^ L.t[1][(s0 >> 8) & 0xff] ^
-                        L.t[2][(s1 >> 16) & 0xff] ^ L.t[3][s2 >> 24] ^ k.w;
-#endif
-    s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    s0 = t0v; s1 = t1; s2 = t2; s3 = t3;
   }
   const uint4 k = rk[NR];
   auto last = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
@@ -438,20 +414,7 @@ template <int NR, bool OPEN>
 __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyDev *__restrict__ keys,
                                                            BatchDesc b) {
   __shared__ Lds L;
-#if BSSL_AMD_SIV_REP
-  for (int e = threadIdx.x; e < 256 * 64; e += kThreads) {
-    const uint32_t v = kSivTables.te0[e >> 6];
-    (&L.t[0][0][0])[e] = ((e >> 5) & 1) ? rotl(v, 8) : v;
-  }
-#else
-  for (int e = threadIdx.x; e < 256; e += kThreads) {
-    const uint32_t v = kSivTables.te0[e];
-    L.t[0][e] = v;
-    L.t[1][e] = rotl(v, 8);
-    L.t[2][e] = rotl(v, 16);
-    L.t[3][e] = rotl(v, 24);
-  }
-#endif
+  for (int e = threadIdx.x; e < 256 * 32; e += kThreads) (&L.t[0][0])[e] = kSivTables.te0[e >> 5];
   __syncthreads();
   const RecLanes R = rec_lanes();
   const int q = R.q;

@@ -6,6 +6,7 @@
 // record data never touches this code.
 #include <string.h>
 
+#include "gf128_ct.h"
 #include "internal.h"
 
 namespace bssl_amd {
@@ -52,12 +53,25 @@ const SboxTable &sbox() {
   return t;
 }
 
-uint8_t xtime(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0)); }
+// S[x] for a secret x (key bytes, the state computing H = E_K(0)): every
+// entry is read and the wanted one selected by a mask, so the host's cache
+// never sees an address that depends on x (the reference keeps its key
+// schedule constant-time too, aes_nohw.cc.inc:935-961).
+uint8_t sbox_ct(uint8_t x) {
+  const uint8_t *S = sbox().s;
+  uint32_t r = 0;
+  for (uint32_t i = 0; i < 256; i++) {
+    const uint32_t eq = ((i ^ x) - 1u) >> 8 & 1u;  // 1 iff i == x
+    r |= S[i] & (0u - eq);
+  }
+  return (uint8_t)r;
+}
+
+uint8_t xtime(uint8_t a) { return (uint8_t)((a << 1) ^ (0x1b & (0u - (a >> 7)))); }
 
 // FIPS-197 KeyExpansion; returns the number of rounds, 0 on a bad length.
 int expand_key(const uint8_t *key, size_t key_len, uint8_t w[240]) {
   if (key_len != 16 && key_len != 24 && key_len != 32) return 0;
-  const uint8_t *S = sbox().s;
   int nk = (int)key_len / 4, nr = nk + 6;
   memcpy(w, key, key_len);
   uint8_t rcon = 1;
@@ -66,13 +80,13 @@ int expand_key(const uint8_t *key, size_t key_len, uint8_t w[240]) {
     memcpy(t, w + 4 * (i - 1), 4);
     if (i % nk == 0) {
       uint8_t t0 = t[0];
-      t[0] = S[t[1]] ^ rcon;
-      t[1] = S[t[2]];
-      t[2] = S[t[3]];
-      t[3] = S[t0];
+      t[0] = sbox_ct(t[1]) ^ rcon;
+      t[1] = sbox_ct(t[2]);
+      t[2] = sbox_ct(t[3]);
+      t[3] = sbox_ct(t0);
       rcon = xtime(rcon);
     } else if (nk == 8 && i % nk == 4) {
-      for (auto &b : t) b = S[b];
+      for (auto &b : t) b = sbox_ct(b);
     }
     for (int j = 0; j < 4; j++) w[4 * i + j] = w[4 * (i - nk) + j] ^ t[j];
   }
@@ -80,13 +94,12 @@ int expand_key(const uint8_t *key, size_t key_len, uint8_t w[240]) {
 }
 
 void encrypt_block(const uint8_t *w, int nr, const uint8_t in[16], uint8_t out[16]) {
-  const uint8_t *S = sbox().s;
   uint8_t s[16];
   for (int i = 0; i < 16; i++) s[i] = in[i] ^ w[i];
   for (int r = 1; r <= nr; r++) {
     uint8_t t[16];
     for (int c = 0; c < 4; c++)
-      for (int row = 0; row < 4; row++) t[4 * c + row] = S[s[4 * ((c + row) & 3) + row]];
+      for (int row = 0; row < 4; row++) t[4 * c + row] = sbox_ct(s[4 * ((c + row) & 3) + row]);
     if (r != nr)
       for (int c = 0; c < 4; c++) {
         uint8_t *a = t + 4 * c;
@@ -126,22 +139,21 @@ void store_u128(U128 v, uint8_t b[16]) {
 
 // Multiply by x: a right shift in GCM's reflected bit order, reducing by
 // x^128 + x^7 + x^2 + x + 1 (0xE1 || 0^120).
+// (Branch-free: H and its powers are secret.)
 U128 mulx(U128 v) {
-  uint64_t carry = v.lo & 1;
+  const uint64_t carry = 0 - (v.lo & 1);
   v.lo = (v.lo >> 1) | (v.hi << 63);
   v.hi >>= 1;
-  if (carry) v.hi ^= UINT64_C(0xE1) << 56;
+  v.hi ^= carry & (UINT64_C(0xE1) << 56);
   return v;
 }
 
 U128 gf_mul(U128 x, U128 y) {
   U128 z{0, 0};
   for (int i = 0; i < 128; i++) {
-    uint64_t bit = i < 64 ? (x.hi >> (63 - i)) & 1 : (x.lo >> (127 - i)) & 1;
-    if (bit) {
-      z.hi ^= y.hi;
-      z.lo ^= y.lo;
-    }
+    const uint64_t bit = 0 - (i < 64 ? (x.hi >> (63 - i)) & 1 : (x.lo >> (127 - i)) & 1);
+    z.hi ^= y.hi & bit;
+    z.lo ^= y.lo & bit;
     y = mulx(y);
   }
   return z;
@@ -175,6 +187,23 @@ bool gcm_key_setup(const uint8_t *key, size_t key_len, GcmKeyDev *out) {
   uint8_t hb[16] = {0};
   encrypt_block(w, nr, hb, hb);  // H = E_K(0^128), gcm.cc.inc:270-272
   U128 p = load_u128(hb);
+  {
+    // H^1 .. H^16 as constant-time multipliers (gf128_ct.h): the reversed
+    // domain is the big-endian integer of the block, i.e. hi:lo.
+    U128 hk = p;
+    for (int k = 1; k <= 16; k++) {
+      Gf128 g;
+      g.w[3] = (uint32_t)(hk.hi >> 32);
+      g.w[2] = (uint32_t)hk.hi;
+      g.w[1] = (uint32_t)(hk.lo >> 32);
+      g.w[0] = (uint32_t)hk.lo;
+      const Gf128 gp = gf_prep(g);
+      for (int j = 0; j < 4; j++) out->hpow_ct[k][j] = gp.w[j];
+      secure_zero(&g, sizeof(g));
+      hk = gf_mul(hk, p);
+    }
+    secure_zero(&hk, sizeof(hk));
+  }
   for (int pw = 0; pw < kGhashPowers; pw++) {
     U128 v[128];
     v[0] = p;

@@ -179,7 +179,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true")
     ap.add_argument("--only", default="", help="regenerate just this digest entry")
+    ap.add_argument("--tls-only", action="store_true", help="regenerate ref_tls.json only")
     args = ap.parse_args()
+    if args.tls_only:
+        return write_ref_tls()
     if args.only:
         return digest_entries(lambda name: name == args.only)
     aead = convert_aead()
@@ -208,7 +211,20 @@ def main():
         json.dump(edge, f, indent=0)
     print(f"ref_edge.json: {len(edge)} cases")
 
+    write_ref_tls()
     return digest_entries(lambda name: not (args.skip_full and name.startswith("config")))
+
+
+def write_ref_tls():
+    """ref_tls.json: TLS 1.2/1.3 records sealed by the reference's own
+    SSLAEADContext (oracle/_ref/ref_tls, built from /root/reference/ssl)."""
+    tool = os.path.join(ROOT, "oracle", "_ref", "ref_tls")
+    if not os.path.exists(tool):
+        subprocess.check_call(["make", "-j8", "-C", os.path.join(ROOT, "oracle", "ref")])
+    recs = json.loads(subprocess.check_output([tool]))
+    with open(os.path.join(HERE, "ref_tls.json"), "w") as f:
+        json.dump(recs, f, indent=0)
+    print(f"ref_tls.json: {sum(len(r['records']) for r in recs)} records")
 
 
 def digest_entries(want):

@@ -19,6 +19,7 @@ torch = pytest.importorskip("torch")
 import boringssl_amd as ba  # noqa: E402
 import oracle_lib as o  # noqa: E402
 from golden_util import AEAD_KEYLEN, batch_digests, load  # noqa: E402
+import tls_util  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -230,14 +231,13 @@ def test_batch_large_ragged_reordered(aead, multikey):
     assert st.all() and back == ins
 
 
-@pytest.mark.parametrize("mode", ["bs", "hybrid", "mix4", "mix8", "bs16"])
+@pytest.mark.parametrize("mode", ["bs16"])
 @pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-192-gcm", "aes-256-gcm"])
 @pytest.mark.parametrize("rlen", [4096, 16384, 17408, 32768])
 def test_bitsliced_gcm_path(aead, rlen, mode, monkeypatch):
-    """The bitsliced engine (BSSL_AMD_GCM_MODE=bs: every wave; =hybrid: half
-    the waves, beside the T-table engine) on uniform, 16-byte-multiple
-    records: full and partial 512-block chunks, seal and open (tags verified,
-    one tampered record)."""
+    """The table-free engine (BSSL_AMD_GCM_MODE=bs16, gcm_bs16_kernel) on
+    uniform, 16-byte-multiple records: full and partial 256-block chunks,
+    seal and open (tags verified, one tampered record)."""
     monkeypatch.setenv("BSSL_AMD_GCM_MODE", mode)
     rng = np.random.default_rng(rlen + len(mode))
     n = 50
@@ -273,13 +273,14 @@ def test_bitsliced_gcm_path(aead, rlen, mode, monkeypatch):
     assert np.array_equal(np.delete(back.reshape(n, rlen), 7, 0), np.delete(pt.reshape(n, rlen), 7, 0))
 
 
-@pytest.mark.parametrize("mode", ["mix4", "mix8", "bs16"])
+@pytest.mark.parametrize("mode", ["bs16"])
 @pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm"])
 def test_mix_kernel_ragged(aead, mode, monkeypatch):
-    """The mixed-role kernel (gcm_mix_kernel) on a ragged one-key batch: its
-    bitsliced waves take only units whose 4 records are 16-byte-aligned
-    multiples of 16 bytes of >= 4 KiB and hand the rest to the T-table engine
-    -- every record must match the oracle either way, sealed and opened."""
+    """The table-free kernel (gcm_bs16_kernel) on a ragged one-key batch: its
+    waves take the bs16 engine only for units whose 4 records are
+    16-byte-aligned multiples of 16 bytes of >= 4 KiB and the T-table engine
+    otherwise -- every record must match the oracle either way, sealed and
+    opened."""
     monkeypatch.setenv("BSSL_AMD_GCM_MODE", mode)
     rng = random.Random(len(mode) * 7 + len(aead))
     key = bytes(rng.getrandbits(8) for _ in range(AEAD_KEYLEN[aead]))
@@ -649,27 +650,7 @@ def test_tls_batch_rejections():
 # on top of the oracle's AEAD.
 
 def _tls_seal_oracle(version, aead, key, fixed_iv, seq0, records, types):
-    tls13 = version == ba.TLS1_3_VERSION
-    chacha = aead == "chacha20-poly1305"
-    aid = o.CHACHA20_POLY1305 if chacha else o.AES_GCM
-    out = []
-    for i, (pt, typ) in enumerate(zip(records, types)):
-        seq = (seq0 + i).to_bytes(8, "big")
-        if tls13 or chacha:  # ssl_aead_ctx.cc:96-103, 326-336, 367-373
-            nonce, explicit = bytes(a ^ b for a, b in zip(fixed_iv, bytes(4) + seq)), b""
-        else:                # fixed IV || explicit nonce in the record (:104-110, 355-365)
-            nonce, explicit = fixed_iv + seq, seq
-        extra = bytes([typ]) if tls13 else b""  # tls_record.cc:272-276
-        ctlen = len(explicit) + len(pt) + len(extra) + 16
-        hdr = bytes([23 if tls13 else typ, 3, 3, ctlen >> 8, ctlen & 0xff])  # :287-298
-        ad = hdr if tls13 else seq + bytes([typ, 3, 3]) + len(pt).to_bytes(2, "big")  # :207-224
-        if len(pt) > 16384:
-            out.append(None)
-            continue
-        ok, ct, tag = o.seal(aid, key, nonce, pt + extra, ad)
-        assert ok
-        out.append((hdr + explicit, ct[:len(pt)], ct[len(pt):] + tag))
-    return out
+    return tls_util.tls_seal_restated(version, aead, key, fixed_iv, seq0, records, types)
 
 
 @pytest.mark.parametrize("version,aead", [(0x0303, "aes-128-gcm"), (0x0303, "aes-256-gcm"),

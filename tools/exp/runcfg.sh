@@ -3,8 +3,8 @@ set -e
 mkdir -p gpurun_out
 B=boringssl_amd/csrc/build
 for rep in ${REPS:-1 2}; do
-  timeout -k 10 200 python bench.py --config $CFG --steps ${STEPS:-5} --warmup 3 --no-cpu-baseline > gpurun_out/c_${CFG}_main_$rep.log 2>&1
+  timeout -k 10 200 python bench.py --config $CFG --steps ${STEPS:-5} --warmup 3 --no-cpu-baseline --no-parity > gpurun_out/c_${CFG}_main_$rep.log 2>&1
   for v in ${VARS:-}; do
-    BSSL_AMD_LIB=$PWD/$B/$v/libbssl_amd.so timeout -k 10 200 python bench.py --config $CFG --steps ${STEPS:-5} --warmup 3 --no-cpu-baseline > gpurun_out/c_${CFG}_${v}_$rep.log 2>&1
+    BSSL_AMD_LIB=$PWD/$B/$v/libbssl_amd.so timeout -k 10 200 python bench.py --config $CFG --steps ${STEPS:-5} --warmup 3 --no-cpu-baseline --no-parity > gpurun_out/c_${CFG}_${v}_$rep.log 2>&1
   done
 done
