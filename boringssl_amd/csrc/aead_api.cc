@@ -250,6 +250,7 @@ int launch_desc(const KeyMaterial *km, const BatchDesc &d, bool open, void *stre
 int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch, bool open,
               bool use_key_index, void *stream, const uint8_t *valid = nullptr) {
   BatchDesc d;
+  memset(&d, 0, sizeof(d));
   d.in = batch->in;
   d.out = batch->out;
   d.offsets = batch->offsets;
@@ -1040,6 +1041,8 @@ struct KeyRunner : IovRunner {
     d.valid = valid;
     return launch_desc(km, d, open, stream);
   }
+  // AES-GCM walks the chunks inside its kernels (gcm.hip, IOV).
+  bool in_place() const override { return km->aead->kind == kAeadAesGcm; }
 };
 
 bool check_iov_batch(const EVP_AEAD *aead, const BSSL_AMD_IOV_BATCH *b) {

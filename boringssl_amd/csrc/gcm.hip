@@ -32,6 +32,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "internal.h"
 #include "bs16_aes.h"
 #include "gf128_ct.h"
@@ -93,6 +95,10 @@ constexpr int kRecPerWave = 4;
 // Tiled (multi-key) path: rotating wave priorities (process_records RP).
 #ifndef BSSL_AMD_GCM_TILE_RP
 #define BSSL_AMD_GCM_TILE_RP 1
+#endif
+// VALU GHASH on every second iteration (diagnostic knob, see process_records).
+#ifndef BSSL_AMD_GCM_VGHASH
+#define BSSL_AMD_GCM_VGHASH 0
 #endif
 // Tiled path: workgroup barrier every N iterations (0 = off; even N).
 #ifndef BSSL_AMD_GCM_TILE_SYNC
@@ -402,14 +408,14 @@ __device__ __forceinline__ uint32_t gh_word(const Gh8 &h) {
 // next block of the lane, its cached rounds 1 and 2 (software pipelining:
 // the next iteration starts at round 3): round i = 0 issues the round-1
 // lookup of `xs` (its round-0 word 3), round i = 1 the four round-2 lookups.
-template <int I, int NR>
+template <int I, int NR, bool NOG = false>
 __device__ __forceinline__ void rounds_s1(uint32_t (&a)[4], const RoundKeys &rk, uint32_t lc0,
                                           uint32_t lc1, Gh8 &h, const uint32_t (&P)[4],
                                           uint32_t &xs, const WindowCache &wc, uint32_t k0,
                                           uint32_t (&nx)[4]) {
   constexpr int R = I + 3;
   if constexpr (R < NR) {
-    constexpr int NG = g_steps<NR>(I);
+    constexpr int NG = NOG ? 0 : g_steps<NR>(I);  // NOG: this block's GHASH step on the VALU
     constexpr int T = g_first<NR>(I);
     constexpr int X = I == 0 ? 1 : I == 1 ? 4 : 0;
     uint32_t xo[X > 0 ? X : 1];
@@ -461,7 +467,7 @@ __device__ __forceinline__ void rounds_s1(uint32_t (&a)[4], const RoundKeys &rk,
       nx[2] = xo[2];
       nx[3] = xo[3];
     }
-    rounds_s1<I + 1, NR>(a, rk, lc0, lc1, h, P, xs, wc, k0, nx);
+    rounds_s1<I + 1, NR, NOG>(a, rk, lc0, lc1, h, P, xs, wc, k0, nx);
   }
 }
 
@@ -654,6 +660,133 @@ __device__ __forceinline__ uint64_t rec_at(const BatchDesc &b, uint64_t i) {
 }
 
 
+// ---------------------------------------------------------------------------
+// iovec records walked in place (BatchDesc::iovecs; reference
+// EVP_AEAD_CTX_sealv / _openv_detached, aead.cc.inc:316-361, 531-584, whose
+// AEADs walk the chunks with ForEachBlockRange, cipher/internal.h:283-411).
+// A lane keeps a cursor on the chunk holding its current stream position:
+// chunk c covers stream bytes [cs, ce) of the record.
+struct IovCur {
+  uint64_t c, cs, ce;
+  const uint8_t *in;
+  uint8_t *out;
+};
+
+__device__ __forceinline__ void iov_at(IovCur &k, const BatchDesc &b, uint64_t c, uint64_t cs) {
+  const IovecDev v = b.iovecs[c];
+  k.c = c;
+  k.cs = cs;
+  k.ce = cs + v.len;
+  k.in = v.in;
+  k.out = v.out;
+}
+
+// Advance to the chunk holding stream byte p (positions only grow).
+__device__ __forceinline__ void iov_seek(IovCur &k, const BatchDesc &b, uint64_t p,
+                                         uint64_t c_end) {
+  while (p >= k.ce && k.c + 1 < c_end) iov_at(k, b, k.c + 1, k.ce);
+}
+
+// 16 bytes at any address: one aligned 16-byte load, or two and a byte shift
+// (both loads stay inside the 16-byte granules that hold the wanted bytes).
+__device__ __forceinline__ uint4 iov_load16(const uint8_t *src) {
+  const uint32_t a = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
+  if (a == 0) return load_blk_nt(src);
+  const uint4 A = load_blk_nt(src - a), B = load_blk_nt(src - a + 16);
+  const uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+  const uint32_t wq = a >> 2, r = a & 3;
+  uint32_t t[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++)
+    t[i] = wq == 0 ? w[i] : wq == 1 ? w[i + 1] : wq == 2 ? w[i + 2] : w[i + 3];
+  return make_uint4(__builtin_amdgcn_alignbyte(t[1], t[0], r),
+                    __builtin_amdgcn_alignbyte(t[2], t[1], r),
+                    __builtin_amdgcn_alignbyte(t[3], t[2], r),
+                    __builtin_amdgcn_alignbyte(t[4], t[3], r));
+}
+
+// 16 bytes to any address: one aligned 16-byte store; else dword stores
+// where dst is 4-byte aligned, or head bytes, 3 aligned dwords and tail
+// bytes (a neighbour lane's block shares the head / tail dwords, written
+// with byte-masked stores).
+__device__ __forceinline__ void iov_store16(uint8_t *dst, uint4 y) {
+  const uint32_t a = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15);
+  if (a == 0) {
+    store_blk_nt(dst, y);
+    return;
+  }
+  const uint32_t w[4] = {y.x, y.y, y.z, y.w};
+  const uint32_t r = a & 3;
+  if (r == 0) {
+    uint32_t *p = reinterpret_cast<uint32_t *>(dst);
+    p[0] = w[0];
+    p[1] = w[1];
+    p[2] = w[2];
+    p[3] = w[3];
+    return;
+  }
+  const uint32_t h = 4 - r;  // head bytes before the first aligned dword
+  if (h & 1) dst[0] = (uint8_t)w[0];
+  if (h & 2) *reinterpret_cast<uint16_t *>(dst + (h & 1)) = (uint16_t)(w[0] >> (8 * (h & 1)));
+  uint32_t *pm = reinterpret_cast<uint32_t *>(dst + h);
+  pm[0] = __builtin_amdgcn_alignbyte(w[1], w[0], h);
+  pm[1] = __builtin_amdgcn_alignbyte(w[2], w[1], h);
+  pm[2] = __builtin_amdgcn_alignbyte(w[3], w[2], h);
+  uint8_t *t = dst + h + 12;  // r tail bytes: bytes h + 12 .. 15
+  const uint32_t tw = w[3] >> (8 * h);
+  if (r & 2) *reinterpret_cast<uint16_t *>(t) = (uint16_t)tw;
+  if (r & 1) t[r & 2] = (uint8_t)(tw >> (8 * (r & 2)));
+}
+
+// Bytes [p, p + n) of the record's stream (n <= 16, zero past n), byte by
+// byte across chunk boundaries (blocks that straddle chunks, the last block).
+__device__ __forceinline__ uint4 iov_gather(const BatchDesc &b, IovCur k, uint64_t p, uint32_t n,
+                                            uint64_t c_end) {
+  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    iov_seek(k, b, p + i, c_end);
+    const uint32_t v = (uint32_t)k.in[p + i - k.cs] << (8 * (i & 3));
+    const uint32_t wi = i >> 2;
+    w0 |= wi == 0 ? v : 0u;
+    w1 |= wi == 1 ? v : 0u;
+    w2 |= wi == 2 ? v : 0u;
+    w3 |= wi == 3 ? v : 0u;
+  }
+  return make_uint4(w0, w1, w2, w3);
+}
+
+__device__ __forceinline__ void iov_scatter(const BatchDesc &b, IovCur k, uint64_t p, uint4 y,
+                                            uint32_t n, uint64_t c_end) {
+  const uint32_t w[4] = {y.x, y.y, y.z, y.w};
+  for (uint32_t i = 0; i < n; i++) {
+    iov_seek(k, b, p + i, c_end);
+    const uint32_t wi = i >> 2;
+    const uint32_t v = wi == 0 ? w[0] : wi == 1 ? w[1] : wi == 2 ? w[2] : w[3];
+    k.out[p + i - k.cs] = (uint8_t)(v >> (8 * (i & 3)));
+  }
+}
+
+// Bytes [pos, pos + n) of the concatenation of chunks v[c0 .. c1) (AD of an
+// iovec record; n <= 16, zero past n).  Walks from c0: the AD is short.
+__device__ __forceinline__ uint4 ivec_load16(const IvecDev *v, uint64_t c0, uint64_t c1,
+                                             uint64_t pos, uint32_t n) {
+  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+  uint64_t c = c0, cs = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    while (c < c1 && pos + i >= cs + v[c].len) {
+      cs += v[c].len;
+      c++;
+    }
+    const uint32_t x = (uint32_t)v[c].in[pos + i - cs] << (8 * (i & 3));
+    const uint32_t wi = i >> 2;
+    w0 |= wi == 0 ? x : 0u;
+    w1 |= wi == 1 ? x : 0u;
+    w2 |= wi == 2 ? x : 0u;
+    w3 |= wi == 3 ? x : 0u;
+  }
+  return make_uint4(w0, w1, w2, w3);
+}
+
 // Per-record state handed from the prologue to the bulk kernel (64 bytes).
 struct alignas(16) RecState {
   uint4 j0;   // pre-counter block J0 (gcm.cc.inc:316-338)
@@ -785,7 +918,10 @@ __global__ __launch_bounds__(256) void gcm_prologue(const GcmKeyDev *__restrict_
     const uint8_t *ad = b.ad + m.ad_off;
     Gf128 ya = {{0, 0, 0, 0}};
     for (uint64_t o = 0; o < m.ad_len; o += 16) {
-      const Gf128 blk = to_gf(load_partial(ad + o, (uint32_t)min<uint64_t>(m.ad_len - o, 16)));
+      const uint32_t n = (uint32_t)min<uint64_t>(m.ad_len - o, 16);
+      const Gf128 blk = to_gf(b.aadvecs ? ivec_load16(b.aadvecs, b.aadvec_start[rec],
+                                                      b.aadvec_start[rec + 1], o, n)
+                                        : load_partial(ad + o, n));
       ya = o ? gf_xor(gf_mul(ya, h1), blk) : blk;
     }
     s.ya = from_gf(ya);
@@ -845,11 +981,19 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
     }
   }
   ok = __shfl(ok, 0, L);
-  // Zero the output of a failed record (aead.cc.inc:132-139, 539-547).
+  // Zero the output of a failed record (aead.cc.inc:132-139, 539-547; an
+  // iovec record's chunks, clear_iovec, :310-333).
   if (active && !ok) {
-    for (uint64_t j = q; j * 16 < m.len; j += L) {
-      const uint32_t n = (uint32_t)min<uint64_t>(m.len - j * 16, 16);
-      store_partial(dst + j * 16, make_uint4(0, 0, 0, 0), n);
+    if (b.iovecs) {
+      for (uint64_t c = b.iovec_start[rec]; c < b.iovec_start[rec + 1]; c++) {
+        const IovecDev v = b.iovecs[c];
+        for (uint64_t i = q; i < v.len; i += L) v.out[i] = 0;
+      }
+    } else {
+      for (uint64_t j = q; j * 16 < m.len; j += L) {
+        const uint32_t n = (uint32_t)min<uint64_t>(m.len - j * 16, 16);
+        store_partial(dst + j * 16, make_uint4(0, 0, 0, 0), n);
+      }
     }
     if (q == 0)
       for (uint32_t i = 0; i < m.xlen; i++) batch_extra_out(b, rec)[i] = 0;
@@ -867,7 +1011,7 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
 // 4) -- in the tiled path all 16 waves must finish their units together, and
 // with fixed priorities the SIMD arbiter's age order makes the youngest wave
 // of each SIMD ~1.9x slower than the oldest.
-template <int NR, bool OPEN, bool XT, int L = 16, bool RP = false>
+template <int NR, bool OPEN, bool XT, int L = 16, bool RP = false, bool IOV = false>
 __device__ __forceinline__ void process_records(const RoundKeys &rk, const BatchDesc &b,
                                                 const RecState *__restrict__ st, uint64_t rec,
                                                 bool active, const uint8_t *smem,
@@ -924,7 +1068,21 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   const int iters = wave_max((int)((nb + L - 1) / L));
   // Full aligned 16-byte blocks of this lane's record; the rest (the partial
   // last block, or every block of an unaligned record) take the byte path.
-  const uint64_t nfull = aligned ? m.len / 16 : 0;
+  // (iovec records: their own paths below.)
+  const uint64_t nfull = aligned && !IOV ? m.len / 16 : 0;
+  // iovec records (IOV): chunk cursors of the loads (one iteration ahead)
+  // and of the stores.
+  static_assert(!(IOV && XT), "iovec records carry no extra bytes");
+  IovCur ldc = {0, 0, 0, nullptr, nullptr}, stc = ldc;
+  uint64_t c_end = 0;
+  if constexpr (IOV) {
+    if (live) {
+      const uint64_t cb = b.iovec_start[rec];
+      c_end = b.iovec_start[rec + 1];
+      if (cb < c_end) iov_at(ldc, b, cb, 0);
+      stc = ldc;
+    }
+  }
   // (Left undefined when not loaded: such a block is never stored or hashed
   // from this value, and a zero-fill would be a VALU write that the waitcnt
   // pass orders after the previous store.)
@@ -933,6 +1091,18 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   // valid 16-byte-aligned address whose value is never used).
   auto load_full = [&](uint64_t j) {
     uint4 v;
+    if constexpr (IOV) {
+      v = make_uint4(0, 0, 0, 0);
+      const uint64_t p = j * 16;
+      if (p < m.len) {
+        iov_seek(ldc, b, p, c_end);
+        if (p + 16 <= ldc.ce && p + 16 <= m.len)
+          v = iov_load16(ldc.in + (p - ldc.cs));
+        else  // straddles chunks, or the record's last partial block
+          v = iov_gather(b, ldc, p, (uint32_t)min<uint64_t>(m.len - p, 16), c_end);
+      }
+      return v;
+    }
 #if BSSL_AMD_ABLATE == 3 || BSSL_AMD_ABLATE == 4  // diagnostic: no plaintext loads
     v = make_uint4((uint32_t)j, 1, 2, 3);
 #elif BSSL_AMD_ABLATE == 7
@@ -965,7 +1135,14 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     wc.update<T>(ctr, s3, c0, c1, c2, rk, smem, lc0, lc1);
     wc.rounds12<T>(k0, s3, cur[0], cur[1], cur[2], cur[3], smem, lc0, lc1);
   }
-  auto step = [&](int it, uint4 x) {
+  // BSSL_AMD_GCM_VGHASH = 2 (diagnostic knob): every second iteration takes
+  // its multiply acc * H^16 on the VALU (gf_mul, constant-time) instead of
+  // the 16 LDS lookups -- the LDS is the binding unit (83 % busy, GHASH 19 %
+  // of it), the VALU ~45 %.
+  const Gf128 h16 = gf_load(key->hpow_ct[16]);
+  (void)h16;
+  auto step = [&](int it, uint4 x, auto vg_tag) {
+    constexpr bool VG = decltype(vg_tag)::value;
     if constexpr (RP) {
       switch ((prio_base + it) & 3) {
         case 0: __builtin_amdgcn_s_setprio(0); break;
@@ -979,8 +1156,13 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     uint32_t xs = bswap32(ctrn) ^ rk.w[0][3];
     wc.update<T>(ctrn, xs, c0, c1, c2, rk, smem, lc0, lc1);
     Gh8 h;
-    g8_rotate(h, acc, rs1, rs2, rbs);
-    h.g = make_uint4(0, 0, 0, 0);
+    if constexpr (VG) {
+      h.r0 = h.r1 = h.r2 = h.r3 = 0;
+      h.g = from_gf(gf_mul(to_gf(acc), h16));
+    } else {
+      g8_rotate(h, acc, rs1, rs2, rbs);
+      h.g = make_uint4(0, 0, 0, 0);
+    }
     uint32_t sa[4] = {cur[0], cur[1], cur[2], cur[3]};
 #if BSSL_AMD_ABLATE == 2 || BSSL_AMD_ABLATE == 5  // diagnostic: no AES rounds 3..NR
     wc.rounds12<T>(k0, xs, cur[0], cur[1], cur[2], cur[3], smem, lc0, lc1);
@@ -998,7 +1180,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
 #if BSSL_AMD_GCM_STAMPS
     const uint64_t st0 = stamp();
 #endif
-    rounds_s1<0, NR>(sa, rk, lc0, lc1, h, P, xs, wc, k0, cur);
+    rounds_s1<0, NR, VG>(sa, rk, lc0, lc1, h, P, xs, wc, k0, cur);
     asm_last_s1(sa, rk.w[NR], lc0);
 #if BSSL_AMD_GCM_STAMPS
     g_stamp_rounds += stamp() - st0;
@@ -1007,6 +1189,21 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
 #endif
     const uint4 ks = make_uint4(sa[0], sa[1], sa[2], sa[3]);
     uint4 y = xor4(x, ks);
+    if constexpr (IOV) {
+      if (j < nb) {
+        const uint64_t p = j * 16;
+        const uint32_t n = (uint32_t)min<uint64_t>(m.len - p, 16);
+        iov_seek(stc, b, p, c_end);
+        if (n == 16 && p + 16 <= stc.ce) {
+          iov_store16(stc.out + (p - stc.cs), y);
+        } else {
+          y = mask_block(y, n);
+          iov_scatter(b, stc, p, y, n, c_end);
+        }
+        acc = xor4(h.g, OPEN ? x : y);
+      }
+      return;
+    }
 #if BSSL_AMD_ABLATE == 4 || BSSL_AMD_ABLATE == 6  // diagnostic: no stores
     if (j < nfull) {
       asm volatile("" ::"v"(y.x), "v"(y.y), "v"(y.z), "v"(y.w));
@@ -1056,14 +1253,14 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   int it = 0;
   for (; it + 2 < iters; it += 3) {
     const uint4 x2 = load_full((uint64_t)(it + 2) * L + q);
-    step(it, x0);
+    step(it, x0, std::integral_constant<bool, false>());
     x0 = load_full((uint64_t)(it + 3) * L + q);
-    step(it + 1, x1);
+    step(it + 1, x1, std::integral_constant<bool, false>());
     x1 = load_full((uint64_t)(it + 4) * L + q);
-    step(it + 2, x2);
+    step(it + 2, x2, std::integral_constant<bool, false>());
   }
-  if (it < iters) step(it, x0);
-  if (it + 1 < iters) step(it + 1, x1);
+  if (it < iters) step(it, x0, std::integral_constant<bool, false>());
+  if (it + 1 < iters) step(it + 1, x1, std::integral_constant<bool, false>());
 #else
   int sync_limit = 0;
 #if BSSL_AMD_GCM_TILE_SYNC
@@ -1091,11 +1288,11 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     if (RP && it > 0 && it + 1 < sync_limit && it % BSSL_AMD_GCM_TILE_SYNC == 0) __syncthreads();
 #endif
     const uint4 x1 = load_full((uint64_t)(it + 1) * L + q);
-    step(it, x0);
+    step(it, x0, std::integral_constant<bool, false>());
     x0 = load_full((uint64_t)(it + 2) * L + q);
-    step(it + 1, x1);
+    step(it + 1, x1, std::integral_constant<bool, (BSSL_AMD_GCM_VGHASH == 2)>());
   }
-  if (it < iters) step(it, x0);
+  if (it < iters) step(it, x0, std::integral_constant<bool, false>());
 #endif
 #if BSSL_AMD_GCM_STAMPS
   g_stamp_loop += stamp() - sl0;
@@ -1128,7 +1325,7 @@ __device__ __forceinline__ void build_g8(uint8_t *smem, const uint4 *__restrict_
 // Declared for 1024 threads whatever W is, so every variant is compiled
 // into 128 VGPRs (an 8-wave workgroup then leaves half of each SIMD's
 // register file free).
-template <int NR, bool OPEN, bool XT, int W>
+template <int NR, bool OPEN, bool XT, int W, bool IOV = false>
 __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__ keys,
                                                     BatchDesc b,
                                                     const RecState *__restrict__ st,
@@ -1185,8 +1382,8 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
       if (first >= n) break;
       const uint64_t i = first + g;
       const bool active = i < n;
-      process_records<NR, OPEN, XT>(rk, b, st, active ? rec_at(b, i) : 0, active, smem, keys, lc0,
-                                    lc1, stamps);
+      process_records<NR, OPEN, XT, 16, false, IOV>(rk, b, st, active ? rec_at(b, i) : 0, active,
+                                                    smem, keys, lc0, lc1, stamps);
     }
 #if BSSL_AMD_GCM_STAMPS
     if (blockIdx.x < 2 && (tid & 63) == 0)
@@ -1520,7 +1717,7 @@ int g_num_cus = 0;
 // waves check their units' records themselves).
 int gcm_mode(const BatchDesc &b) {
   const char *e = getenv("BSSL_AMD_GCM_MODE");
-  if (!e || strcmp(e, "bs16") || b.extra_len || b.key_index) return 0;
+  if (!e || strcmp(e, "bs16") || b.extra_len || b.key_index || b.iovecs) return 0;
   return 1;
 }
 
@@ -1574,7 +1771,10 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
   } else {
     const uint64_t tiles = (b.num_records + kWaves * kRecPerWave - 1) / (kWaves * kRecPerWave);
     const unsigned grid = (unsigned)(tiles < (uint64_t)g_num_cus ? tiles : (uint64_t)g_num_cus);
-    if (b.extra_len)
+    if (b.iovecs)  // (one key: the ctx API)
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, true>), dim3(grid), dim3(kWaves * 64),
+                         0, s, keys, bo, cst, units);
+    else if (b.extra_len)
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, true, kWaves>), dim3(grid), dim3(kWaves * 64), 0, s,
                          keys, bo, cst, units);
     else

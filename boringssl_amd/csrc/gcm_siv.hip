@@ -33,11 +33,12 @@
 namespace bssl_amd {
 namespace {
 
-// AES tables: T0 alone, replicated once per LDS bank (entry x for lane l at
-// t[x][l & 31], 32 KiB), so every lookup of a wave is bank-conflict free
-// whatever the (secret) index -- the constant-time argument of gcm.hip's
-// tables; T1..T3 are rotations of T0.  (Round 1/2 used
-// four plain 1 KiB tables, whose bank conflicts depend on the data.)
+// AES tables: T0 and T1 = rotl8(T0), each replicated once per LDS bank (entry
+// x of table t for lane l at t[x][t][l & 31], 64 KiB), so every lookup of a
+// wave is bank-conflict free whatever the (secret) index -- the
+// constant-time argument of gcm.hip's tables; T2/T3 are
+// rot16(T0/T1), one rotate per column.  (Rounds 1/2 used four plain 1 KiB
+// tables, whose bank conflicts depend on the data.)
 // BSSL_AMD_SIV_SPLIT = 1: the per-block multiply by H^16 as four independent
 // Shoup chains (gmul4) instead of one 32-step chain.
 #ifndef BSSL_AMD_SIV_SPLIT
@@ -68,10 +69,13 @@ namespace {
 #define BSSL_AMD_SIV_CTRCACHE 0
 #endif
 constexpr int kL = 16;                // lanes per record
-// 384 threads (24 records, 6 waves): two workgroups per CU fit the LDS
-// (2 x 68.5 KiB) and the 168-VGPR budget (3 waves per SIMD).
-constexpr int kThreads = 384;
-constexpr int kRecs = kThreads / kL;  // records per workgroup
+// One persistent 768-thread workgroup per CU (12 waves: the 168-VGPR budget's
+// 3 waves per SIMD; LDS 64 KiB of tables + 48 record slots = 137 KiB).  Each
+// wave takes 4-record units from a grid-wide counter and keeps 4 record slots
+// of its own, so waves never wait for each other (a per-workgroup barrier at
+// every record start held 48 records in lock-step).
+constexpr int kThreads = 768;
+constexpr int kRecs = kThreads / kL;  // record slots per workgroup
 constexpr int kPows = 5;              // H, H^2, H^4, H^8, H^16
 
 struct Tables {
@@ -113,18 +117,21 @@ constexpr Tables make_tables() {
 __constant__ Tables kSivTables = make_tables();
 
 struct Lds {
-  uint32_t t[256][32];         // T0, replica (lane & 31)
+  uint32_t t[256][2][32];      // T0 / T1, replica (lane & 31)
   uint4 rk[kRecs][15];         // each record's encryption round keys
   uint4 m[kRecs][kPows][16];   // each record's Shoup tables
 };
-static_assert(2 * sizeof(Lds) <= 160 * 1024, "two workgroups per CU");
+static_assert(sizeof(Lds) <= 160 * 1024, "LDS per workgroup");
 
 __device__ __forceinline__ uint32_t rotl(uint32_t v, int n) {
   return __builtin_amdgcn_alignbit(v, v, 32 - n);
 }
 
 __device__ __forceinline__ uint32_t t0(const Lds &L, uint32_t x) {
-  return L.t[x][threadIdx.x & 31];
+  return L.t[x][0][threadIdx.x & 31];
+}
+__device__ __forceinline__ uint32_t t1(const Lds &L, uint32_t x) {
+  return L.t[x][1][threadIdx.x & 31];
 }
 __device__ __forceinline__ uint32_t sbox(const Lds &L, uint32_t x) {
   return (t0(L, x) >> 8) & 0xff;
@@ -132,7 +139,7 @@ __device__ __forceinline__ uint32_t sbox(const Lds &L, uint32_t x) {
 
 // Table T_t[x] (T_t = rotl(T0, 8t)).
 __device__ __forceinline__ uint32_t tt(const Lds &L, int t, uint32_t x) {
-  return t ? rotl(t0(L, x), 8 * t) : t0(L, x);
+  return t == 0 ? t0(L, x) : t == 1 ? t1(L, x) : rotl(t == 2 ? t0(L, x) : t1(L, x), 16);
 }
 
 // FIPS-197 cipher on little-endian column words, from round R0 on (s = the
@@ -143,10 +150,10 @@ __device__ __forceinline__ uint4 aes_enc_from(uint32_t s0, uint32_t s1, uint32_t
 #pragma unroll
   for (int r = R0; r < NR; r++) {
     const uint4 k = rk[r];
-    // T0[a] ^ T1[b] ^ T2[c] ^ T3[d] = T0[a] ^ rotl8(T0[b] ^ rotl8(T0[c] ^ rotl8(T0[d])))
+    // T0[a] ^ T1[b] ^ T2[c] ^ T3[d] = T0[a] ^ T1[b] ^ rot16(T0[c] ^ T1[d])
     auto col = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t kk) {
-      const uint32_t x = rotl(t0(L, (c >> 16) & 0xff) ^ rotl(t0(L, d >> 24), 8), 8);
-      return t0(L, a & 0xff) ^ rotl(t0(L, (b >> 8) & 0xff) ^ x, 8) ^ kk;
+      return t0(L, a & 0xff) ^ t1(L, (b >> 8) & 0xff) ^
+             rotl(t0(L, (c >> 16) & 0xff) ^ t1(L, d >> 24), 16) ^ kk;
     };
     const uint32_t t0v = col(s0, s1, s2, s3, k.x), t1 = col(s1, s2, s3, s0, k.y),
                    t2 = col(s2, s3, s0, s1, k.z), t3 = col(s3, s0, s1, s2, k.w);
@@ -410,16 +417,23 @@ __device__ __forceinline__ T siv_meta(const T *arr, uint64_t i, bool active) {
   return *p;
 }
 
+// One record (16 lanes, the record's slot `slot` of the workgroup's LDS):
+// everything a record needs happens inside its wave, so the only
+// synchronisation is wave-local (siv_wave_sync).
+__device__ __forceinline__ void siv_wave_sync() {
+  // LDS writes of some lanes read back by other lanes of the same wave: LDS
+  // executes a wave's instructions in order; this keeps the compiler from
+  // reordering across the hand-off.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int NR, bool OPEN>
-__global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyDev *__restrict__ keys,
-                                                           BatchDesc b) {
-  __shared__ Lds L;
-  for (int e = threadIdx.x; e < 256 * 32; e += kThreads) (&L.t[0][0])[e] = kSivTables.te0[e >> 5];
-  __syncthreads();
-  const RecLanes R = rec_lanes();
+__device__ __forceinline__ void siv_record(const GcmKeyDev *__restrict__ keys, const BatchDesc &b,
+                                           Lds &L, const RecLanes &R, uint64_t rec) {
   const int q = R.q;
   const int slot = R.slot;
-  const uint64_t rec = (uint64_t)blockIdx.x * kRecs + slot;
   const bool active = rec < b.num_records;
   uint64_t off = 0, len = 0, ad_off = 0, ad_len = 0;
   uint32_t kidx = 0;
@@ -526,7 +540,7 @@ __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyD
     if (q & 2) e = xor4(e, b2);
     if (q & 1) e = xor4(e, b1);
     L.m[slot][p][q] = e;
-    __syncthreads();
+    siv_wave_sync();
     if (p + 1 < kPows) hp = gmul(hp, L.m[slot][p]);
   }
   const uint4 *rk = L.rk[slot];
@@ -641,6 +655,29 @@ __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyD
   if (active && !ok)
     for (uint64_t p = q; 16 * p < len; p += kL)
       store_block(dst + 16 * p, make_uint4(0, 0, 0, 0), len - 16 * p);
+  siv_wave_sync();  // the slot's round keys / tables are free for the next record
+}
+
+template <int NR, bool OPEN>
+__global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyDev *__restrict__ keys,
+                                                           BatchDesc b,
+                                                           uint32_t *__restrict__ units) {
+  __shared__ Lds L;
+  for (int e = threadIdx.x; e < 256 * 64; e += kThreads) {
+    const uint32_t v = kSivTables.te0[e >> 6];
+    (&L.t[0][0][0])[e] = ((e >> 5) & 1) ? rotl(v, 8) : v;
+  }
+  __syncthreads();
+  const RecLanes R = rec_lanes();
+  const int lane = threadIdx.x & 63;
+  const int local = R.slot & 3;  // the wave's record slots are 4w .. 4w + 3
+  for (;;) {
+    uint32_t u = 0;
+    if (lane == 0) u = atomicAdd(units, 1u);
+    u = __builtin_amdgcn_readfirstlane(__shfl(u, 0, 64));
+    if ((uint64_t)u * 4 >= b.num_records) break;
+    siv_record<NR, OPEN>(keys, b, L, R, (uint64_t)u * 4 + local);
+  }
 }
 
 }  // namespace
@@ -649,26 +686,40 @@ int launch_gcm_siv(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr,
                    const KernelEvents *ev) {
   if (b.num_records == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const uint64_t blocks = (b.num_records + kRecs - 1) / kRecs;
-  if (blocks > 0x7fffffffu) return 1;
+  static int num_cus = 0;
+  if (!num_cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 1;
+  }
+  uint32_t *units = nullptr;  // the grid-wide unit counter
+  if (hipMallocAsync(reinterpret_cast<void **>(&units), 64, s) != hipSuccess) return 2;
+  if (hipMemsetAsync(units, 0, 64, s) != hipSuccess) {
+    hipFreeAsync(units, s);
+    return 2;
+  }
+  const uint64_t wanted = (b.num_records + kRecs - 1) / kRecs;
+  const unsigned grid = (unsigned)(wanted < (uint64_t)num_cus ? wanted : (uint64_t)num_cus);
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
   if (nr == 14) {
     if (open)
-      hipLaunchKernelGGL((gcm_siv_kernel<14, true>), dim3((unsigned)blocks), dim3(kThreads), 0,
-                         s, keys, b);
+      hipLaunchKernelGGL((gcm_siv_kernel<14, true>), dim3(grid), dim3(kThreads), 0, s, keys, b,
+                         units);
     else
-      hipLaunchKernelGGL((gcm_siv_kernel<14, false>), dim3((unsigned)blocks), dim3(kThreads), 0,
-                         s, keys, b);
+      hipLaunchKernelGGL((gcm_siv_kernel<14, false>), dim3(grid), dim3(kThreads), 0, s, keys, b,
+                         units);
   } else {
     if (open)
-      hipLaunchKernelGGL((gcm_siv_kernel<10, true>), dim3((unsigned)blocks), dim3(kThreads), 0,
-                         s, keys, b);
+      hipLaunchKernelGGL((gcm_siv_kernel<10, true>), dim3(grid), dim3(kThreads), 0, s, keys, b,
+                         units);
     else
-      hipLaunchKernelGGL((gcm_siv_kernel<10, false>), dim3((unsigned)blocks), dim3(kThreads), 0,
-                         s, keys, b);
+      hipLaunchKernelGGL((gcm_siv_kernel<10, false>), dim3(grid), dim3(kThreads), 0, s, keys, b,
+                         units);
   }
   const int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
+  hipFreeAsync(units, s);
   return rc;
 }
 

@@ -55,6 +55,18 @@ enum AeadKind : int {
   kAeadAesGcmSiv = 3
 };
 
+// Device chunk descriptors of iovec records: CRYPTO_IOVEC / CRYPTO_IVEC
+// (reference include/openssl/aead.h:400-414) on the device.
+struct IovecDev {
+  uint8_t *out;
+  const uint8_t *in;
+  uint64_t len;
+};
+struct IvecDev {
+  const uint8_t *in;
+  uint64_t len;
+};
+
 // Record-batch descriptor (device pointers), see BSSL_AMD_BATCH.
 struct BatchDesc {
   const uint8_t *in;
@@ -95,6 +107,15 @@ struct BatchDesc {
   uint32_t extra_stride;
   uint32_t extra_out_stride;
   uint32_t tag_stride;
+  // iovec records walked in place by the AES-GCM kernels (iovec.hip,
+  // EVP_AEAD_CTX_sealv_batch_device): when `iovecs` is set, record i's message
+  // is the concatenation of iovecs[iovec_start[i] .. iovec_start[i+1]) and its
+  // AD that of aadvecs[aadvec_start[i] ..] (or none); `lengths` / `ad_lengths`
+  // hold the totals and in / out / offsets / ad are unused.  Null otherwise.
+  const IovecDev *iovecs;
+  const uint64_t *iovec_start;
+  const IvecDev *aadvecs;
+  const uint64_t *aadvec_start;
 };
 
 // Tag / extra addresses of record i.
@@ -161,17 +182,7 @@ struct TlsPrepare {
   uint8_t *nonces, *prefix, *ad, *extra, *valid;
 };
 int launch_tls_prepare(const TlsPrepare &p, void *stream);
-// Batches of non-contiguous records (iovec.hip): CRYPTO_IOVEC / CRYPTO_IVEC
-// layouts (reference include/openssl/aead.h:400-414) on the device.
-struct IovecDev {
-  uint8_t *out;
-  const uint8_t *in;
-  uint64_t len;
-};
-struct IvecDev {
-  const uint8_t *in;
-  uint64_t len;
-};
+// Batches of non-contiguous records (iovec.hip).
 struct IovBatchDesc {
   uint64_t num_records;
   const IovecDev *iovecs;
@@ -187,6 +198,9 @@ struct IovBatchDesc {
 // whose tag_len / key fields the runner fills in).  Returns 0 or an error.
 struct IovRunner {
   virtual int operator()(BatchDesc &d) const = 0;
+  // Whether the AEAD's kernels walk the chunks in place (BatchDesc::iovecs,
+  // AES-GCM); otherwise the records are gathered into staging and scattered.
+  virtual bool in_place() const { return false; }
 };
 // Gather -> run -> scatter; synchronises `stream` once (staging size).
 int iov_batch_run(const IovBatchDesc &b, const IovRunner &run, void *stream);

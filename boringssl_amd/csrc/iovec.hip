@@ -5,20 +5,25 @@
 // aead.cc.inc:316-361, 531-584) take one record as an array of CRYPTO_IOVEC
 // {out, in, len} chunks and its AD as an array of CRYPTO_IVEC {in, len}
 // (include/openssl/aead.h:400-414); the AEADs walk the chunks with
-// bssl::iovec::ForEachBlockRange (crypto/cipher/internal.h), i.e. the record
-// is the concatenation of its chunks.  Here a batch of such records is
+// bssl::iovec::ForEachBlockRange (crypto/cipher/internal.h:283-411), i.e. the
+// record is the concatenation of its chunks.
+//
+// AES-GCM (round 3): the bulk kernels walk the chunks in place
+// (BatchDesc::iovecs, gcm.hip IOV): each lane keeps a cursor on the chunk of
+// its current block and loads / stores 16-byte blocks at any alignment;
+// only the per-record totals are computed here (iov_lengths), with no
+// staging, copies or stream synchronisation.
+//
+// ChaCha20-Poly1305, XChaCha20-Poly1305 and AES-GCM-SIV: the chunks are
 // gathered into one contiguous device staging area (records 16-byte aligned,
 // so the bulk kernels take their aligned fast path), sealed or opened in place
 // by the same bulk kernels as any batch, and scattered back to the chunks'
 // `out` pointers.  A failed record is zero-filled in the staging area by the
 // bulk kernel, so the scatter zeroes its chunks (clear_iovec,
-// aead.cc.inc:310-314, 325-333).
-//
-// Copies: one wave per record walks its chunks in order; each chunk is copied
-// in 16-byte destination words, assembled with v_alignbyte from aligned dword
-// loads when the source is not 4-byte aligned (chunks have arbitrary lengths,
-// so a record's later chunks start at arbitrary alignments), with a byte loop
-// for the head and tail.
+// aead.cc.inc:310-314, 325-333).  Copies: one wave per record walks its
+// chunks in order; each chunk is copied in 16-byte destination words,
+// assembled with v_alignbyte from aligned dword loads when the source is not
+// 4-byte aligned, with a byte loop for the head and tail.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -107,12 +112,41 @@ __global__ __launch_bounds__(kCopyThreads) void iov_copy(const IovBatchDesc b,
   }
 }
 
+// In-place form (AES-GCM): only the per-record totals are computed; the bulk
+// kernels read and write the chunks themselves (BatchDesc::iovecs).  No
+// staging, no copies, no synchronisation.
+int iov_batch_run_in_place(const IovBatchDesc &b, const IovRunner &run, hipStream_t s) {
+  const uint64_t n = b.num_records;
+  uint64_t *meta = nullptr;  // len, padded, ad_len, ad_padded (n each)
+  if (hipMallocAsync(reinterpret_cast<void **>(&meta), 4 * n * 8 + 64, s) != hipSuccess) return 2;
+  uint64_t *len = meta, *padded = meta + n, *ad_len = meta + 2 * n, *ad_padded = meta + 3 * n;
+  hipLaunchKernelGGL(iov_lengths, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b, len,
+                     padded, ad_len, ad_padded);
+  BatchDesc d = {};
+  d.lengths = len;
+  d.ad_lengths = ad_len;
+  d.nonces = b.nonces;
+  d.nonce_len = b.nonce_len;
+  d.tags = b.tags;
+  d.status = b.status;
+  d.num_records = n;
+  d.iovecs = b.iovecs;
+  d.iovec_start = b.iovec_start;
+  d.aadvecs = b.aadvecs;
+  d.aadvec_start = b.aadvec_start;
+  int rc = run(d);
+  hipFreeAsync(meta, s);
+  if (!rc && hipGetLastError() != hipSuccess) rc = 1;
+  return rc;
+}
+
 }  // namespace
 
 int iov_batch_run(const IovBatchDesc &b, const IovRunner &run, void *stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const uint64_t n = b.num_records;
   if (n == 0) return 0;
+  if (run.in_place()) return iov_batch_run_in_place(b, run, s);
   size_t temp = 0;
   if (hipcub::DeviceScan::ExclusiveSum(nullptr, temp, (const uint64_t *)nullptr,
                                        (uint64_t *)nullptr, n + 1, s) != hipSuccess)

@@ -844,6 +844,85 @@ def test_iovec_batch_vs_oracle(aead):
             assert st[i] == 1 and got == pts[i], i
 
 
+@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm"])
+@pytest.mark.parametrize("n", [300, 4500])
+def test_iovec_in_place_walk(aead, n):
+    """The AES-GCM kernels walk iovec chunks in place (BatchDesc::iovecs):
+    chunks of 0..4097 bytes incl. empty and 1-byte chunks, input and output
+    at independent alignments 0..15 (so the loads and the stores shift by
+    different amounts), blocks straddling several chunks, records up to
+    32 KiB, and >= 4096 records (length-ordered schedule); seal vs the
+    oracle, then open with a corrupted tag zeroing that record's chunks."""
+    rng = random.Random(n * 31 + len(aead))
+    key = bytes(rng.getrandbits(8) for _ in range(AEAD_KEYLEN[aead]))
+    lens = [rng.choice([0, 1, 15, 16, 17, 31, 255, 1350, 4096, 16384, 16397, 32768])
+            for _ in range(n)]
+    pts = [rng.randbytes(L) for L in lens]
+    ads = [rng.randbytes(rng.choice([0, 5, 13, 29])) for _ in range(n)]
+    nonces = [rng.randbytes(12) for _ in range(n)]
+    chunks, starts = [], [0]  # (in_off, out_off, bytes)
+    ipos, opos = 0, 0
+    for i in range(n):
+        data, k = pts[i], 0
+        while k < len(data) or (k == 0 and rng.random() < 0.5):
+            size = rng.choice([0, 1, 2, 3, 15, 16, 17, 64, 255, 1000, 4097, 1 << 20])
+            part = data[k:k + size]
+            ipos += rng.randint(0, 15)
+            opos += rng.randint(0, 15)
+            chunks.append((ipos, opos, part))
+            ipos += len(part)
+            opos += len(part)
+            k += len(part)
+            if size == 0 and k >= len(data):
+                break
+        starts.append(len(chunks))
+    src = np.zeros(ipos + 32, dtype=np.uint8)
+    for io, _, part in chunks:
+        src[io:io + len(part)] = np.frombuffer(part, dtype=np.uint8)
+    adbuf, ad_offs = _pack(ads, 1)
+    d_src, d_ad = _t(src), _t(adbuf)
+    d_dst = torch.zeros(opos + 32, dtype=torch.uint8, device=DEV)
+    sb, db, ab = d_src.data_ptr(), d_dst.data_ptr(), d_ad.data_ptr()
+    iov = np.array([(db + oo, sb + io, len(p)) for io, oo, p in chunks], dtype=np.int64)
+    aiv = np.array([(ab + int(ad_offs[i]), len(ads[i])) for i in range(n)], dtype=np.int64)
+    d_starts = _t(np.array(starts, np.int64))
+    d_astarts = _t(np.arange(n + 1, dtype=np.int64))
+    d_nonce = _t(np.frombuffer(b"".join(nonces), dtype=np.uint8).copy())
+    d_tags = torch.zeros(16 * n, dtype=torch.uint8, device=DEV)
+    d_st = torch.full((n,), 7, dtype=torch.uint8, device=DEV)
+    ctx = ba.AEADCtx(aead, key, 16)
+    b = ba.make_iov_batch(n, _t(iov.reshape(-1, 3)), d_starts, d_tags, d_nonce, 12,
+                          aadvecs=_t(aiv.reshape(-1, 2)), aadvec_start=d_astarts, status=d_st)
+    ctx.sealv_batch_device(b)
+    torch.cuda.synchronize()
+    assert d_st.cpu().tolist() == [1] * n
+    out, tags = d_dst.cpu().numpy(), d_tags.cpu().numpy()
+    cts = []
+    for i in range(n):
+        ok, ct, tag = o.seal(ORACLE_ID[aead], key, nonces[i], pts[i], ads[i])
+        got = b"".join(out[oo:oo + len(p)].tobytes() for _, oo, p in chunks[starts[i]:starts[i + 1]])
+        assert ok and got == ct and tags[16 * i:16 * i + 16].tobytes() == tag, (i, lens[i])
+        cts.append(ct)
+    # Open in place (out == in on the ciphertext arena), one corrupted tag.
+    bad = {3, n // 2}
+    tg = tags.copy()
+    for i in bad:
+        tg[16 * i + 5] ^= 0x10
+    iov2 = np.array([(db + oo, db + oo, len(p)) for _, oo, p in chunks], dtype=np.int64)
+    d_st.fill_(7)
+    b2 = ba.make_iov_batch(n, _t(iov2.reshape(-1, 3)), d_starts, _t(tg), d_nonce, 12,
+                           aadvecs=_t(aiv.reshape(-1, 2)), aadvec_start=d_astarts, status=d_st)
+    ctx.openv_detached_batch_device(b2)
+    torch.cuda.synchronize()
+    st, back = d_st.cpu().numpy(), d_dst.cpu().numpy()
+    for i in range(n):
+        got = b"".join(back[oo:oo + len(p)].tobytes() for _, oo, p in chunks[starts[i]:starts[i + 1]])
+        if i in bad:
+            assert st[i] == 0 and got == bytes(lens[i]), i
+        else:
+            assert st[i] == 1 and got == pts[i], i
+
+
 @pytest.mark.multigpu
 def test_context_used_from_another_device():
     """A context created on GPU 0 and used after the thread switched to GPU 1:

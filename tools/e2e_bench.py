@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    aead, key_len, _, length, _ = bench.CONFIGS[args.config]
+    aead, key_len, _, length, _, _ = bench.CONFIGS[args.config]
     assert length != "mixed"
     n, c = args.records, args.chunk
     stride = (length + 15) // 16 * 16
