@@ -632,25 +632,36 @@ __device__ __forceinline__ uint4 crypt_partial_x(const uint8_t *src, uint8_t *ds
   return y;
 }
 
+// 16-byte block loads and stores at any address.  The HSA runtime runs the
+// shader memory in unaligned mode (SH_MEM_CONFIG.alignment_mode), so
+// global_load/store_dwordx4 take byte addresses; the 1-byte-aligned type lets
+// the compiler emit them for records that are not 16-byte aligned (the same
+// instruction an aligned block uses; an unaligned one costs its extra cache
+// line in the TA, nothing on the VALU).
+typedef uint32_t u32_any __attribute__((aligned(1)));
+
 __device__ __forceinline__ uint4 load_blk_nt(const uint8_t *p) {
+  const u32_any *ip = reinterpret_cast<const u32_any *>(p);
 #if BSSL_AMD_GCM_NT_LOAD
-  const uint4 *ip = reinterpret_cast<const uint4 *>(p);
-  return make_uint4(__builtin_nontemporal_load(&ip->x), __builtin_nontemporal_load(&ip->y),
-                    __builtin_nontemporal_load(&ip->z), __builtin_nontemporal_load(&ip->w));
+  return make_uint4(__builtin_nontemporal_load(ip), __builtin_nontemporal_load(ip + 1),
+                    __builtin_nontemporal_load(ip + 2), __builtin_nontemporal_load(ip + 3));
 #else
-  return *reinterpret_cast<const uint4 *>(p);
+  return make_uint4(ip[0], ip[1], ip[2], ip[3]);
 #endif
 }
 
 __device__ __forceinline__ void store_blk_nt(uint8_t *p, uint4 y) {
+  u32_any *o = reinterpret_cast<u32_any *>(p);
 #if BSSL_AMD_GCM_NT_STORE
-  uint4 *o = reinterpret_cast<uint4 *>(p);
-  __builtin_nontemporal_store(y.x, &o->x);
-  __builtin_nontemporal_store(y.y, &o->y);
-  __builtin_nontemporal_store(y.z, &o->z);
-  __builtin_nontemporal_store(y.w, &o->w);
+  __builtin_nontemporal_store(y.x, o);
+  __builtin_nontemporal_store(y.y, o + 1);
+  __builtin_nontemporal_store(y.z, o + 2);
+  __builtin_nontemporal_store(y.w, o + 3);
 #else
-  *reinterpret_cast<uint4 *>(p) = y;
+  o[0] = y.x;
+  o[1] = y.y;
+  o[2] = y.z;
+  o[3] = y.w;
 #endif
 }
 
@@ -687,59 +698,56 @@ __device__ __forceinline__ void iov_seek(IovCur &k, const BatchDesc &b, uint64_t
   while (p >= k.ce && k.c + 1 < c_end) iov_at(k, b, k.c + 1, k.ce);
 }
 
-// 16 bytes at any address: one aligned 16-byte load, or two and a byte shift
-// (both loads stay inside the 16-byte granules that hold the wanted bytes).
-__device__ __forceinline__ uint4 iov_load16(const uint8_t *src) {
-  const uint32_t a = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
-  if (a == 0) return load_blk_nt(src);
-  const uint4 A = load_blk_nt(src - a), B = load_blk_nt(src - a + 16);
-  const uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+// Bytes [a, a + 16) of the 32 bytes A || B (a = 0..16).
+__device__ __forceinline__ uint4 bytes_at(uint4 A, uint4 B, uint32_t a) {
+  const uint32_t w[9] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, 0u};
   const uint32_t wq = a >> 2, r = a & 3;
   uint32_t t[5];
 #pragma unroll
   for (int i = 0; i < 5; i++)
-    t[i] = wq == 0 ? w[i] : wq == 1 ? w[i + 1] : wq == 2 ? w[i + 2] : w[i + 3];
+    t[i] = wq == 0 ? w[i] : wq == 1 ? w[i + 1] : wq == 2 ? w[i + 2] : wq == 3 ? w[i + 3] : w[i + 4];
   return make_uint4(__builtin_amdgcn_alignbyte(t[1], t[0], r),
                     __builtin_amdgcn_alignbyte(t[2], t[1], r),
                     __builtin_amdgcn_alignbyte(t[3], t[2], r),
                     __builtin_amdgcn_alignbyte(t[4], t[3], r));
 }
 
-// 16 bytes to any address: one aligned 16-byte store; else dword stores
-// where dst is 4-byte aligned, or head bytes, 3 aligned dwords and tail
-// bytes (a neighbour lane's block shares the head / tail dwords, written
-// with byte-masked stores).
-__device__ __forceinline__ void iov_store16(uint8_t *dst, uint4 y) {
-  const uint32_t a = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15);
-  if (a == 0) {
-    store_blk_nt(dst, y);
-    return;
+// Bytes [p, p + n) (n <= 16, zero past n) of a block that ends in chunk k.c
+// or the next chunk (the usual straddle: at most one boundary): one partial
+// load per piece, joined by a byte shift.  Returns false (nothing loaded)
+// when more chunks are involved.
+__device__ __forceinline__ bool iov_load2(const BatchDesc &b, const IovCur &k, uint64_t p,
+                                          uint32_t n, uint64_t c_end, uint4 &v) {
+  const uint32_t n1 = (uint32_t)min<uint64_t>(n, k.ce - p);
+  uint4 v2 = make_uint4(0, 0, 0, 0);
+  if (n1 < n) {
+    if (k.c + 1 >= c_end) return false;
+    const IovecDev nx = b.iovecs[k.c + 1];
+    if (nx.len < n - n1) return false;
+    v2 = load_partial(nx.in, n - n1);
   }
-  const uint32_t w[4] = {y.x, y.y, y.z, y.w};
-  const uint32_t r = a & 3;
-  if (r == 0) {
-    uint32_t *p = reinterpret_cast<uint32_t *>(dst);
-    p[0] = w[0];
-    p[1] = w[1];
-    p[2] = w[2];
-    p[3] = w[3];
-    return;
+  const uint4 v1 = load_partial(k.in + (p - k.cs), n1);
+  const uint4 s2 = bytes_at(make_uint4(0, 0, 0, 0), v2, 16 - n1);  // v2 << 8 n1
+  v = make_uint4(v1.x | s2.x, v1.y | s2.y, v1.z | s2.z, v1.w | s2.w);
+  return true;
+}
+
+__device__ __forceinline__ bool iov_store2(const BatchDesc &b, const IovCur &k, uint64_t p,
+                                           uint4 y, uint32_t n, uint64_t c_end) {
+  const uint32_t n1 = (uint32_t)min<uint64_t>(n, k.ce - p);
+  IovecDev nx = {nullptr, nullptr, 0};
+  if (n1 < n) {
+    if (k.c + 1 >= c_end) return false;
+    nx = b.iovecs[k.c + 1];
+    if (nx.len < n - n1) return false;
   }
-  const uint32_t h = 4 - r;  // head bytes before the first aligned dword
-  if (h & 1) dst[0] = (uint8_t)w[0];
-  if (h & 2) *reinterpret_cast<uint16_t *>(dst + (h & 1)) = (uint16_t)(w[0] >> (8 * (h & 1)));
-  uint32_t *pm = reinterpret_cast<uint32_t *>(dst + h);
-  pm[0] = __builtin_amdgcn_alignbyte(w[1], w[0], h);
-  pm[1] = __builtin_amdgcn_alignbyte(w[2], w[1], h);
-  pm[2] = __builtin_amdgcn_alignbyte(w[3], w[2], h);
-  uint8_t *t = dst + h + 12;  // r tail bytes: bytes h + 12 .. 15
-  const uint32_t tw = w[3] >> (8 * h);
-  if (r & 2) *reinterpret_cast<uint16_t *>(t) = (uint16_t)tw;
-  if (r & 1) t[r & 2] = (uint8_t)(tw >> (8 * (r & 2)));
+  store_partial(k.out + (p - k.cs), y, n1);
+  if (n1 < n) store_partial(nx.out, bytes_at(y, make_uint4(0, 0, 0, 0), n1), n - n1);
+  return true;
 }
 
 // Bytes [p, p + n) of the record's stream (n <= 16, zero past n), byte by
-// byte across chunk boundaries (blocks that straddle chunks, the last block).
+// byte across chunk boundaries (blocks over three or more chunks).
 __device__ __forceinline__ uint4 iov_gather(const BatchDesc &b, IovCur k, uint64_t p, uint32_t n,
                                             uint64_t c_end) {
   uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
@@ -1043,8 +1051,6 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   const uint32_t c0 = s.j0.x ^ rk.w[0][0], c1 = s.j0.y ^ rk.w[0][1], c2 = s.j0.z ^ rk.w[0][2];
   const uint8_t *src = b.in + m.off;
   uint8_t *dst = b.out + m.off;
-  const bool aligned = ((reinterpret_cast<uintptr_t>(src) |
-                         reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
   uint4 acc = (q == L - 1 && live) ? s.ya : make_uint4(0, 0, 0, 0);
   // GHASH lane constants (Gh8): rotation by q bytes and the slot offsets.
   const bool rs1 = (q >> 2) & 1, rs2 = (q >> 3) & 1;  // (rotation by q mod 16)
@@ -1066,15 +1072,22 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
                       rotl(tload<T>(smem, taddr<2>(lc0, c2)) ^ rk.w[1][0], 16);
   WindowCache wc;
   const int iters = wave_max((int)((nb + L - 1) / L));
-  // Full aligned 16-byte blocks of this lane's record; the rest (the partial
-  // last block, or every block of an unaligned record) take the byte path.
+  // Full 16-byte blocks of this lane's record, at any alignment (one
+  // dwordx4 each, load_blk_nt); the partial last block takes the byte path.
   // (iovec records: their own paths below.)
-  const uint64_t nfull = aligned && !IOV ? m.len / 16 : 0;
+  const uint64_t nfull = !IOV ? m.len / 16 : 0;
   // iovec records (IOV): chunk cursors of the loads (one iteration ahead)
   // and of the stores.
   static_assert(!(IOV && XT), "iovec records carry no extra bytes");
   IovCur ldc = {0, 0, 0, nullptr, nullptr}, stc = ldc;
   uint64_t c_end = 0;
+  // Runs: a lane's next block is 16·L bytes further on; while it stays inside
+  // the cursor's chunk (`*_left` >= 16) the block is one dwordx4 at `*_ptr`,
+  // with no cursor arithmetic.  Anything else (a chunk boundary, the record's
+  // last block, the first block) takes the cursor path, which re-anchors.
+  const uint8_t *ld_ptr = nullptr;
+  uint8_t *st_ptr = nullptr;
+  int64_t ld_left = -1, st_left = -1;
   if constexpr (IOV) {
     if (live) {
       const uint64_t cb = b.iovec_start[rec];
@@ -1092,15 +1105,24 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   auto load_full = [&](uint64_t j) {
     uint4 v;
     if constexpr (IOV) {
-      v = make_uint4(0, 0, 0, 0);
-      const uint64_t p = j * 16;
-      if (p < m.len) {
-        iov_seek(ldc, b, p, c_end);
-        if (p + 16 <= ldc.ce && p + 16 <= m.len)
-          v = iov_load16(ldc.in + (p - ldc.cs));
-        else  // straddles chunks, or the record's last partial block
-          v = iov_gather(b, ldc, p, (uint32_t)min<uint64_t>(m.len - p, 16), c_end);
+      if (ld_left >= 16) {
+        v = load_blk_nt(ld_ptr);
+      } else {
+        v = make_uint4(0, 0, 0, 0);
+        const uint64_t p = j * 16;
+        if (p < m.len) {
+          iov_seek(ldc, b, p, c_end);
+          const uint32_t n = (uint32_t)min<uint64_t>(m.len - p, 16);
+          if (n == 16 && p + 16 <= ldc.ce)
+            v = load_blk_nt(ldc.in + (p - ldc.cs));
+          else if (!iov_load2(b, ldc, p, n, c_end, v))  // a straddle, the last block
+            v = iov_gather(b, ldc, p, n, c_end);        // (three or more chunks)
+          ld_ptr = ldc.in + (p - ldc.cs);
+          ld_left = (int64_t)(ldc.ce - p);
+        }
       }
+      ld_ptr += 16 * L;
+      ld_left -= 16 * L;
       return v;
     }
 #if BSSL_AMD_ABLATE == 3 || BSSL_AMD_ABLATE == 4  // diagnostic: no plaintext loads
@@ -1190,18 +1212,24 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     const uint4 ks = make_uint4(sa[0], sa[1], sa[2], sa[3]);
     uint4 y = xor4(x, ks);
     if constexpr (IOV) {
-      if (j < nb) {
+      if (st_left >= 16) {
+        store_blk_nt(st_ptr, y);
+      } else if (j < nb) {
         const uint64_t p = j * 16;
         const uint32_t n = (uint32_t)min<uint64_t>(m.len - p, 16);
         iov_seek(stc, b, p, c_end);
         if (n == 16 && p + 16 <= stc.ce) {
-          iov_store16(stc.out + (p - stc.cs), y);
+          store_blk_nt(stc.out + (p - stc.cs), y);
         } else {
           y = mask_block(y, n);
-          iov_scatter(b, stc, p, y, n, c_end);
+          if (!iov_store2(b, stc, p, y, n, c_end)) iov_scatter(b, stc, p, y, n, c_end);
         }
-        acc = xor4(h.g, OPEN ? x : y);
+        st_ptr = stc.out + (p - stc.cs);
+        st_left = (int64_t)(stc.ce - p);
       }
+      st_ptr += 16 * L;
+      st_left -= 16 * L;
+      if (j < nb) acc = xor4(h.g, OPEN ? x : y);
       return;
     }
 #if BSSL_AMD_ABLATE == 4 || BSSL_AMD_ABLATE == 6  // diagnostic: no stores
@@ -1209,17 +1237,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
       asm volatile("" ::"v"(y.x), "v"(y.y), "v"(y.z), "v"(y.w));
 #else
     if (j < nfull) {
-#if BSSL_AMD_GCM_NT_STORE  // non-temporal ciphertext stores
-      {
-        uint4 *o = reinterpret_cast<uint4 *>(dst + j * 16);
-        __builtin_nontemporal_store(y.x, &o->x);
-        __builtin_nontemporal_store(y.y, &o->y);
-        __builtin_nontemporal_store(y.z, &o->z);
-        __builtin_nontemporal_store(y.w, &o->w);
-      }
-#else
-      *reinterpret_cast<uint4 *>(dst + j * 16) = y;
-#endif
+      store_blk_nt(dst + j * 16, y);
 #endif
     } else if (j < nb) {
       const uint32_t n = (uint32_t)min<uint64_t>(m.len + m.xlen - j * 16, 16);
@@ -1367,7 +1385,7 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
     // grid-wide counter, so waves that the SIMD arbiter favours (older
     // waves issue first) simply process more units instead of waiting at a
     // per-tile barrier for the slowest wave.
-    build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab[4]), tid);
+    build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab16), tid);
     __syncthreads();
     RoundKeys rk;
 #pragma unroll
@@ -1435,7 +1453,7 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
         __syncthreads();
         // Byte table of H^16 from the key's nibble tables (power 4): entry
         // (e, p) = T[2p][e >> 4] ^ T[2p+1][e & 15] (key_setup.cc layout).
-        build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[k].htab[4]), tid);
+        build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[k].htab16), tid);
         __syncthreads();
         loaded = k;
       }
@@ -1677,7 +1695,7 @@ __global__ __launch_bounds__(1024) void gcm_bs16_kernel(const GcmKeyDev *__restr
     const uint32_t v = kTables.te0[idx];
     reinterpret_cast<uint32_t *>(smem + kLdsAes)[e] = slot ? rotl(v, 8) : v;
   }
-  build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab[4]), tid);
+  build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab16), tid);
   __syncthreads();
   const uint32_t *rkp = &keys[0].rk_plain[0][0];
   const uint64_t n = b.num_records;

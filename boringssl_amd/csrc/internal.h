@@ -2,10 +2,10 @@
 //
 // Device data layout (all resident in HBM, 16-byte aligned):
 //
-//   GcmKeyDev   one per AES-GCM key (49,920 bytes): the AES round keys (T-table
-//               and plain forms), the GHASH multiplication tables for
-//               H, H^2, H^4, H^8, H^16, H^32 and the powers H^1..H^16 as
-//               multipliers of the constant-time VALU product (gf128_ct.h).
+//   GcmKeyDev   one per AES-GCM key (8,960 bytes): the AES round keys (T-table
+//               and plain forms), the GHASH nibble table of H^16 and the powers
+//               H^1..H^16 as multipliers of the constant-time VALU product
+//               (gf128_ct.h).
 //               Equivalent of the reference's GCM128_KEY
 //               (crypto/fipsmodule/aes/internal.h:325-334), re-laid-out for the
 //               LDS-table GHASH of gcm.hip.
@@ -18,10 +18,6 @@
 #include <stdint.h>
 
 namespace bssl_amd {
-
-// GHASH table powers held per key: kGhashPow[i] = H^(2^i).
-constexpr int kGhashPowers = 6;           // H, H^2, H^4, H^8, H^16, H^32
-constexpr int kGhashTableWords = 32 * 16 * 4;  // 32 nibble positions x 16 values x 16 B
 
 struct alignas(16) GcmKeyDev {
   // Round keys as little-endian words of the FIPS-197 schedule bytes; the
@@ -37,12 +33,14 @@ struct alignas(16) GcmKeyDev {
   // prepared as multipliers (gf_prep): the constant-time VALU products of the
   // record-end combine, the tag and the prologue's AD / J0 hashes.
   uint32_t hpow_ct[17][4];
-  // htab[p][pos][v] = (element with nibble `pos` equal to v) * H^(2^p), as 4
+  // htab16[pos][v] = (element with nibble `pos` equal to v) * H^16, as 4
   // little-endian words of the 16 GCM-order bytes.  Nibble position
   // pos = 2*k + 0 is the high nibble of byte k, 2*k + 1 the low nibble.
-  uint32_t htab[kGhashPowers][32][16][4];
+  // (Rounds 1-2 also held H, H^2, H^4, H^8, H^32 for the record-end tree,
+  // which is now the constant-time VALU product.)
+  uint32_t htab16[32][16][4];
 };
-static_assert(sizeof(GcmKeyDev) == 240 + 16 + 240 + 17 * 16 + kGhashPowers * 8192, "layout");
+static_assert(sizeof(GcmKeyDev) == 240 + 16 + 240 + 17 * 16 + 8192, "layout");
 
 struct alignas(16) ChaChaKeyDev {
   uint32_t k[8];

@@ -21,9 +21,9 @@
 // `out` pointers.  A failed record is zero-filled in the staging area by the
 // bulk kernel, so the scatter zeroes its chunks (clear_iovec,
 // aead.cc.inc:310-314, 325-333).  Copies: one wave per record walks its
-// chunks in order; each chunk is copied in 16-byte destination words,
-// assembled with v_alignbyte from aligned dword loads when the source is not
-// 4-byte aligned, with a byte loop for the head and tail.
+// chunks in order; each chunk is copied in aligned 16-byte destination words
+// loaded by one dwordx4 at any source alignment, with a byte loop for the
+// head and tail.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -42,25 +42,12 @@ __device__ __forceinline__ void copy_bytes(uint8_t *dst, const uint8_t *src, uin
   if (lane < head) dst[lane] = src[lane];
   const uint64_t words = (n - head) / 16;
   uint4 *d = reinterpret_cast<uint4 *>(dst + head);
-  const uint8_t *s = src + head;
-  const uint32_t m = reinterpret_cast<uintptr_t>(s) & 3;
-  if ((reinterpret_cast<uintptr_t>(s) & 15) == 0) {
-    for (uint64_t w = lane; w < words; w += 64) d[w] = reinterpret_cast<const uint4 *>(s)[w];
-  } else if (m == 0) {
-    for (uint64_t w = lane; w < words; w += 64) {
-      const uint32_t *sp = reinterpret_cast<const uint32_t *>(s + 16 * w);
-      d[w] = make_uint4(sp[0], sp[1], sp[2], sp[3]);
-    }
-  } else {
-    // Five aligned dwords cover the 16 source bytes (each holds at least one
-    // of them, so no load leaves the chunk's pages); v_alignbyte shifts.
-    for (uint64_t w = lane; w < words; w += 64) {
-      const uint32_t *sp = reinterpret_cast<const uint32_t *>(s + 16 * w - m);
-      const uint32_t d0 = sp[0], d1 = sp[1], d2 = sp[2], d3 = sp[3], d4 = sp[4];
-      d[w] = make_uint4(__builtin_amdgcn_alignbyte(d1, d0, m), __builtin_amdgcn_alignbyte(d2, d1, m),
-                        __builtin_amdgcn_alignbyte(d3, d2, m), __builtin_amdgcn_alignbyte(d4, d3, m));
-    }
-  }
+  // Source words at any alignment: one dwordx4 each (the shader memory runs
+  // in unaligned mode; the loads stay inside the chunk).
+  typedef uint32_t u32_any __attribute__((aligned(1)));
+  const u32_any *sp = reinterpret_cast<const u32_any *>(src + head);
+  for (uint64_t w = lane; w < words; w += 64)
+    d[w] = make_uint4(sp[4 * w], sp[4 * w + 1], sp[4 * w + 2], sp[4 * w + 3]);
   for (uint64_t i = head + 16 * words + lane; i < n; i += 64) dst[i] = src[i];
 }
 

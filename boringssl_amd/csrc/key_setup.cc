@@ -204,7 +204,10 @@ bool gcm_key_setup(const uint8_t *key, size_t key_len, GcmKeyDev *out) {
     }
     secure_zero(&hk, sizeof(hk));
   }
-  for (int pw = 0; pw < kGhashPowers; pw++) {
+  // The nibble table of H^16 (the bulk kernel expands it into its LDS byte
+  // table, gcm.hip build_g8).
+  for (int sq = 0; sq < 4; sq++) p = gf_mul(p, p);
+  {
     U128 v[128];
     v[0] = p;
     for (int i = 1; i < 128; i++) v[i] = mulx(v[i - 1]);
@@ -220,10 +223,9 @@ bool gcm_key_setup(const uint8_t *key, size_t key_len, GcmKeyDev *out) {
           uint8_t b[16];
           store_u128(acc, b);
           for (int j = 0; j < 4; j++)
-            out->htab[pw][2 * k + half][val][j] = load_le32(b + 4 * j);
+            out->htab16[2 * k + half][val][j] = load_le32(b + 4 * j);
           secure_zero(b, sizeof(b));
         }
-    p = gf_mul(p, p);
     secure_zero(v, sizeof(v));
   }
   // The reference wipes key state on cleanup (OPENSSL_cleanse); so do the

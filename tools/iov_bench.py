@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--records", type=int, default=1 << 18)
     ap.add_argument("--len", type=int, default=16384)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--in-gap", type=int, default=1,
+                    help="bytes between input records (1: record starts at every alignment)")
+    ap.add_argument("--out-gap", type=int, default=1, help="the same for the outputs")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(0)
@@ -38,16 +41,17 @@ def main():
     g = torch.Generator(device=dev).manual_seed(1)
     # chunk layout: record i occupies [base_i, base_i + L + 1) with a 1-byte
     # gap, so record starts (and most chunk starts) are unaligned
-    stride = L + 1
-    src = torch.randint(0, 256, (n * stride + 64,), dtype=torch.uint8, device=dev, generator=g)
-    dst = torch.zeros_like(src)
-    base = torch.arange(n, dtype=torch.int64, device=dev) * stride
+    sin, sout = L + a.in_gap, L + a.out_gap
+    src = torch.randint(0, 256, (n * sin + 64,), dtype=torch.uint8, device=dev, generator=g)
+    dst = torch.zeros(n * sout + 64, dtype=torch.uint8, device=dev)
+    bin_ = torch.arange(n, dtype=torch.int64, device=dev) * sin
+    bout = torch.arange(n, dtype=torch.int64, device=dev) * sout
     cut1 = torch.full((n,), min(5, L), dtype=torch.int64, device=dev)
     cut2 = torch.full((n,), max(min(5, L), L // 2), dtype=torch.int64, device=dev)
     offs = torch.stack([torch.zeros_like(cut1), cut1, cut2], 1)       # chunk start in record
     lens = torch.stack([cut1, cut2 - cut1, L - cut2], 1)              # chunk length
-    iov = torch.stack([dst.data_ptr() + base[:, None] + offs,
-                       src.data_ptr() + base[:, None] + offs, lens], 2).reshape(-1, 3).contiguous()
+    iov = torch.stack([dst.data_ptr() + bout[:, None] + offs,
+                       src.data_ptr() + bin_[:, None] + offs, lens], 2).reshape(-1, 3).contiguous()
     starts = torch.arange(0, 3 * n + 1, 3, dtype=torch.int64, device=dev)
     ad = torch.randint(0, 256, (13 * n,), dtype=torch.uint8, device=dev, generator=g)
     aiv = torch.stack([ad.data_ptr() + 13 * torch.arange(n, dtype=torch.int64, device=dev),
@@ -65,9 +69,14 @@ def main():
     cct = torch.zeros_like(cpt)
     cb = ba.make_batch(n, cpt, cct, tags, nonces, nl, ad, record_stride=(L + 15) // 16 * 16,
                        record_len=L, ad_stride=13, ad_len=13, status=status)
+    # ... and contiguous at the iovec layout's input stride (unaligned records
+    # when in_gap is not a multiple of 16; in place).
+    ub = ba.make_batch(n, src, src, tags, nonces, nl, ad, record_stride=sin, record_len=L,
+                       ad_stride=13, ad_len=13, status=status)
     res = {}
     for name, op, batch in (("iovec", ctx.sealv_batch_device, b),
-                            ("contiguous", ctx.seal_batch_device, cb)):
+                            ("contiguous", ctx.seal_batch_device, cb),
+                            ("contiguous_at_stride", ctx.seal_batch_device, ub)):
         op(batch)
         torch.cuda.synchronize()
         assert bool(status.all()), name
@@ -77,8 +86,8 @@ def main():
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / a.steps
         res[name] = {"ms_per_batch": round(dt * 1e3, 3), "gib_per_s": round(n * L / dt / 2**30, 2)}
-    print(json.dumps({"aead": a.aead, "records": n, "record_bytes": L,
-                      "chunks_per_record": 3, **res}))
+    print(json.dumps({"aead": a.aead, "records": n, "record_bytes": L, "in_gap": a.in_gap,
+                      "out_gap": a.out_gap, "chunks_per_record": 3, **res}))
 
 
 if __name__ == "__main__":

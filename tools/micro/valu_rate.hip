@@ -37,6 +37,8 @@ constexpr int kIters = 256;
 #define I_XAD(i) "v_xad_u32 %" #i ", %" #i ", %8, %9\n"
 #define I_ADD3(i) "v_add3_u32 %" #i ", %" #i ", %8, %9\n"
 #define I_LSHL(i) "v_lshlrev_b32 %" #i ", 7, %" #i "\n"
+#define I_XOR_SDWA(i) "v_xor_b32_sdwa %" #i ", %" #i ", %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0\n"
+#define I_PK_ADD16(i) "v_pk_add_u16 %" #i ", %" #i ", %8 op_sel:[1,1] op_sel_hi:[0,0]\n"
 
 // ChaCha quarter-round-like dependent triples (add, xor, rotate) on ILP
 // independent chains.
@@ -74,6 +76,8 @@ __global__ void rate(uint64_t *out, uint32_t a, uint32_t b) {
     // ChaCha block) vs ILP 8 (two blocks interleaved); order within a step
     // keeps each chain's add -> xor -> rotate dependent.
     if (K == 17) { QBODY4 QBODY4 asm volatile("v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n" : "+v"(r[5]) : "v"(a)); }
+    if (K == 19) { BODY8(I_XOR_SDWA) BODY8(I_XOR_SDWA) BODY8(I_XOR_SDWA) BODY8(I_XOR_SDWA) }
+    if (K == 20) { BODY8(I_PK_ADD16) BODY8(I_PK_ADD16) BODY8(I_PK_ADD16) BODY8(I_PK_ADD16) }
     if (K == 18) { QBODY8 asm volatile("v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n" : "+v"(r[5]) : "v"(a)); }
   }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -87,7 +91,8 @@ int main() {
   const char *names[] = {"v_add_u32", "v_xor_b32", "v_alignbit_b32", "v_bitop3_b32", "v_mul_lo_u32",
                          "v_mul_hi_u32", "v_mad_u64_u32", "v_lshrrev_b64", "v_lshl_add_u64",
                          "v_perm_b32", "v_alignbyte_b32", "v_lshl_or_b32", "v_xad_u32", "v_add3_u32",
-                         "v_lshlrev_b32", "v_xor_b32 ~0", "v_alignbit(0)", "QR ILP4(+8 add)", "QR ILP8(+8 add)"};
+                         "v_lshlrev_b32", "v_xor_b32 ~0", "v_alignbit(0)", "QR ILP4(+8 add)", "QR ILP8(+8 add)",
+                         "v_xor_b32_sdwa", "v_pk_add_u16"};
   uint64_t *d;
   CK(hipMalloc(&d, 1 << 20));
   uint64_t h[4096];
@@ -95,7 +100,7 @@ int main() {
   // same occupancy is reported beside them.
   for (int waves = 1; waves <= 4; waves *= 4) {
     double base = 0;
-    for (int k = 0; k < 19; k++) {
+    for (int k = 0; k < 21; k++) {
       for (int rep = 0; rep < 2; rep++) {
         // one workgroup per CU, `waves` waves per SIMD
         const int threads = 256 * waves;
@@ -119,6 +124,8 @@ int main() {
           case 16: rate<16><<<256, threads>>>(d, 3, 5); break;
           case 17: rate<17><<<256, threads>>>(d, 3, 5); break;
           case 18: rate<18><<<256, threads>>>(d, 3, 5); break;
+          case 19: rate<19><<<256, threads>>>(d, 3, 5); break;
+          case 20: rate<20><<<256, threads>>>(d, 3, 5); break;
         }
         CK(hipDeviceSynchronize());
       }
