@@ -1079,21 +1079,20 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   // iovec records (IOV): chunk cursors of the loads (one iteration ahead)
   // and of the stores.
   static_assert(!(IOV && XT), "iovec records carry no extra bytes");
-  IovCur ldc = {0, 0, 0, nullptr, nullptr}, stc = ldc;
-  uint64_t c_end = 0;
-  // Runs: a lane's next block is 16·L bytes further on; while it stays inside
-  // the cursor's chunk (`*_left` >= 16) the block is one dwordx4 at `*_ptr`,
-  // with no cursor arithmetic.  Anything else (a chunk boundary, the record's
-  // last block, the first block) takes the cursor path, which re-anchors.
+  // Between chunk boundaries a lane carries only its run pointers: the next
+  // block is 16·L bytes further on, and while it stays inside the chunk
+  // (`*_left` >= 16) it is one dwordx4 at `*_ptr`.  Anything else (a chunk
+  // boundary, the record's last block, the first block) takes the cursor
+  // path: the chunk cursor (chunk index and its stream start; the rest is
+  // reloaded from the chunk array) seeks, handles the block and re-anchors the
+  // run.  (The compact state keeps the IOV kernel's hot loop free of spills.)
+  uint64_t ld_c = 0, ld_cs = 0, st_c = 0, st_cs = 0;
   const uint8_t *ld_ptr = nullptr;
   uint8_t *st_ptr = nullptr;
-  int64_t ld_left = -1, st_left = -1;
+  int32_t ld_left = -1, st_left = -1;
   if constexpr (IOV) {
     if (live) {
-      const uint64_t cb = b.iovec_start[rec];
-      c_end = b.iovec_start[rec + 1];
-      if (cb < c_end) iov_at(ldc, b, cb, 0);
-      stc = ldc;
+      ld_c = st_c = b.iovec_start[rec];
     }
   }
   // (Left undefined when not loaded: such a block is never stored or hashed
@@ -1107,22 +1106,27 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     if constexpr (IOV) {
       if (ld_left >= 16) {
         v = load_blk_nt(ld_ptr);
+        ld_ptr += 16 * L;
+        ld_left -= 16 * L;
       } else {
         v = make_uint4(0, 0, 0, 0);
         const uint64_t p = j * 16;
         if (p < m.len) {
-          iov_seek(ldc, b, p, c_end);
+          const uint64_t c_end = b.iovec_start[rec + 1];
+          IovCur k;
+          iov_at(k, b, ld_c, ld_cs);
+          iov_seek(k, b, p, c_end);
           const uint32_t n = (uint32_t)min<uint64_t>(m.len - p, 16);
-          if (n == 16 && p + 16 <= ldc.ce)
-            v = load_blk_nt(ldc.in + (p - ldc.cs));
-          else if (!iov_load2(b, ldc, p, n, c_end, v))  // a straddle, the last block
-            v = iov_gather(b, ldc, p, n, c_end);        // (three or more chunks)
-          ld_ptr = ldc.in + (p - ldc.cs);
-          ld_left = (int64_t)(ldc.ce - p);
+          if (n == 16 && p + 16 <= k.ce)
+            v = load_blk_nt(k.in + (p - k.cs));
+          else if (!iov_load2(b, k, p, n, c_end, v))  // a straddle, the last block
+            v = iov_gather(b, k, p, n, c_end);        // (three or more chunks)
+          ld_c = k.c;
+          ld_cs = k.cs;
+          ld_ptr = k.in + (p - k.cs) + 16 * L;
+          ld_left = (int32_t)min<uint64_t>(k.ce - p, 1u << 30) - 16 * L;
         }
       }
-      ld_ptr += 16 * L;
-      ld_left -= 16 * L;
       return v;
     }
 #if BSSL_AMD_ABLATE == 3 || BSSL_AMD_ABLATE == 4  // diagnostic: no plaintext loads
@@ -1214,21 +1218,26 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     if constexpr (IOV) {
       if (st_left >= 16) {
         store_blk_nt(st_ptr, y);
+        st_ptr += 16 * L;
+        st_left -= 16 * L;
       } else if (j < nb) {
         const uint64_t p = j * 16;
         const uint32_t n = (uint32_t)min<uint64_t>(m.len - p, 16);
-        iov_seek(stc, b, p, c_end);
-        if (n == 16 && p + 16 <= stc.ce) {
-          store_blk_nt(stc.out + (p - stc.cs), y);
+        const uint64_t c_end = b.iovec_start[rec + 1];
+        IovCur k;
+        iov_at(k, b, st_c, st_cs);
+        iov_seek(k, b, p, c_end);
+        if (n == 16 && p + 16 <= k.ce) {
+          store_blk_nt(k.out + (p - k.cs), y);
         } else {
           y = mask_block(y, n);
-          if (!iov_store2(b, stc, p, y, n, c_end)) iov_scatter(b, stc, p, y, n, c_end);
+          if (!iov_store2(b, k, p, y, n, c_end)) iov_scatter(b, k, p, y, n, c_end);
         }
-        st_ptr = stc.out + (p - stc.cs);
-        st_left = (int64_t)(stc.ce - p);
+        st_c = k.c;
+        st_cs = k.cs;
+        st_ptr = k.out + (p - k.cs) + 16 * L;
+        st_left = (int32_t)min<uint64_t>(k.ce - p, 1u << 30) - 16 * L;
       }
-      st_ptr += 16 * L;
-      st_left -= 16 * L;
       if (j < nb) acc = xor4(h.g, OPEN ? x : y);
       return;
     }
