@@ -362,6 +362,16 @@ Scratch *scratch(size_t bytes) {
 
 size_t round16(size_t n) { return (n + 15) & ~size_t(15); }
 
+// Largest record the single-record path seals in mapped host memory
+// (BSSL_AMD_ONE_RECORD_MAP_MAX overrides; 0 = always copy).
+size_t one_record_map_max() {
+  static const size_t v = [] {
+    const char *e = getenv("BSSL_AMD_ONE_RECORD_MAP_MAX");
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)65536;
+  }();
+  return v;
+}
+
 // Seal or open one record held in host memory.  `in`/`out` may be equal.
 // For open, `tag` is read; for seal it is written (tag_len bytes).
 // Staging layout (device and pinned host alike): nonce | AD | tag, status
@@ -384,12 +394,17 @@ int one_record(const EVP_AEAD_CTX *ctx, bool open, const uint8_t *in, uint8_t *o
     return 0;
   }
   hipStream_t s = sc->stream;
-  uint8_t *d = sc->dev, *h = sc->host;
+  // Records up to kMapMax bytes are read and written by the kernels directly
+  // in the pinned host buffer (mapped into the GPU's address space): no DMA
+  // copies, whose two launches and completions were most of a short record's
+  // latency.  Longer records take one H2D and one D2H copy.
+  const bool mapped = len <= one_record_map_max();
+  uint8_t *h = sc->host, *d = mapped ? sc->host : sc->dev;
   if (nonce_len) memcpy(h + o_nonce, nonce, nonce_len);
   if (ad_len) memcpy(h + o_ad, ad, ad_len);
   if (open && tag_len) memcpy(h + o_tag, tag, tag_len);
   if (len) memcpy(h + o_in, in, len);
-  if (hipMemcpyAsync(d, h, o_in + len, hipMemcpyHostToDevice, s) != hipSuccess) {
+  if (!mapped && hipMemcpyAsync(d, h, o_in + len, hipMemcpyHostToDevice, s) != hipSuccess) {
     PUT_ERROR(ERR_R_INTERNAL_ERROR);
     return 0;
   }
@@ -406,8 +421,8 @@ int one_record(const EVP_AEAD_CTX *ctx, bool open, const uint8_t *in, uint8_t *o
   b.tags = d + o_tag;
   b.status = d + o_status;
   if (!run_batch(st->km, tag_len, &b, open, false, s)) return 0;
-  bool ok = hipMemcpyAsync(h + o_tag, d + o_tag, o_in - o_tag + len, hipMemcpyDeviceToHost, s) ==
-            hipSuccess;
+  bool ok = mapped || hipMemcpyAsync(h + o_tag, d + o_tag, o_in - o_tag + len,
+                                     hipMemcpyDeviceToHost, s) == hipSuccess;
   ok &= hipStreamSynchronize(s) == hipSuccess;
   if (!ok) {
     PUT_ERROR(ERR_R_INTERNAL_ERROR);
@@ -1026,7 +1041,7 @@ int EVP_AEAD_CTX_open_batch_device(const EVP_AEAD_CTX *ctx, const BSSL_AMD_BATCH
 
 namespace {
 
-// The bulk kernels of `km` over the gathered records of an iovec batch.
+// The bulk kernels of `km` over an iovec batch (they walk the chunks in place).
 struct KeyRunner : IovRunner {
   const KeyMaterial *km;
   size_t tag_len;
@@ -1041,8 +1056,6 @@ struct KeyRunner : IovRunner {
     d.valid = valid;
     return launch_desc(km, d, open, stream);
   }
-  // AES-GCM walks the chunks inside its kernels (gcm.hip, IOV).
-  bool in_place() const override { return km->aead->kind == kAeadAesGcm; }
 };
 
 bool check_iov_batch(const EVP_AEAD *aead, const BSSL_AMD_IOV_BATCH *b) {

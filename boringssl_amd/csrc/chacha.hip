@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include "internal.h"
+#include "iov_dev.h"
 
 namespace bssl_amd {
 namespace {
@@ -62,8 +63,29 @@ struct ChaState {
   uint32_t x[16];
 };
 
+// d = rotl(d ^ a, 16) as two SDWA XORs (one per 16-bit half, the halves
+// swapped) instead of an XOR and a v_alignbit_b32 (diagnostic knob; the
+// alignbit is one of the slow-issue VALU instructions).
+#ifndef BSSL_AMD_CHACHA_SDWA
+#define BSSL_AMD_CHACHA_SDWA 0
+#endif
+__device__ __forceinline__ uint32_t xor_rot16(uint32_t d, uint32_t a) {
+#if BSSL_AMD_CHACHA_SDWA
+  uint32_t t;
+  asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 "
+      "src1_sel:WORD_0\n\t"
+      "v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 "
+      "src1_sel:WORD_1"
+      : "=&v"(t)
+      : "v"(d), "v"(a));
+  return t;
+#else
+  return rotl(d ^ a, 16);
+#endif
+}
+
 #define QR(a, b, c, d)                 \
-  a += b; d = rotl(d ^ a, 16);         \
+  a += b; d = xor_rot16(d, a);         \
   c += d; b = rotl(b ^ c, 12);         \
   a += b; d = rotl(d ^ a, 8);          \
   c += d; b = rotl(b ^ c, 7);
@@ -461,7 +483,8 @@ __device__ __forceinline__ T meta_load(const T *arr, uint64_t i, bool active) {
 }
 
 // One wave group: records pos = grp * (64 / L) + lane / L.
-template <bool OPEN, int L, bool XT, bool XC>
+// IOV: iovec records walked in place (BatchDesc::iovecs; no extra bytes).
+template <bool OPEN, int L, bool XT, bool XC, bool IOV>
 __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ keys,
                                              const BatchDesc &b, uint64_t grp) {
 #if BSSL_AMD_CHACHA_STAMPS
@@ -470,6 +493,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   CSTAMP(0);
   if (BSSL_AMD_CHACHA_PRIO) __builtin_amdgcn_s_setprio(BSSL_AMD_CHACHA_PRIO);
   static_assert(L == 2 || L == 4 || L == 8 || L == 16, "lanes per record");
+  static_assert(!(IOV && XT), "iovec records carry no extra bytes");
   constexpr int kLog = L == 2 ? 1 : L == 4 ? 2 : L == 8 ? 3 : 4;
   const int lane = threadIdx.x & 63;
   const int q = lane & (L - 1);
@@ -553,11 +577,21 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   // The lane's first AD block (block q), loaded now so its latency hides
   // under the first ChaCha block instead of stalling the Poly1305 setup.
   uint32_t adw[4] = {0, 0, 0, 0};
+  // AD block k of an iovec record: bytes of its CRYPTO_IVEC chunks.
+  auto ivec_block = [&](uint64_t k, uint32_t w[4]) {
+    const uint4 v = ivec_load16(b.aadvecs, b.aadvec_start[rec], b.aadvec_start[rec + 1], 16 * k,
+                                (uint32_t)min<uint64_t>(m.ad_len - 16 * k, 16));
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+  };
   {
     const uint8_t *ad = b.ad + (live ? m.ad_off : 0);
     const uint64_t k = (uint64_t)q;
-    if (live && 16 * k < m.ad_len)
-      load16_partial(ad + 16 * k, (uint32_t)min<uint64_t>(m.ad_len - 16 * k, 16), adw);
+    if (live && 16 * k < m.ad_len) {
+      if constexpr (IOV)
+        ivec_block(k, adw);
+      else
+        load16_partial(ad + 16 * k, (uint32_t)min<uint64_t>(m.ad_len - 16 * k, 16), adw);
+    }
   }
   // Message = the record's `in` bytes then b.extra_len extra bytes
   // (BatchDesc::extra, the TLS 1.3 inner type), whose ciphertext goes to
@@ -572,8 +606,8 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   const uint32_t tail_blocks = (uint32_t)(npoly & 3);
   const uint8_t *src = b.in + m.off;
   uint8_t *dst = b.out + m.off;
-  const bool aligned = ((reinterpret_cast<uintptr_t>(src) |
-                         reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+  const bool aligned = !IOV && ((reinterpret_cast<uintptr_t>(src) |
+                                 reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
   // Slot u of the record (lane u mod L, iteration u / L) holds the Poly1305
   // key block for u = 0 and data block d = u - 1 - sh for u >= 1 + sh (ChaCha
   // counter d + 1).  sh = 1 leaves slot 1 idle so that, for a record on a
@@ -581,7 +615,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   // 4 it - 1 - sh ..) covers whole 128-byte lines instead of half lines at
   // both ends (the other half written one iteration later); the Poly1305
   // element order then starts with a zero element (Y_A at v = sh).
-  constexpr bool kCoalSh = BSSL_AMD_CHACHA_COAL && BSSL_AMD_CHACHA_SHIFT && L == 4;
+  constexpr bool kCoalSh = BSSL_AMD_CHACHA_COAL && BSSL_AMD_CHACHA_SHIFT && L == 4 && !IOV;
   // (Wave-uniform: 1 only if every live record of the wave is 128-byte
   // aligned, so the slot arithmetic stays scalar.)
   const uint64_t live_mask = __ballot(live);
@@ -595,7 +629,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   // chunk j at + 16 ((j + q + r) mod 4) -- conflict-free both for the 16
   // chunks of a record and for the 4 chunks a lane reads of its own block).
   __shared__ uint4 s_c0[kThreads][4];
-  constexpr bool kCoal = BSSL_AMD_CHACHA_COAL && L == 4;
+  constexpr bool kCoal = BSSL_AMD_CHACHA_COAL && L == 4 && !IOV;
   // Per record slot: byte offset and the number of full 64-byte blocks the
   // coalesced path moves (0 unless the record is live and 16-byte aligned).
   __shared__ uint4 s_rinfo[kThreads / L];
@@ -612,8 +646,63 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   // the ciphertext words (masked past the end) in c[].
   // Input of data block d = u-1 when it is a full aligned 64-byte block
   // (issued before the ChaCha rounds so the HBM latency hides under them).
+  // iovec records (IOV): each lane walks the chunks with a cursor for its
+  // loads and one for its stores (chunk index and the chunk's stream start,
+  // as gcm.hip).  Between chunk boundaries only a running pointer moves: the
+  // lane's next block is 64 L bytes further on, and while it lies inside the
+  // chunk (`*_left` >= 64) it is four dwordx4 at any alignment.  A block
+  // across chunks or the record's last block goes through 16-byte pieces
+  // (iov_load2 / iov_store2, the byte walk over three or more chunks).
+  uint64_t ld_c = 0, ld_cs = 0, st_c = 0, st_cs = 0;
+  const uint8_t *ld_ptr = nullptr;
+  uint8_t *st_ptr = nullptr;
+  int64_t ld_left = -1, st_left = -1;
+  bool pre_ok = false;  // pre[] holds the lane's whole current block
+  if constexpr (IOV) {
+    if (live) ld_c = st_c = b.iovec_start[rec];
+  }
   auto prefetch = [&](uint64_t u, uint4 pre[4]) {
     const uint64_t d = u - 1 - sh;
+    if constexpr (IOV) {
+      // The lane's whole 64-byte block, when it lies in one chunk, goes to
+      // the wave's staging area by LDS-DMA (four 16-byte pieces at any
+      // alignment, piece i of lane l at + 1024 i + 16 l: no VGPRs held across
+      // the rounds); anything else takes crypt_block's piece path.
+      pre_ok = false;
+      if (u >= 1 && d < nblk && m.len >= 64 * d + 64) {
+        const uint8_t *gp = nullptr;
+        if (ld_left >= 64) {
+          gp = ld_ptr;
+          ld_ptr += 64 * L;
+          ld_left -= 64 * L;
+        } else {
+          const uint64_t p = 64 * d;
+          IovCur k;
+          iov_at(k, b, ld_c, ld_cs);
+          iov_seek(k, b, p, b.iovec_start[rec + 1]);
+          ld_c = k.c;
+          ld_cs = k.cs;
+          if (p + 64 <= k.ce) {
+            gp = k.in + (p - k.cs);
+            ld_ptr = gp + 64 * L;
+            ld_left = (int64_t)(k.ce - p) - 64 * L;
+          } else {
+            ld_left = -1;
+          }
+        }
+        if (gp) {
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            __builtin_amdgcn_global_load_lds(
+                reinterpret_cast<const void *>(gp + 16 * i),
+                reinterpret_cast<__attribute__((address_space(3))) void *>(
+                    reinterpret_cast<uintptr_t>(stage + 1024 * i)),
+                16, 0, 0);
+          pre_ok = true;
+        }
+      }
+      return;
+    }
     if (u >= 1 + sh && d < nblk && aligned && m.len >= 64 * d + 64) {
 #if BSSL_AMD_CHACHA_ABLATE == 1
       if (u >= (uint64_t)L) {
@@ -632,7 +721,102 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     const uint64_t d = u - 1 - sh;
     const uint64_t rem = vlen - 64 * d;
     uint32_t x[16], y[16];
-    if (kCoal && staged && m.len >= 64 * d + 64 && aligned) {
+    if constexpr (IOV) {
+      const uint64_t p = 64 * d;
+      const uint32_t n = (uint32_t)min<uint64_t>(rem, 64);
+      const uint64_t c_end = b.iovec_start[rec + 1];
+      uint8_t *my = stage + 16 * lane;  // piece i at + 1024 i
+      if (pre_ok) {
+        // Whole block from the LDS-DMA staging (the caller waited for it).
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const uint4 v = *reinterpret_cast<const uint4 *>(my + 1024 * i);
+          x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) y[i] = x[i] ^ ks[i];
+        if (st_left >= 64) {
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            store16_any(st_ptr + 16 * i,
+                        make_uint4(y[4 * i], y[4 * i + 1], y[4 * i + 2], y[4 * i + 3]));
+          st_ptr += 64 * L;
+          st_left -= 64 * L;
+        } else {
+          IovCur k;
+          iov_at(k, b, st_c, st_cs);
+          iov_seek(k, b, p, c_end);
+          st_c = k.c;
+          st_cs = k.cs;
+          // (The output chunks have the input chunks' lengths, so a block
+          // the loads found in one chunk lies in one output chunk too.)
+          if (p + 64 <= k.ce) {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+              store16_any(k.out + (p - k.cs) + 16 * i,
+                          make_uint4(y[4 * i], y[4 * i + 1], y[4 * i + 2], y[4 * i + 3]));
+            st_ptr = k.out + (p - k.cs) + 64 * L;
+            st_left = (int64_t)(k.ce - p) - 64 * L;
+          } else {  // (not reached: see above)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+              const uint64_t pi = p + 16 * i;
+              iov_seek(k, b, pi, c_end);
+              const uint4 v = make_uint4(y[4 * i], y[4 * i + 1], y[4 * i + 2], y[4 * i + 3]);
+              if (!iov_store2(b, k, pi, v, 16, c_end)) iov_scatter(b, k, pi, v, 16, c_end);
+            }
+            st_c = k.c;
+            st_cs = k.cs;
+            st_left = -1;
+          }
+        }
+      } else {
+        // A block across chunks or the record's last block: 16-byte pieces;
+        // the keystream waits in the staging slot and each piece's
+        // ciphertext (seal: output, open: input) replaces it there.
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          *reinterpret_cast<uint4 *>(my + 1024 * i) =
+              make_uint4(ks[4 * i], ks[4 * i + 1], ks[4 * i + 2], ks[4 * i + 3]);
+        IovCur k;
+        iov_at(k, b, ld_c, ld_cs);
+        IovCur ko;
+        iov_at(ko, b, st_c, st_cs);
+#pragma unroll 1
+        for (int i = 0; i < 4; i++) {
+          const uint32_t ni = n > 16u * i ? min(n - 16u * i, 16u) : 0u;
+          uint4 v = make_uint4(0, 0, 0, 0), w = make_uint4(0, 0, 0, 0);
+          if (ni) {
+            const uint64_t pi = p + 16 * i;
+            iov_seek(k, b, pi, c_end);
+            if (ni == 16 && pi + 16 <= k.ce)
+              v = load16_any(k.in + (pi - k.cs));
+            else if (!iov_load2(b, k, pi, ni, c_end, v))
+              v = iov_gather(b, k, pi, ni, c_end);
+            const uint4 kw = *reinterpret_cast<const uint4 *>(my + 1024 * i);
+            w = mask_block(make_uint4(v.x ^ kw.x, v.y ^ kw.y, v.z ^ kw.z, v.w ^ kw.w), ni);
+            iov_seek(ko, b, pi, c_end);
+            if (ni == 16 && pi + 16 <= ko.ce)
+              store16_any(ko.out + (pi - ko.cs), w);
+            else if (!iov_store2(b, ko, pi, w, ni, c_end))
+              iov_scatter(b, ko, pi, w, ni, c_end);
+          }
+          *reinterpret_cast<uint4 *>(my + 1024 * i) = OPEN ? v : w;
+        }
+        ld_c = k.c;
+        ld_cs = k.cs;
+        ld_left = -1;
+        st_c = ko.c;
+        st_cs = ko.cs;
+        st_left = -1;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const uint4 v = *reinterpret_cast<const uint4 *>(my + 1024 * i);
+          x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
+          y[4 * i] = v.x; y[4 * i + 1] = v.y; y[4 * i + 2] = v.z; y[4 * i + 3] = v.w;
+        }
+      }
+    } else if (kCoal && staged && m.len >= 64 * d + 64 && aligned) {
       // Full block, coalesced I/O: input from the staging area, output back
       // to it (stored after the iteration by record-contiguous stores).
       uint8_t *my = stage + rslot * 256 + q * 64;
@@ -710,6 +894,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   prefetch((uint64_t)q, pre);
   chacha_block(key, (uint32_t)q >= 1 + sh ? (uint32_t)q - sh : 0u, nonce, ks);
   const bool have0 = (uint32_t)q >= 1 + sh && (uint64_t)q - sh <= nblk;
+  if constexpr (IOV) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (LDS-DMA, prefetch)
   if (have0) crypt_block((uint64_t)q, ks, pre, c0, false);
   CSTAMP(1);
   if (BSSL_AMD_CHACHA_PRIO) __builtin_amdgcn_s_setprio(0);
@@ -787,6 +972,11 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     const uint64_t nab = live ? (m.ad_len + 15) / 16 : 0;
     const int wmax = wave_max((int)min<uint64_t>(nab, 0x7fffffff));
     auto ad_block = [&](uint64_t k) {
+      if constexpr (IOV) {
+        uint32_t w[4];
+        ivec_block(k, w);
+        return pblock(w[0], w[1], w[2], w[3]);
+      }
       const uint8_t *p = ad + 16 * k;
       const uint64_t avail = m.ad_len - 16 * k;
       return pblock(load_le32_bytes(p, avail), load_le32_bytes(p + 4, avail > 4 ? avail - 4 : 0),
@@ -903,7 +1093,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
 #else
     chacha_block_raw(kl, (uint32_t)(u - sh), nonce, ks);
 #endif
-    if constexpr (kCoal) {
+    if constexpr (kCoal || IOV) {
       // vmcnt(0): the LDS-DMA loads have landed.  The keystream words are
       // inputs so the rounds stay ahead of the wait (hipcc otherwise sinks
       // them below it and the load latency is exposed).
@@ -1006,7 +1196,13 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     }
   }
   ok = __shfl(ok, 0, L);
-  if (active && !ok) {
+  if (active && !ok && IOV) {
+    // clear_iovec (aead.cc.inc:310-333): the record's chunks.
+    for (uint64_t c = b.iovec_start[rec]; c < b.iovec_start[rec + 1]; c++) {
+      const IovecDev v = b.iovecs[c];
+      for (uint64_t i = q; i < v.len; i += L) v.out[i] = 0;
+    }
+  } else if (active && !ok) {
     for (uint64_t j = q; j * 16 < m.len; j += L) {
       const uint64_t n = min<uint64_t>(m.len - j * 16, 16);
       for (uint64_t i = 0; i < n; i++) dst[j * 16 + i] = 0;
@@ -1026,17 +1222,17 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
 }
 
 // One wave group per wave.
-template <bool OPEN, int L, bool XT, bool XC>
+template <bool OPEN, int L, bool XT, bool XC, bool IOV>
 __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
     const ChaChaKeyDev *__restrict__ keys, BatchDesc b) {
-  chacha_group<OPEN, L, XT, XC>(keys, b,
+  chacha_group<OPEN, L, XT, XC, IOV>(keys, b,
                                 (uint64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6));
 }
 
-template <bool OPEN, bool XT, bool XC>
+template <bool OPEN, bool XT, bool XC, bool IOV = false>
 void launch_one(const ChaChaKeyDev *keys, const BatchDesc &b, uint64_t blocks, hipStream_t s) {
   constexpr int L = BSSL_AMD_CHACHA_L;
-  hipLaunchKernelGGL((chacha_poly_kernel<OPEN, L, XT, XC>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((chacha_poly_kernel<OPEN, L, XT, XC, IOV>), dim3((unsigned)blocks),
                      dim3(kThreads), 0, s, keys, b);
 }
 
@@ -1064,7 +1260,14 @@ int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, bool 
   }
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
   const bool xt = b.extra_len != 0;
-  if (xchacha) {
+  if (b.iovecs) {  // iovec records walked in place (never with extra bytes)
+    if (xchacha)
+      open ? launch_one<true, false, true, true>(keys, bo, blocks, s)
+           : launch_one<false, false, true, true>(keys, bo, blocks, s);
+    else
+      open ? launch_one<true, false, false, true>(keys, bo, blocks, s)
+           : launch_one<false, false, false, true>(keys, bo, blocks, s);
+  } else if (xchacha) {
     if (open)
       xt ? launch_one<true, true, true>(keys, bo, blocks, s)
          : launch_one<true, false, true>(keys, bo, blocks, s);

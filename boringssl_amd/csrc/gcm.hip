@@ -35,6 +35,7 @@
 #include <type_traits>
 
 #include "internal.h"
+#include "iov_dev.h"
 #include "bs16_aes.h"
 #include "gf128_ct.h"
 
@@ -481,70 +482,6 @@ __device__ __forceinline__ uint4 shfl_down4(uint4 v, int d, int width) {
                     __shfl_down(v.z, d, width), __shfl_down(v.w, d, width));
 }
 
-// ---------------------------------------------------------------------------
-// Record buffers.
-// Bytes [p, p + n) (n <= 16), zero past n, with aligned dword loads: only
-// dwords holding at least one of the bytes are read (they lie in the same
-// pages as those bytes), then funnel-shifted.  (Byte loads cost one memory
-// request per byte.)
-__device__ __forceinline__ uint4 load_partial(const uint8_t *p, uint32_t n) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t *base = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
-  const uint32_t sh = (uint32_t)(a & 3);
-  const uint32_t nd = n ? (sh + n + 3) / 4 : 0u;  // dwords touched
-  uint32_t d[5];
-#pragma unroll
-  for (int k = 0; k < 5; k++) d[k] = (uint32_t)k < nd ? base[k] : 0u;
-  uint32_t w[4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint32_t v = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
-    const uint32_t lo = 4u * i;
-    w[i] = v & ((n >= lo + 4) ? 0xffffffffu : (n <= lo) ? 0u : ((1u << (8 * (n - lo))) - 1u));
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-// Bytes [0, n) of v to p: one 16-byte store for a whole aligned block,
-// dword (+ short / byte) stores when p is 4-byte aligned, else bytes.
-// (Each narrow store is a memory request of its own; a record's tag and
-// tail otherwise cost up to 31 of them.)
-__device__ __forceinline__ void store_partial(uint8_t *p, uint4 v, uint32_t n) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  if (n >= 16 && (a & 15) == 0) {
-    *reinterpret_cast<uint4 *>(p) = v;
-  } else if ((a & 3) == 0) {
-    uint32_t *pw = reinterpret_cast<uint32_t *>(p);
-    uint32_t last = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      if (4u * i + 4 <= n) pw[i] = w[i];
-      if (n / 4 == (uint32_t)i) last = w[i];
-    }
-    const uint32_t r = n & 3;
-    if (r) {
-      uint8_t *q = p + (n & ~3u);
-      if (r & 2) *reinterpret_cast<uint16_t *>(q) = (uint16_t)last;
-      if (r & 1) q[r & 2] = (uint8_t)(last >> (8 * (r & 2)));
-    }
-  } else {
-    for (uint32_t i = 0; i < n; i++) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
-  }
-}
-
-__device__ __forceinline__ uint4 mask_block(uint4 v, uint32_t n) {
-  if (n >= 16) return v;
-  uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint32_t lo = 4 * i;
-    const uint32_t m = (n >= lo + 4) ? 0xffffffffu : (n <= lo) ? 0u : ((1u << (8 * (n - lo))) - 1u);
-    w[i] &= m;
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
 __device__ __forceinline__ uint32_t bswap32(uint32_t v) {
   return __builtin_amdgcn_perm(0, v, 0x00010203u);
 }
@@ -632,13 +569,7 @@ __device__ __forceinline__ uint4 crypt_partial_x(const uint8_t *src, uint8_t *ds
   return y;
 }
 
-// 16-byte block loads and stores at any address.  The HSA runtime runs the
-// shader memory in unaligned mode (SH_MEM_CONFIG.alignment_mode), so
-// global_load/store_dwordx4 take byte addresses; the 1-byte-aligned type lets
-// the compiler emit them for records that are not 16-byte aligned (the same
-// instruction an aligned block uses; an unaligned one costs its extra cache
-// line in the TA, nothing on the VALU).
-typedef uint32_t u32_any __attribute__((aligned(1)));
+// 16-byte block loads and stores at any address (u32_any, iov_dev.h).
 
 __device__ __forceinline__ uint4 load_blk_nt(const uint8_t *p) {
   const u32_any *ip = reinterpret_cast<const u32_any *>(p);
@@ -670,130 +601,6 @@ __device__ __forceinline__ uint64_t rec_at(const BatchDesc &b, uint64_t i) {
   return b.order ? (uint64_t)b.order[i] : i;  // (one load; no order array: none)
 }
 
-
-// ---------------------------------------------------------------------------
-// iovec records walked in place (BatchDesc::iovecs; reference
-// EVP_AEAD_CTX_sealv / _openv_detached, aead.cc.inc:316-361, 531-584, whose
-// AEADs walk the chunks with ForEachBlockRange, cipher/internal.h:283-411).
-// A lane keeps a cursor on the chunk holding its current stream position:
-// chunk c covers stream bytes [cs, ce) of the record.
-struct IovCur {
-  uint64_t c, cs, ce;
-  const uint8_t *in;
-  uint8_t *out;
-};
-
-__device__ __forceinline__ void iov_at(IovCur &k, const BatchDesc &b, uint64_t c, uint64_t cs) {
-  const IovecDev v = b.iovecs[c];
-  k.c = c;
-  k.cs = cs;
-  k.ce = cs + v.len;
-  k.in = v.in;
-  k.out = v.out;
-}
-
-// Advance to the chunk holding stream byte p (positions only grow).
-__device__ __forceinline__ void iov_seek(IovCur &k, const BatchDesc &b, uint64_t p,
-                                         uint64_t c_end) {
-  while (p >= k.ce && k.c + 1 < c_end) iov_at(k, b, k.c + 1, k.ce);
-}
-
-// Bytes [a, a + 16) of the 32 bytes A || B (a = 0..16).
-__device__ __forceinline__ uint4 bytes_at(uint4 A, uint4 B, uint32_t a) {
-  const uint32_t w[9] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, 0u};
-  const uint32_t wq = a >> 2, r = a & 3;
-  uint32_t t[5];
-#pragma unroll
-  for (int i = 0; i < 5; i++)
-    t[i] = wq == 0 ? w[i] : wq == 1 ? w[i + 1] : wq == 2 ? w[i + 2] : wq == 3 ? w[i + 3] : w[i + 4];
-  return make_uint4(__builtin_amdgcn_alignbyte(t[1], t[0], r),
-                    __builtin_amdgcn_alignbyte(t[2], t[1], r),
-                    __builtin_amdgcn_alignbyte(t[3], t[2], r),
-                    __builtin_amdgcn_alignbyte(t[4], t[3], r));
-}
-
-// Bytes [p, p + n) (n <= 16, zero past n) of a block that ends in chunk k.c
-// or the next chunk (the usual straddle: at most one boundary): one partial
-// load per piece, joined by a byte shift.  Returns false (nothing loaded)
-// when more chunks are involved.
-__device__ __forceinline__ bool iov_load2(const BatchDesc &b, const IovCur &k, uint64_t p,
-                                          uint32_t n, uint64_t c_end, uint4 &v) {
-  const uint32_t n1 = (uint32_t)min<uint64_t>(n, k.ce - p);
-  uint4 v2 = make_uint4(0, 0, 0, 0);
-  if (n1 < n) {
-    if (k.c + 1 >= c_end) return false;
-    const IovecDev nx = b.iovecs[k.c + 1];
-    if (nx.len < n - n1) return false;
-    v2 = load_partial(nx.in, n - n1);
-  }
-  const uint4 v1 = load_partial(k.in + (p - k.cs), n1);
-  const uint4 s2 = bytes_at(make_uint4(0, 0, 0, 0), v2, 16 - n1);  // v2 << 8 n1
-  v = make_uint4(v1.x | s2.x, v1.y | s2.y, v1.z | s2.z, v1.w | s2.w);
-  return true;
-}
-
-__device__ __forceinline__ bool iov_store2(const BatchDesc &b, const IovCur &k, uint64_t p,
-                                           uint4 y, uint32_t n, uint64_t c_end) {
-  const uint32_t n1 = (uint32_t)min<uint64_t>(n, k.ce - p);
-  IovecDev nx = {nullptr, nullptr, 0};
-  if (n1 < n) {
-    if (k.c + 1 >= c_end) return false;
-    nx = b.iovecs[k.c + 1];
-    if (nx.len < n - n1) return false;
-  }
-  store_partial(k.out + (p - k.cs), y, n1);
-  if (n1 < n) store_partial(nx.out, bytes_at(y, make_uint4(0, 0, 0, 0), n1), n - n1);
-  return true;
-}
-
-// Bytes [p, p + n) of the record's stream (n <= 16, zero past n), byte by
-// byte across chunk boundaries (blocks over three or more chunks).
-__device__ __forceinline__ uint4 iov_gather(const BatchDesc &b, IovCur k, uint64_t p, uint32_t n,
-                                            uint64_t c_end) {
-  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-  for (uint32_t i = 0; i < n; i++) {
-    iov_seek(k, b, p + i, c_end);
-    const uint32_t v = (uint32_t)k.in[p + i - k.cs] << (8 * (i & 3));
-    const uint32_t wi = i >> 2;
-    w0 |= wi == 0 ? v : 0u;
-    w1 |= wi == 1 ? v : 0u;
-    w2 |= wi == 2 ? v : 0u;
-    w3 |= wi == 3 ? v : 0u;
-  }
-  return make_uint4(w0, w1, w2, w3);
-}
-
-__device__ __forceinline__ void iov_scatter(const BatchDesc &b, IovCur k, uint64_t p, uint4 y,
-                                            uint32_t n, uint64_t c_end) {
-  const uint32_t w[4] = {y.x, y.y, y.z, y.w};
-  for (uint32_t i = 0; i < n; i++) {
-    iov_seek(k, b, p + i, c_end);
-    const uint32_t wi = i >> 2;
-    const uint32_t v = wi == 0 ? w[0] : wi == 1 ? w[1] : wi == 2 ? w[2] : w[3];
-    k.out[p + i - k.cs] = (uint8_t)(v >> (8 * (i & 3)));
-  }
-}
-
-// Bytes [pos, pos + n) of the concatenation of chunks v[c0 .. c1) (AD of an
-// iovec record; n <= 16, zero past n).  Walks from c0: the AD is short.
-__device__ __forceinline__ uint4 ivec_load16(const IvecDev *v, uint64_t c0, uint64_t c1,
-                                             uint64_t pos, uint32_t n) {
-  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-  uint64_t c = c0, cs = 0;
-  for (uint32_t i = 0; i < n; i++) {
-    while (c < c1 && pos + i >= cs + v[c].len) {
-      cs += v[c].len;
-      c++;
-    }
-    const uint32_t x = (uint32_t)v[c].in[pos + i - cs] << (8 * (i & 3));
-    const uint32_t wi = i >> 2;
-    w0 |= wi == 0 ? x : 0u;
-    w1 |= wi == 1 ? x : 0u;
-    w2 |= wi == 2 ? x : 0u;
-    w3 |= wi == 3 ? x : 0u;
-  }
-  return make_uint4(w0, w1, w2, w3);
-}
 
 // Per-record state handed from the prologue to the bulk kernel (64 bytes).
 struct alignas(16) RecState {

@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include "internal.h"
+#include "iov_dev.h"
 
 namespace bssl_amd {
 namespace {
@@ -429,7 +430,10 @@ __device__ __forceinline__ void siv_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int NR, bool OPEN>
+// IOV: iovec records walked in place (BatchDesc::iovecs, iov_dev.h): both
+// passes over the message follow the chunks with per-lane walks (stride
+// 16 kL bytes).
+template <int NR, bool OPEN, bool IOV>
 __device__ __forceinline__ void siv_record(const GcmKeyDev *__restrict__ keys, const BatchDesc &b,
                                            Lds &L, const RecLanes &R, uint64_t rec) {
   const int q = R.q;
@@ -561,17 +565,36 @@ __device__ __forceinline__ void siv_record(const GcmKeyDev *__restrict__ keys, c
   uint4 acc = make_uint4(0, 0, 0, 0);
   uint64_t jlast = 0;
   bool any = false;
+  IovWalk wl, ws;  // (IOV) loads and stores of the lane's message blocks
+  if constexpr (IOV) {
+    if (live) {
+      iov_walk_init(wl, b, rec);
+      iov_walk_init(ws, b, rec);
+    }
+  }
   for (uint64_t j = q; j < n; j += kL) {
     uint4 blk;
     if (j < nA) {
-      blk = load_block(ad + 16 * j, ad_len - 16 * j);
+      if constexpr (IOV)
+        blk = ivec_load16(b.aadvecs, b.aadvec_start[rec], b.aadvec_start[rec + 1], 16 * j,
+                          (uint32_t)min<uint64_t>(ad_len - 16 * j, 16));
+      else
+        blk = load_block(ad + 16 * j, ad_len - 16 * j);
     } else if (j < nA + nP) {
       const uint64_t p = j - nA;
-      const uint4 x = load_block(src + 16 * p, len - 16 * p);
+      const uint32_t pn = (uint32_t)min<uint64_t>(len - 16 * p, 16);
+      uint4 x;
+      if constexpr (IOV)
+        x = iov_walk_load(wl, b, rec, 16 * p, pn, 16 * kL);
+      else
+        x = load_block(src + 16 * p, len - 16 * p);
       if (OPEN) {
         const uint4 ks = aes_enc<NR>(make_uint4(ctr0.x + (uint32_t)p, ctr0.y, ctr0.z, ctr0.w), rk, L);
         uint4 y = xor4(x, ks);
-        store_block(dst + 16 * p, y, len - 16 * p);
+        if constexpr (IOV)
+          iov_walk_store(ws, b, rec, 16 * p, y, pn, 16 * kL);
+        else
+          store_block(dst + 16 * p, y, len - 16 * p);
         const uint64_t rem = len - 16 * p;  // mask the padding of a partial block
         if (rem < 16) {
           uint32_t w[4] = {y.x, y.y, y.z, y.w};
@@ -635,8 +658,17 @@ __device__ __forceinline__ void siv_record(const GcmKeyDev *__restrict__ keys, c
     const uint32_t s1 = ctr0.y ^ r0.y, s2 = ctr0.z ^ r0.z, s3 = ctr0.w ^ r0.w;
     CtrWindow wc;
 #endif
+    if constexpr (IOV) {
+      iov_walk_init(wl, b, rec);
+      iov_walk_init(ws, b, rec);
+    }
     for (uint64_t p = q; p < nP; p += kL) {
-      const uint4 x = load_block(src + 16 * p, len - 16 * p);
+      const uint32_t pn = (uint32_t)min<uint64_t>(len - 16 * p, 16);
+      uint4 x;
+      if constexpr (IOV)
+        x = iov_walk_load(wl, b, rec, 16 * p, pn, 16 * kL);
+      else
+        x = load_block(src + 16 * p, len - 16 * p);
 #if BSSL_AMD_SIV_CTRCACHE
       const uint32_t s0 = (ctr0.x + (uint32_t)p) ^ r0.x;
       wc.update(s0, s1, s2, s3, rk, L);
@@ -644,7 +676,10 @@ __device__ __forceinline__ void siv_record(const GcmKeyDev *__restrict__ keys, c
 #else
       const uint4 ks = aes_enc<NR>(make_uint4(ctr0.x + (uint32_t)p, ctr0.y, ctr0.z, ctr0.w), rk, L);
 #endif
-      store_block(dst + 16 * p, xor4(x, ks), len - 16 * p);
+      if constexpr (IOV)
+        iov_walk_store(ws, b, rec, 16 * p, mask_block(xor4(x, ks), pn), pn, 16 * kL);
+      else
+        store_block(dst + 16 * p, xor4(x, ks), len - 16 * p);
     }
   }
   if (active && q == 0) {
@@ -652,13 +687,17 @@ __device__ __forceinline__ void siv_record(const GcmKeyDev *__restrict__ keys, c
     if (b.status) b.status[rec] = ok ? 1 : 0;
   }
   // Zero the output of a failed record (aead.cc.inc:132-139, 539-547).
-  if (active && !ok)
-    for (uint64_t p = q; 16 * p < len; p += kL)
-      store_block(dst + 16 * p, make_uint4(0, 0, 0, 0), len - 16 * p);
+  if (active && !ok) {
+    if constexpr (IOV)
+      iov_clear(b, rec, q, kL);
+    else
+      for (uint64_t p = q; 16 * p < len; p += kL)
+        store_block(dst + 16 * p, make_uint4(0, 0, 0, 0), len - 16 * p);
+  }
   siv_wave_sync();  // the slot's round keys / tables are free for the next record
 }
 
-template <int NR, bool OPEN>
+template <int NR, bool OPEN, bool IOV>
 __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyDev *__restrict__ keys,
                                                            BatchDesc b,
                                                            uint32_t *__restrict__ units) {
@@ -676,7 +715,7 @@ __global__ __launch_bounds__(kThreads) SIV_OCC void gcm_siv_kernel(const GcmKeyD
     if (lane == 0) u = atomicAdd(units, 1u);
     u = __builtin_amdgcn_readfirstlane(__shfl(u, 0, 64));
     if ((uint64_t)u * 4 >= b.num_records) break;
-    siv_record<NR, OPEN>(keys, b, L, R, (uint64_t)u * 4 + local);
+    siv_record<NR, OPEN, IOV>(keys, b, L, R, (uint64_t)u * 4 + local);
   }
 }
 
@@ -702,20 +741,18 @@ int launch_gcm_siv(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr,
   const uint64_t wanted = (b.num_records + kRecs - 1) / kRecs;
   const unsigned grid = (unsigned)(wanted < (uint64_t)num_cus ? wanted : (uint64_t)num_cus);
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
+  const bool iov = b.iovecs != nullptr;
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, s, keys, b, units); };
   if (nr == 14) {
     if (open)
-      hipLaunchKernelGGL((gcm_siv_kernel<14, true>), dim3(grid), dim3(kThreads), 0, s, keys, b,
-                         units);
+      iov ? go(gcm_siv_kernel<14, true, true>) : go(gcm_siv_kernel<14, true, false>);
     else
-      hipLaunchKernelGGL((gcm_siv_kernel<14, false>), dim3(grid), dim3(kThreads), 0, s, keys, b,
-                         units);
+      iov ? go(gcm_siv_kernel<14, false, true>) : go(gcm_siv_kernel<14, false, false>);
   } else {
     if (open)
-      hipLaunchKernelGGL((gcm_siv_kernel<10, true>), dim3(grid), dim3(kThreads), 0, s, keys, b,
-                         units);
+      iov ? go(gcm_siv_kernel<10, true, true>) : go(gcm_siv_kernel<10, true, false>);
     else
-      hipLaunchKernelGGL((gcm_siv_kernel<10, false>), dim3(grid), dim3(kThreads), 0, s, keys, b,
-                         units);
+      iov ? go(gcm_siv_kernel<10, false, true>) : go(gcm_siv_kernel<10, false, false>);
   }
   const int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);

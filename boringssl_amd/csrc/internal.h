@@ -192,15 +192,12 @@ struct IovBatchDesc {
   uint8_t *tags;
   uint8_t *status;
 };
-// Runs the bulk kernels over the gathered records (a contiguous BatchDesc
+// Runs the bulk kernels over an iovec batch (a BatchDesc with `iovecs` set,
 // whose tag_len / key fields the runner fills in).  Returns 0 or an error.
 struct IovRunner {
   virtual int operator()(BatchDesc &d) const = 0;
-  // Whether the AEAD's kernels walk the chunks in place (BatchDesc::iovecs,
-  // AES-GCM); otherwise the records are gathered into staging and scattered.
-  virtual bool in_place() const { return false; }
 };
-// Gather -> run -> scatter; synchronises `stream` once (staging size).
+// Per-record totals -> run; no staging, no stream synchronisation.
 int iov_batch_run(const IovBatchDesc &b, const IovRunner &run, void *stream);
 int launch_synth(uint64_t first, size_t n, const uint64_t *offsets,
                  const uint64_t *lengths, uint8_t *pt, uint8_t *nonces,

@@ -844,22 +844,25 @@ def test_iovec_batch_vs_oracle(aead):
             assert st[i] == 1 and got == pts[i], i
 
 
-@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm"])
+@pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm", "chacha20-poly1305",
+                                  "xchacha20-poly1305", "aes-128-gcm-siv", "aes-256-gcm-siv"])
 @pytest.mark.parametrize("n", [300, 4500])
 def test_iovec_in_place_walk(aead, n):
-    """The AES-GCM kernels walk iovec chunks in place (BatchDesc::iovecs):
-    chunks of 0..4097 bytes incl. empty and 1-byte chunks, input and output
-    at independent alignments 0..15 (so the loads and the stores shift by
-    different amounts), blocks straddling several chunks, records up to
-    32 KiB, and >= 4096 records (length-ordered schedule); seal vs the
+    """Every AEAD's kernels walk iovec chunks in place
+    (BatchDesc::iovecs): chunks of 0..4097 bytes incl. empty and 1-byte
+    chunks, input and output at independent alignments 0..15 (so the loads
+    and the stores shift by different amounts), blocks straddling several
+    chunks, records up to 32 KiB, AD of up to 100 bytes in one or two
+    chunks, and >= 4096 records (length-ordered schedule); seal vs the
     oracle, then open with a corrupted tag zeroing that record's chunks."""
     rng = random.Random(n * 31 + len(aead))
     key = bytes(rng.getrandbits(8) for _ in range(AEAD_KEYLEN[aead]))
-    lens = [rng.choice([0, 1, 15, 16, 17, 31, 255, 1350, 4096, 16384, 16397, 32768])
+    nl = _nl(aead)
+    lens = [rng.choice([0, 1, 15, 16, 17, 31, 63, 64, 65, 255, 1350, 4096, 16384, 16397, 32768])
             for _ in range(n)]
     pts = [rng.randbytes(L) for L in lens]
-    ads = [rng.randbytes(rng.choice([0, 5, 13, 29])) for _ in range(n)]
-    nonces = [rng.randbytes(12) for _ in range(n)]
+    ads = [rng.randbytes(rng.choice([0, 5, 13, 29, 64, 100])) for _ in range(n)]
+    nonces = [rng.randbytes(nl) for _ in range(n)]
     chunks, starts = [], [0]  # (in_off, out_off, bytes)
     ipos, opos = 0, 0
     for i in range(n):
@@ -884,14 +887,24 @@ def test_iovec_in_place_walk(aead, n):
     d_dst = torch.zeros(opos + 32, dtype=torch.uint8, device=DEV)
     sb, db, ab = d_src.data_ptr(), d_dst.data_ptr(), d_ad.data_ptr()
     iov = np.array([(db + oo, sb + io, len(p)) for io, oo, p in chunks], dtype=np.int64)
-    aiv = np.array([(ab + int(ad_offs[i]), len(ads[i])) for i in range(n)], dtype=np.int64)
+    # AD longer than 10 bytes in two chunks (cut at a random point).
+    aiv_l, astarts = [], [0]
+    for i in range(n):
+        a0, la = int(ad_offs[i]), len(ads[i])
+        if la > 10:
+            cut = rng.randint(1, la - 1)
+            aiv_l += [(ab + a0, cut), (ab + a0 + cut, la - cut)]
+        else:
+            aiv_l.append((ab + a0, la))
+        astarts.append(len(aiv_l))
+    aiv = np.array(aiv_l, dtype=np.int64)
     d_starts = _t(np.array(starts, np.int64))
-    d_astarts = _t(np.arange(n + 1, dtype=np.int64))
+    d_astarts = _t(np.array(astarts, np.int64))
     d_nonce = _t(np.frombuffer(b"".join(nonces), dtype=np.uint8).copy())
     d_tags = torch.zeros(16 * n, dtype=torch.uint8, device=DEV)
     d_st = torch.full((n,), 7, dtype=torch.uint8, device=DEV)
     ctx = ba.AEADCtx(aead, key, 16)
-    b = ba.make_iov_batch(n, _t(iov.reshape(-1, 3)), d_starts, d_tags, d_nonce, 12,
+    b = ba.make_iov_batch(n, _t(iov.reshape(-1, 3)), d_starts, d_tags, d_nonce, nl,
                           aadvecs=_t(aiv.reshape(-1, 2)), aadvec_start=d_astarts, status=d_st)
     ctx.sealv_batch_device(b)
     torch.cuda.synchronize()
@@ -910,7 +923,7 @@ def test_iovec_in_place_walk(aead, n):
         tg[16 * i + 5] ^= 0x10
     iov2 = np.array([(db + oo, db + oo, len(p)) for _, oo, p in chunks], dtype=np.int64)
     d_st.fill_(7)
-    b2 = ba.make_iov_batch(n, _t(iov2.reshape(-1, 3)), d_starts, _t(tg), d_nonce, 12,
+    b2 = ba.make_iov_batch(n, _t(iov2.reshape(-1, 3)), d_starts, _t(tg), d_nonce, nl,
                            aadvecs=_t(aiv.reshape(-1, 2)), aadvec_start=d_astarts, status=d_st)
     ctx.openv_detached_batch_device(b2)
     torch.cuda.synchronize()
