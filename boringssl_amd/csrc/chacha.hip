@@ -928,20 +928,20 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   // The record's powers of r go to LDS (slot per record, written by its lane
   // 0, read back by all L lanes as broadcasts): kept in registers across the
   // ChaCha rounds they cost ~35 VGPRs and thereby a wave per SIMD.
-  // Slot layout: pw[0..kLog+2] then r^3, 5 limbs each.
-  __shared__ uint32_t s_pow[kThreads / L][5 * (kLog + 4)];
+  // s_apow: the block loop's four multipliers R^L, r^3, r^2, r with their 5x
+  // multiples, 16-byte aligned (one batch of ds_read_b128 per absorb);
+  // s_pow: r^(2^k) for k = 2 .. kLog + 1 (the AD and lane trees), 5 limbs
+  // each -- r and r^2 are read from s_apow.
+  __shared__ uint32_t s_pow[kThreads / L][5 * kLog];
   __shared__ uint4 s_apow[kThreads / L][9];
   uint32_t *const mypow = s_pow[threadIdx.x / L];
+  const uint32_t *const apw = reinterpret_cast<const uint32_t *>(s_apow[threadIdx.x / L]);
   if (q == 0) {
     const P r3v = pmul(pw[1], pw[0]);
 #pragma unroll
-    for (int k = 0; k <= kLog + 2; k++)
+    for (int k = 2; k <= kLog + 1; k++)
 #pragma unroll
-      for (int i = 0; i < 5; i++) mypow[5 * k + i] = pw[k].h[i];
-#pragma unroll
-    for (int i = 0; i < 5; i++) mypow[5 * (kLog + 3) + i] = r3v.h[i];
-    // The block loop's four multipliers R^L, r^3, r^2, r with their 5x
-    // multiples, 16-byte aligned: one batch of ds_read_b128 per absorb.
+      for (int i = 0; i < 5; i++) mypow[5 * (k - 2) + i] = pw[k].h[i];
     const P *am[4] = {&pw[kLog + 2], &r3v, &pw[1], &pw[0]};
     uint32_t *ap = reinterpret_cast<uint32_t *>(s_apow[threadIdx.x / L]);
 #pragma unroll
@@ -953,17 +953,17 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     }
   }
   __builtin_amdgcn_wave_barrier();
-  // Power k (k = kLog + 3: r^3), re-read at each use (the address is
-  // laundered so the loads are not hoisted out of the loops).
+  // r^(2^k), k = 0 .. kLog + 1, re-read at each use (the offset is laundered
+  // so the loads are not hoisted out of the loops).
   auto pwr = [&](int k) {
-    uint32_t off = 5 * k;
+    const uint32_t *base = k < 2 ? apw : mypow;
+    uint32_t off = k == 0 ? 27u : k == 1 ? 18u : 5u * (k - 2);
     asm volatile("" : "+v"(off));
     P o;
 #pragma unroll
-    for (int i = 0; i < 5; i++) o.h[i] = mypow[off + i];
+    for (int i = 0; i < 5; i++) o.h[i] = base[off + i];
     return o;
   };
-  constexpr int kR3 = kLog + 3, kStride = kLog + 2;  // r^3, R^L = r^(4L)
 
   // AD: exclusive Horner in r over the zero-padded 16-byte blocks, stride L.
   P ya = pzero();
