@@ -45,6 +45,22 @@ constexpr int kThreads = BSSL_AMD_CHACHA_THREADS;
 #ifndef BSSL_AMD_CHACHA_PRIO
 #define BSSL_AMD_CHACHA_PRIO 2
 #endif
+// XChaCha20-Poly1305 runs with 2 lanes per record (32 records per wave):
+// its per-record HChaCha20 makes the per-record work heavier, and spreading
+// it over twice the blocks per lane measured +3.7-4.5 % on config3x (same-box
+// A/Bs: 1,036 vs 999 and 1,038 vs 993 GiB/s; ChaCha20-Poly1305 ties at 1,084
+// vs 1,085), at 3 waves per SIMD (no spills; 4 waves would spill 22
+// registers, -8 %).
+#ifndef BSSL_AMD_XCHACHA_L
+#define BSSL_AMD_XCHACHA_L 2
+#endif
+// iovec records (IOV kernels): per-lane block I/O either way (the
+// record-contiguous staging needs whole aligned records), so 2 lanes per
+// record at 3 waves per SIMD without spills: 694 vs 552 GiB/s (4 lanes, 61
+// spills) on 3-chunk 1350-byte records.
+#ifndef BSSL_AMD_CHACHA_IOV_L
+#define BSSL_AMD_CHACHA_IOV_L 2
+#endif
 #ifndef BSSL_AMD_CHACHA_L
 #define BSSL_AMD_CHACHA_L 4
 #endif
@@ -425,7 +441,7 @@ __device__ __forceinline__ void crypt_block_x(const uint8_t *src, uint8_t *dst, 
 #define BSSL_AMD_CHACHA_WPE 4
 #endif
 #if BSSL_AMD_CHACHA_WPE
-#define CHACHA_OCC __attribute__((amdgpu_waves_per_eu(BSSL_AMD_CHACHA_WPE)))
+#define CHACHA_OCC __attribute__((amdgpu_waves_per_eu(L == 2 ? 3 : BSSL_AMD_CHACHA_WPE)))
 #else
 #define CHACHA_OCC
 #endif
@@ -1221,7 +1237,9 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
 #endif
 }
 
-// One wave group per wave.
+// One wave group per wave.  (A persistent form -- 4 or 8 workgroups per CU
+// taking record groups from a grid-wide counter -- measured 7-8 % slower on
+// configs 3 and 3x, profiles/r03/s10/.)
 template <bool OPEN, int L, bool XT, bool XC, bool IOV>
 __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
     const ChaChaKeyDev *__restrict__ keys, BatchDesc b) {
@@ -1231,7 +1249,7 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
 
 template <bool OPEN, bool XT, bool XC, bool IOV = false>
 void launch_one(const ChaChaKeyDev *keys, const BatchDesc &b, uint64_t blocks, hipStream_t s) {
-  constexpr int L = BSSL_AMD_CHACHA_L;
+  constexpr int L = XC ? BSSL_AMD_XCHACHA_L : IOV ? BSSL_AMD_CHACHA_IOV_L : BSSL_AMD_CHACHA_L;
   hipLaunchKernelGGL((chacha_poly_kernel<OPEN, L, XT, XC, IOV>), dim3((unsigned)blocks),
                      dim3(kThreads), 0, s, keys, b);
 }
@@ -1242,7 +1260,9 @@ int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, bool 
                   void *stream, const KernelEvents *ev) {
   if (b.num_records == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  constexpr int L = BSSL_AMD_CHACHA_L;  // lanes per record (see chacha_poly_kernel)
+  const int L = xchacha   ? BSSL_AMD_XCHACHA_L
+                : b.iovecs ? BSSL_AMD_CHACHA_IOV_L
+                           : BSSL_AMD_CHACHA_L;  // lanes per record (launch_one)
   const uint64_t blocks = (b.num_records * L + kThreads - 1) / kThreads;
   if (blocks > 0x7fffffffu) return 1;
   BatchDesc bo = b;  // with the processing order of a ragged batch
