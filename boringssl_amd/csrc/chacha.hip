@@ -61,9 +61,6 @@ constexpr int kThreads = BSSL_AMD_CHACHA_THREADS;
 #ifndef BSSL_AMD_CHACHA_IOV_L
 #define BSSL_AMD_CHACHA_IOV_L 2
 #endif
-#ifndef BSSL_AMD_CHACHA_L
-#define BSSL_AMD_CHACHA_L 4
-#endif
 #ifndef BSSL_AMD_CHACHA_UNROLL
 #define BSSL_AMD_CHACHA_UNROLL 10
 #endif
@@ -1247,11 +1244,22 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
                                 (uint64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6));
 }
 
-template <bool OPEN, bool XT, bool XC, bool IOV = false>
-void launch_one(const ChaChaKeyDev *keys, const BatchDesc &b, uint64_t blocks, hipStream_t s) {
-  constexpr int L = XC ? BSSL_AMD_XCHACHA_L : IOV ? BSSL_AMD_CHACHA_IOV_L : BSSL_AMD_CHACHA_L;
+template <int L, bool OPEN, bool XT, bool XC, bool IOV = false>
+void launch_one(const ChaChaKeyDev *keys, const BatchDesc &b, hipStream_t s) {
+  const uint64_t blocks = (b.num_records * L + kThreads - 1) / kThreads;
   hipLaunchKernelGGL((chacha_poly_kernel<OPEN, L, XT, XC, IOV>), dim3((unsigned)blocks),
                      dim3(kThreads), 0, s, keys, b);
+}
+
+// ChaCha20-Poly1305 batches take 4 lanes per record (the record-contiguous
+// LDS-DMA I/O, whole 128-byte lines with the slot shift) only when every
+// record sits on a 128-byte boundary -- a uniform layout with a 128-byte
+// multiple stride -- and 2 lanes per record otherwise: config 3 at 128-byte
+// alignment 1,085-1,092 (4 lanes) vs 1,076 GiB/s (2 lanes), at 16-byte
+// alignment 1,021-1,032 vs 1,066-1,080 (same box, profiles/r03/s11/).
+bool whole_lines(const BatchDesc &b) {
+  return !b.offsets && b.record_stride % 128 == 0 &&
+         ((reinterpret_cast<uintptr_t>(b.in) | reinterpret_cast<uintptr_t>(b.out)) & 127) == 0;
 }
 
 }  // namespace
@@ -1260,11 +1268,7 @@ int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, bool 
                   void *stream, const KernelEvents *ev) {
   if (b.num_records == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int L = xchacha   ? BSSL_AMD_XCHACHA_L
-                : b.iovecs ? BSSL_AMD_CHACHA_IOV_L
-                           : BSSL_AMD_CHACHA_L;  // lanes per record (launch_one)
-  const uint64_t blocks = (b.num_records * L + kThreads - 1) / kThreads;
-  if (blocks > 0x7fffffffu) return 1;
+  if ((b.num_records * 4 + kThreads - 1) / kThreads > 0x7fffffffu) return 1;
   BatchDesc bo = b;  // with the processing order of a ragged batch
   uint32_t *order = nullptr;
   if (wants_length_order(b)) {
@@ -1280,26 +1284,35 @@ int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, bool 
   }
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
   const bool xt = b.extra_len != 0;
+  constexpr int LX = BSSL_AMD_XCHACHA_L, LI = BSSL_AMD_CHACHA_IOV_L;
   if (b.iovecs) {  // iovec records walked in place (never with extra bytes)
     if (xchacha)
-      open ? launch_one<true, false, true, true>(keys, bo, blocks, s)
-           : launch_one<false, false, true, true>(keys, bo, blocks, s);
+      open ? launch_one<LX, true, false, true, true>(keys, bo, s)
+           : launch_one<LX, false, false, true, true>(keys, bo, s);
     else
-      open ? launch_one<true, false, false, true>(keys, bo, blocks, s)
-           : launch_one<false, false, false, true>(keys, bo, blocks, s);
+      open ? launch_one<LI, true, false, false, true>(keys, bo, s)
+           : launch_one<LI, false, false, false, true>(keys, bo, s);
   } else if (xchacha) {
     if (open)
-      xt ? launch_one<true, true, true>(keys, bo, blocks, s)
-         : launch_one<true, false, true>(keys, bo, blocks, s);
+      xt ? launch_one<LX, true, true, true>(keys, bo, s)
+         : launch_one<LX, true, false, true>(keys, bo, s);
     else
-      xt ? launch_one<false, true, true>(keys, bo, blocks, s)
-         : launch_one<false, false, true>(keys, bo, blocks, s);
-  } else if (open) {
-    xt ? launch_one<true, true, false>(keys, bo, blocks, s)
-       : launch_one<true, false, false>(keys, bo, blocks, s);
+      xt ? launch_one<LX, false, true, true>(keys, bo, s)
+         : launch_one<LX, false, false, true>(keys, bo, s);
+  } else if (whole_lines(b)) {
+    if (open)
+      xt ? launch_one<4, true, true, false>(keys, bo, s)
+         : launch_one<4, true, false, false>(keys, bo, s);
+    else
+      xt ? launch_one<4, false, true, false>(keys, bo, s)
+         : launch_one<4, false, false, false>(keys, bo, s);
   } else {
-    xt ? launch_one<false, true, false>(keys, bo, blocks, s)
-       : launch_one<false, false, false>(keys, bo, blocks, s);
+    if (open)
+      xt ? launch_one<2, true, true, false>(keys, bo, s)
+         : launch_one<2, true, false, false>(keys, bo, s);
+    else
+      xt ? launch_one<2, false, true, false>(keys, bo, s)
+         : launch_one<2, false, false, false>(keys, bo, s);
   }
   const int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);

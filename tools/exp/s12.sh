@@ -1,0 +1,12 @@
+set -u
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 1200 python -u -m pytest tests/ -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest.log 2>&1 || { tail -30 gpurun_out/pytest.log; exit 1; }
+tail -1 gpurun_out/pytest.log
+for al in 128 16; do
+ for c in config3 config3x; do
+  BSSL_AMD_ALIGN=$al timeout -k 10 300 python bench.py --config $c --no-cpu-baseline > gpurun_out/b_${c}_a$al.log 2>&1 || exit 1
+  echo "$c align=$al $(grep -o '"value": [0-9.]*\|"parity": "[^"]*"\|"avg_kernel_ms": [0-9.]*' gpurun_out/b_${c}_a$al.log | tr '\n' ' ')"
+ done
+done
