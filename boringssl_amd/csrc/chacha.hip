@@ -45,21 +45,14 @@ constexpr int kThreads = BSSL_AMD_CHACHA_THREADS;
 #ifndef BSSL_AMD_CHACHA_PRIO
 #define BSSL_AMD_CHACHA_PRIO 2
 #endif
-// XChaCha20-Poly1305 runs with 2 lanes per record (32 records per wave):
-// its per-record HChaCha20 makes the per-record work heavier, and spreading
-// it over twice the blocks per lane measured +3.7-4.5 % on config3x (same-box
-// A/Bs: 1,036 vs 999 and 1,038 vs 993 GiB/s; ChaCha20-Poly1305 ties at 1,084
-// vs 1,085), at 3 waves per SIMD (no spills; 4 waves would spill 22
-// registers, -8 %).
-#ifndef BSSL_AMD_XCHACHA_L
-#define BSSL_AMD_XCHACHA_L 2
-#endif
-// iovec records (IOV kernels): per-lane block I/O either way (the
-// record-contiguous staging needs whole aligned records), so 2 lanes per
-// record at 3 waves per SIMD without spills: 694 vs 552 GiB/s (4 lanes, 61
-// spills) on 3-chunk 1350-byte records.
-#ifndef BSSL_AMD_CHACHA_IOV_L
-#define BSSL_AMD_CHACHA_IOV_L 2
+// Lanes per record (round 3: 2 for every AEAD and layout, 32 records per
+// wave, 3 waves per SIMD at ~150-170 VGPRs without spills).  Against 4 lanes
+// (128 VGPRs, 4 waves, 27-43 spills), same box (profiles/r03/s13/): config 3
+// at 128-byte alignment 1,192 vs 1,069-1,079 GiB/s, config3x 1,110-1,124 vs
+// 999; the per-record work (key block, powers of r, lane tree, tag; for
+// XChaCha one HChaCha20) is spread over twice the blocks per lane.
+#ifndef BSSL_AMD_CHACHA_LANES
+#define BSSL_AMD_CHACHA_LANES 2
 #endif
 #ifndef BSSL_AMD_CHACHA_UNROLL
 #define BSSL_AMD_CHACHA_UNROLL 10
@@ -497,7 +490,9 @@ __device__ __forceinline__ T meta_load(const T *arr, uint64_t i, bool active) {
 
 // One wave group: records pos = grp * (64 / L) + lane / L.
 // IOV: iovec records walked in place (BatchDesc::iovecs; no extra bytes).
-template <bool OPEN, int L, bool XT, bool XC, bool IOV>
+// COAL: the record-contiguous I/O (launch_chacha picks it for batches whose
+// records all start 128-byte lines).
+template <bool OPEN, int L, bool XT, bool XC, bool IOV, bool COAL>
 __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ keys,
                                              const BatchDesc &b, uint64_t grp) {
 #if BSSL_AMD_CHACHA_STAMPS
@@ -628,7 +623,8 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   // 4 it - 1 - sh ..) covers whole 128-byte lines instead of half lines at
   // both ends (the other half written one iteration later); the Poly1305
   // element order then starts with a zero element (Y_A at v = sh).
-  constexpr bool kCoalSh = BSSL_AMD_CHACHA_COAL && BSSL_AMD_CHACHA_SHIFT && L == 4 && !IOV;
+  constexpr bool kCoalL = COAL && (L == 4 || L == 2);
+  constexpr bool kCoalSh = BSSL_AMD_CHACHA_COAL && BSSL_AMD_CHACHA_SHIFT && kCoalL && !IOV;
   // (Wave-uniform: 1 only if every live record of the wave is 128-byte
   // aligned, so the slot arithmetic stays scalar.)
   const uint64_t live_mask = __ballot(live);
@@ -642,18 +638,21 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   // chunk j at + 16 ((j + q + r) mod 4) -- conflict-free both for the 16
   // chunks of a record and for the 4 chunks a lane reads of its own block).
   __shared__ uint4 s_c0[kThreads][4];
-  constexpr bool kCoal = BSSL_AMD_CHACHA_COAL && L == 4 && !IOV;
+  constexpr bool kCoal = BSSL_AMD_CHACHA_COAL && kCoalL && !IOV;
   // Per record slot: byte offset and the number of full 64-byte blocks the
   // coalesced path moves (0 unless the record is live and 16-byte aligned).
   __shared__ uint4 s_rinfo[kThreads / L];
   const int wbase = threadIdx.x & ~63;
   uint8_t *const stage = reinterpret_cast<uint8_t *>(&s_c0[wbase][0]);
-  const int rslot = lane / L;
   if (kCoal && q == 0) {
     const uint32_t nfull = live && aligned ? (uint32_t)(m.len / 64) : 0u;
     s_rinfo[threadIdx.x / L] = make_uint4((uint32_t)m.off, (uint32_t)(m.off >> 32), nfull, sh);
   }
-  auto saddr = [](int r, int qq, int j) { return r * 256 + qq * 64 + ((j + qq + r) & 3) * 16; };
+  // Staging: the 64-byte block of wave lane t (record slot t / L, block
+  // t mod L of the iteration's run) at t * 64, its 16-byte chunk j at
+  // + 16 ((j + t + t / 4) mod 4): the 16 lanes of a ds_read_b128 lane group
+  // read 16 distinct bank quads, for L = 4 and L = 2 alike.
+  auto saddr = [](int t, int j) { return t * 64 + ((j + (t & 3) + (t >> 2)) & 3) * 16; };
 
   // Encrypt (or decrypt) the data block of ChaCha block u held in ks; returns
   // the ciphertext words (masked past the end) in c[].
@@ -832,17 +831,17 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     } else if (kCoal && staged && m.len >= 64 * d + 64 && aligned) {
       // Full block, coalesced I/O: input from the staging area, output back
       // to it (stored after the iteration by record-contiguous stores).
-      uint8_t *my = stage + rslot * 256 + q * 64;
+      uint8_t *my = stage + lane * 64;
 #pragma unroll
       for (int i = 0; i < 4; i++) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(my + ((i + q + rslot) & 3) * 16);
+        const uint4 v = *reinterpret_cast<const uint4 *>(my + ((i + (lane & 3) + (lane >> 2)) & 3) * 16);
         x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
       }
 #pragma unroll
       for (int i = 0; i < 16; i++) y[i] = x[i] ^ ks[i];
 #pragma unroll
       for (int i = 0; i < 4; i++)
-        *reinterpret_cast<uint4 *>(my + ((i + q + rslot) & 3) * 16) =
+        *reinterpret_cast<uint4 *>(my + ((i + (lane & 3) + (lane >> 2)) & 3) * 16) =
             make_uint4(y[4 * i], y[4 * i + 1], y[4 * i + 2], y[4 * i + 3]);
     } else if (m.len >= 64 * d + 64 && aligned) {
       uint4 *dp = reinterpret_cast<uint4 *>(dst + 64 * d);
@@ -1061,14 +1060,18 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     absorb((uint64_t)q, c0);
   }
   CSTAMP(2);
-  // Coalesced I/O: in instruction k, lane l moves 16-byte chunk l mod 16 of
-  // record slot 4k + l/16's data blocks 4 it - 1 .. 4 it + 2 (256 bytes).
-  const int cq = (lane & 15) >> 2, cj = lane & 3;
+  // Coalesced I/O: in instruction k, lane l moves 16-byte chunk cj = l mod 4
+  // of the block of wave lane t = 16 k + l / 4 (record slot t / L, block
+  // t mod L of the iteration: data block it L + t mod L - 1 - sh), so the 64
+  // lanes cover 1 KiB of whole record runs (L = 4: 4 records x 256 bytes;
+  // L = 2: 8 records x 128 bytes).
+  const int cj = lane & 3;
   auto coal_addr = [&](int k, int it, uint64_t &addr) {
-    uint32_t slot = wbase / L + 4 * k + (lane >> 4);
+    const int t = 16 * k + (lane >> 2);
+    uint32_t slot = wbase / L + t / L;
     asm volatile("" : "+v"(slot));  // re-read per use, not hoisted (registers)
     const uint4 inf = s_rinfo[slot];
-    const uint64_t dd = (uint64_t)it * 4 + cq - 1 - inf.w;  // (it >= 1: no wrap)
+    const uint64_t dd = (uint64_t)it * L + (t & (L - 1)) - 1 - inf.w;  // (it >= 1: no wrap)
     addr = ((uint64_t)inf.y << 32 | inf.x) + 64 * dd + 16 * cj;
     return dd < inf.z;
   };
@@ -1082,14 +1085,14 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     if constexpr (kCoal) {
       // Direct-to-LDS loads (global_load_lds_dwordx4, no VGPRs): instruction
       // k writes the wave's staging bytes [1024 k, 1024 k + 1024) lane-
-      // linearly, so lane l lands at record slot r = 4k + l/16, position
-      // l mod 16 = 4 qq + p, and loads the chunk j whose swizzled position
-      // (j + qq + r) mod 4 is p.
+      // linearly, so lane l lands in the block of wave lane t = 16 k + l / 4
+      // at position p = l mod 4, and loads the chunk j whose swizzled
+      // position (saddr) is p.
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         uint64_t a;
-        const int r = 4 * k + (lane >> 4);
-        const int j = (cj - cq - r) & 3;
+        const int t = 16 * k + (lane >> 2);
+        const int j = (cj - (t & 3) - (t >> 2)) & 3;
         if (BSSL_AMD_CHACHA_ABLATE != 7 && coal_addr(k, it, a))
           __builtin_amdgcn_global_load_lds(
               reinterpret_cast<const void *>(b.in + a - 16 * cj + 16 * j),
@@ -1129,7 +1132,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
       for (int k = 0; k < 4; k++) {
         uint64_t a;
         if (coal_addr(k, it, a)) {
-          const uint4 v = *reinterpret_cast<const uint4 *>(stage + saddr(4 * k + (lane >> 4), cq, cj));
+          const uint4 v = *reinterpret_cast<const uint4 *>(stage + saddr(16 * k + (lane >> 2), cj));
           if (BSSL_AMD_CHACHA_ABLATE == 8)
             asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
           else
@@ -1237,26 +1240,32 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
 // One wave group per wave.  (A persistent form -- 4 or 8 workgroups per CU
 // taking record groups from a grid-wide counter -- measured 7-8 % slower on
 // configs 3 and 3x, profiles/r03/s10/.)
-template <bool OPEN, int L, bool XT, bool XC, bool IOV>
+template <bool OPEN, int L, bool XT, bool XC, bool IOV, bool COAL>
 __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
     const ChaChaKeyDev *__restrict__ keys, BatchDesc b) {
-  chacha_group<OPEN, L, XT, XC, IOV>(keys, b,
+  chacha_group<OPEN, L, XT, XC, IOV, COAL>(keys, b,
                                 (uint64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6));
 }
 
-template <int L, bool OPEN, bool XT, bool XC, bool IOV = false>
+template <bool OPEN, bool XT, bool XC, bool IOV, bool COAL>
 void launch_one(const ChaChaKeyDev *keys, const BatchDesc &b, hipStream_t s) {
+  constexpr int L = BSSL_AMD_CHACHA_LANES;
   const uint64_t blocks = (b.num_records * L + kThreads - 1) / kThreads;
-  hipLaunchKernelGGL((chacha_poly_kernel<OPEN, L, XT, XC, IOV>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((chacha_poly_kernel<OPEN, L, XT, XC, IOV, COAL>), dim3((unsigned)blocks),
                      dim3(kThreads), 0, s, keys, b);
 }
 
-// ChaCha20-Poly1305 batches take 4 lanes per record (the record-contiguous
-// LDS-DMA I/O, whole 128-byte lines with the slot shift) only when every
-// record sits on a 128-byte boundary -- a uniform layout with a 128-byte
-// multiple stride -- and 2 lanes per record otherwise: config 3 at 128-byte
-// alignment 1,085-1,092 (4 lanes) vs 1,076 GiB/s (2 lanes), at 16-byte
-// alignment 1,021-1,032 vs 1,066-1,080 (same box, profiles/r03/s11/).
+template <bool XT, bool XC, bool IOV, bool COAL>
+void launch_dir(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, hipStream_t s) {
+  open ? launch_one<true, XT, XC, IOV, COAL>(keys, b, s)
+       : launch_one<false, XT, XC, IOV, COAL>(keys, b, s);
+}
+
+// The record-contiguous I/O with the slot shift moves whole 128-byte lines
+// only when every record starts one: a uniform layout with a 128-byte
+// multiple stride and 128-byte-aligned buffers.  Otherwise each lane moves
+// its own 64-byte block: config 3 at 16-byte alignment 1,059-1,069 GiB/s that
+// way against 939-952 with the record-contiguous I/O (profiles/r03/s13/).
 bool whole_lines(const BatchDesc &b) {
   return !b.offsets && b.record_stride % 128 == 0 &&
          ((reinterpret_cast<uintptr_t>(b.in) | reinterpret_cast<uintptr_t>(b.out)) & 127) == 0;
@@ -1268,7 +1277,7 @@ int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, bool 
                   void *stream, const KernelEvents *ev) {
   if (b.num_records == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if ((b.num_records * 4 + kThreads - 1) / kThreads > 0x7fffffffu) return 1;
+  if ((b.num_records * BSSL_AMD_CHACHA_LANES + kThreads - 1) / kThreads > 0x7fffffffu) return 1;
   BatchDesc bo = b;  // with the processing order of a ragged batch
   uint32_t *order = nullptr;
   if (wants_length_order(b)) {
@@ -1283,36 +1292,24 @@ int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, bool 
     bo.order = order;
   }
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
-  const bool xt = b.extra_len != 0;
-  constexpr int LX = BSSL_AMD_XCHACHA_L, LI = BSSL_AMD_CHACHA_IOV_L;
+  const bool xt = b.extra_len != 0, coal = whole_lines(b);
   if (b.iovecs) {  // iovec records walked in place (never with extra bytes)
-    if (xchacha)
-      open ? launch_one<LX, true, false, true, true>(keys, bo, s)
-           : launch_one<LX, false, false, true, true>(keys, bo, s);
-    else
-      open ? launch_one<LI, true, false, false, true>(keys, bo, s)
-           : launch_one<LI, false, false, false, true>(keys, bo, s);
+    xchacha ? launch_dir<false, true, true, false>(keys, bo, open, s)
+            : launch_dir<false, false, true, false>(keys, bo, open, s);
   } else if (xchacha) {
-    if (open)
-      xt ? launch_one<LX, true, true, true>(keys, bo, s)
-         : launch_one<LX, true, false, true>(keys, bo, s);
+    if (xt)
+      coal ? launch_dir<true, true, false, true>(keys, bo, open, s)
+           : launch_dir<true, true, false, false>(keys, bo, open, s);
     else
-      xt ? launch_one<LX, false, true, true>(keys, bo, s)
-         : launch_one<LX, false, false, true>(keys, bo, s);
-  } else if (whole_lines(b)) {
-    if (open)
-      xt ? launch_one<4, true, true, false>(keys, bo, s)
-         : launch_one<4, true, false, false>(keys, bo, s);
-    else
-      xt ? launch_one<4, false, true, false>(keys, bo, s)
-         : launch_one<4, false, false, false>(keys, bo, s);
+      coal ? launch_dir<false, true, false, true>(keys, bo, open, s)
+           : launch_dir<false, true, false, false>(keys, bo, open, s);
   } else {
-    if (open)
-      xt ? launch_one<2, true, true, false>(keys, bo, s)
-         : launch_one<2, true, false, false>(keys, bo, s);
+    if (xt)
+      coal ? launch_dir<true, false, false, true>(keys, bo, open, s)
+           : launch_dir<true, false, false, false>(keys, bo, open, s);
     else
-      xt ? launch_one<2, false, true, false>(keys, bo, s)
-         : launch_one<2, false, false, false>(keys, bo, s);
+      coal ? launch_dir<false, false, false, true>(keys, bo, open, s)
+           : launch_dir<false, false, false, false>(keys, bo, open, s);
   }
   const int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
