@@ -491,8 +491,9 @@ __device__ __forceinline__ T meta_load(const T *arr, uint64_t i, bool active) {
 // One wave group: records pos = grp * (64 / L) + lane / L.
 // IOV: iovec records walked in place (BatchDesc::iovecs; no extra bytes).
 // COAL: the record-contiguous I/O (launch_chacha picks it for batches whose
-// records all start 128-byte lines).
-template <bool OPEN, int L, bool XT, bool XC, bool IOV, bool COAL>
+// records all start 128-byte lines).  ANY: per-lane block I/O at any record
+// alignment (uniform batches that are not 16-byte aligned; no extra bytes).
+template <bool OPEN, int L, bool XT, bool XC, bool IOV, bool COAL, bool ANY>
 __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ keys,
                                              const BatchDesc &b, uint64_t grp) {
 #if BSSL_AMD_CHACHA_STAMPS
@@ -715,6 +716,14 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
       }
       return;
     }
+    if constexpr (ANY) {
+      // (Any alignment: one dwordx4 per 16 bytes, iov_dev.h load16_any.)
+      if (u >= 1 + sh && d < nblk && m.len >= 64 * d + 64) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) pre[i] = load16_any(src + 64 * d + 16 * i);
+      }
+      return;
+    }
     if (u >= 1 + sh && d < nblk && aligned && m.len >= 64 * d + 64) {
 #if BSSL_AMD_CHACHA_ABLATE == 1
       if (u >= (uint64_t)L) {
@@ -843,6 +852,46 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
       for (int i = 0; i < 4; i++)
         *reinterpret_cast<uint4 *>(my + ((i + (lane & 3) + (lane >> 2)) & 3) * 16) =
             make_uint4(y[4 * i], y[4 * i + 1], y[4 * i + 2], y[4 * i + 3]);
+    } else if constexpr (ANY) {
+      static_assert(!XT && !COAL && !IOV, "ANY kernels: plain per-lane records");
+      uint8_t *dp = dst + 64 * d;
+      const uint32_t n = (uint32_t)min<uint64_t>(rem, 64);
+      if (n == 64) {
+        // A full block at any alignment (one dwordx4 per 16 bytes).
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const uint4 v = pre[i];
+          x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) y[i] = x[i] ^ ks[i];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          store16_any(dp + 16 * i, make_uint4(y[4 * i], y[4 * i + 1], y[4 * i + 2], y[4 * i + 3]));
+      } else {
+        // The last, partial block: dword loads funnel-shifted to any
+        // alignment; 16-byte, dword or byte stores by the destination's
+        // alignment (store_partial).
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t nk = n > 16u * k ? min(n - 16u * k, 16u) : 0u;
+          load16_partial(src + 64 * d + 16 * k, nk, x + 4 * k);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+          const uint32_t mask = n >= 4u * i + 4 ? 0xffffffffu
+                                : n <= 4u * i   ? 0u
+                                                : ((1u << (8 * (n - 4 * i))) - 1u);
+          y[i] = (x[i] ^ ks[i]) & mask;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t nk = n > 16u * k ? min(n - 16u * k, 16u) : 0u;
+          if (nk)
+            store_partial(dp + 16 * k,
+                          make_uint4(y[4 * k], y[4 * k + 1], y[4 * k + 2], y[4 * k + 3]), nk);
+        }
+      }
     } else if (m.len >= 64 * d + 64 && aligned) {
       uint4 *dp = reinterpret_cast<uint4 *>(dst + 64 * d);
 #pragma unroll
@@ -1240,25 +1289,36 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
 // One wave group per wave.  (A persistent form -- 4 or 8 workgroups per CU
 // taking record groups from a grid-wide counter -- measured 7-8 % slower on
 // configs 3 and 3x, profiles/r03/s10/.)
-template <bool OPEN, int L, bool XT, bool XC, bool IOV, bool COAL>
+template <bool OPEN, int L, bool XT, bool XC, bool IOV, bool COAL, bool ANY>
 __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
     const ChaChaKeyDev *__restrict__ keys, BatchDesc b) {
-  chacha_group<OPEN, L, XT, XC, IOV, COAL>(keys, b,
+  chacha_group<OPEN, L, XT, XC, IOV, COAL, ANY>(keys, b,
                                 (uint64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6));
 }
 
-template <bool OPEN, bool XT, bool XC, bool IOV, bool COAL>
+template <bool OPEN, bool XT, bool XC, bool IOV, bool COAL, bool ANY>
 void launch_one(const ChaChaKeyDev *keys, const BatchDesc &b, hipStream_t s) {
   constexpr int L = BSSL_AMD_CHACHA_LANES;
   const uint64_t blocks = (b.num_records * L + kThreads - 1) / kThreads;
-  hipLaunchKernelGGL((chacha_poly_kernel<OPEN, L, XT, XC, IOV, COAL>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((chacha_poly_kernel<OPEN, L, XT, XC, IOV, COAL, ANY>), dim3((unsigned)blocks),
                      dim3(kThreads), 0, s, keys, b);
 }
 
-template <bool XT, bool XC, bool IOV, bool COAL>
+template <bool XT, bool XC, bool IOV, bool COAL, bool ANY = false>
 void launch_dir(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, hipStream_t s) {
-  open ? launch_one<true, XT, XC, IOV, COAL>(keys, b, s)
-       : launch_one<false, XT, XC, IOV, COAL>(keys, b, s);
+  open ? launch_one<true, XT, XC, IOV, COAL, ANY>(keys, b, s)
+       : launch_one<false, XT, XC, IOV, COAL, ANY>(keys, b, s);
+}
+
+// Uniform batches whose records are not 16-byte aligned take the ANY kernels
+// (one dwordx4 per 16 bytes at any address): 1350-byte records at a
+// 1351-byte stride 994 against 158 GiB/s through the aligned kernels' byte
+// path (profiles/r03/s16/).  Ragged batches keep the aligned kernels (an
+// unaligned record there takes the byte path).
+bool unaligned_uniform(const BatchDesc &b) {
+  return !b.offsets &&
+         ((reinterpret_cast<uintptr_t>(b.in) | reinterpret_cast<uintptr_t>(b.out) |
+           b.record_stride) & 15) != 0;
 }
 
 // The record-contiguous I/O with the slot shift moves whole 128-byte lines
@@ -1296,6 +1356,9 @@ int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, bool 
   if (b.iovecs) {  // iovec records walked in place (never with extra bytes)
     xchacha ? launch_dir<false, true, true, false>(keys, bo, open, s)
             : launch_dir<false, false, true, false>(keys, bo, open, s);
+  } else if (!xt && unaligned_uniform(b)) {
+    xchacha ? launch_dir<false, true, false, false, true>(keys, bo, open, s)
+            : launch_dir<false, false, false, false, true>(keys, bo, open, s);
   } else if (xchacha) {
     if (xt)
       coal ? launch_dir<true, true, false, true>(keys, bo, open, s)

@@ -85,11 +85,13 @@ def _uniform_case(aead, n, rlen, stride, ad_len, seed):
 
 @pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm", "chacha20-poly1305",
                                   "xchacha20-poly1305", "aes-128-gcm-siv", "aes-256-gcm-siv"])
-@pytest.mark.parametrize("rlen,stride", [(16384, 16384), (1350, 1408), (1408, 1408)])
+@pytest.mark.parametrize("rlen,stride", [(16384, 16384), (1350, 1408), (1408, 1408), (1350, 1351)])
 @pytest.mark.parametrize("n,ad_len", [(64, 40), (1000, 13), (4096, 13)])
 def test_uniform_batch_vs_oracle(aead, rlen, stride, n, ad_len):
-    """Uniform layout, 128-byte-aligned records, multi-record batches: every
-    ciphertext and tag equals the oracle's; then open in place."""
+    """Uniform layout, multi-record batches -- 128-byte-aligned records (the
+    bench's whole-line layout) and, at a 1351-byte stride, records at every
+    byte alignment (ChaCha's ANY kernels): every ciphertext and tag equals the
+    oracle's; then open in place."""
     key, nl, base, pt, recs, nonces, ad = _uniform_case(aead, n, rlen, stride, ad_len,
                                                         zlib.crc32(repr((aead, rlen, n, ad_len)).encode()))
     d_pt = torch.from_numpy(pt).to(DEV)
