@@ -22,4 +22,4 @@ for c in config3 config3x config4 config5 configS; do step bench_$c 600 python b
 step bench_config2_open 300 python bench.py --op open --no-cpu-baseline
 step bench_config3_open 300 python bench.py --config config3 --op open --no-cpu-baseline
 step rehearse2 600 env BSSL_AMD_REHEARSE_DEVICES=1 python bench.py --gpus 2 --no-cpu-baseline
-O=$O/prof CONFIGS="config2 config3 config4 config5 configS" PASSES="stats pmc" bash tools/profile.sh
+O=$O/prof CONFIGS="config2 config3 config3x config4 config5 configS" PASSES="stats pmc" bash tools/profile.sh
