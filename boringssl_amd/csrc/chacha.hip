@@ -431,7 +431,10 @@ __device__ __forceinline__ void crypt_block_x(const uint8_t *src, uint8_t *dst, 
 #define BSSL_AMD_CHACHA_WPE 4
 #endif
 #if BSSL_AMD_CHACHA_WPE
-#define CHACHA_OCC __attribute__((amdgpu_waves_per_eu(L == 2 ? 3 : BSSL_AMD_CHACHA_WPE)))
+#ifndef BSSL_AMD_CHACHA_WPE2
+#define BSSL_AMD_CHACHA_WPE2 3
+#endif
+#define CHACHA_OCC __attribute__((amdgpu_waves_per_eu(L == 2 ? BSSL_AMD_CHACHA_WPE2 : BSSL_AMD_CHACHA_WPE)))
 #else
 #define CHACHA_OCC
 #endif
