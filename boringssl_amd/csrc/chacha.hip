@@ -430,6 +430,11 @@ __device__ __forceinline__ void crypt_block_x(const uint8_t *src, uint8_t *dst, 
 #ifndef BSSL_AMD_CHACHA_WPE
 #define BSSL_AMD_CHACHA_WPE 4
 #endif
+// iovec records: the lane's whole block comes by LDS-DMA into the wave's
+// staging area (1) or by four dwordx4 loads held in VGPRs across the rounds (0).
+#ifndef BSSL_AMD_CHACHA_IOV_DMA
+#define BSSL_AMD_CHACHA_IOV_DMA 1
+#endif
 #if BSSL_AMD_CHACHA_WPE
 #ifndef BSSL_AMD_CHACHA_WPE2
 #define BSSL_AMD_CHACHA_WPE2 3
@@ -707,6 +712,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
           }
         }
         if (gp) {
+#if BSSL_AMD_CHACHA_IOV_DMA
 #pragma unroll
           for (int i = 0; i < 4; i++)
             __builtin_amdgcn_global_load_lds(
@@ -714,6 +720,10 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
                 reinterpret_cast<__attribute__((address_space(3))) void *>(
                     reinterpret_cast<uintptr_t>(stage + 1024 * i)),
                 16, 0, 0);
+#else
+#pragma unroll
+          for (int i = 0; i < 4; i++) pre[i] = load16_any(gp + 16 * i);
+#endif
           pre_ok = true;
         }
       }
@@ -754,7 +764,11 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
         // Whole block from the LDS-DMA staging (the caller waited for it).
 #pragma unroll
         for (int i = 0; i < 4; i++) {
+#if BSSL_AMD_CHACHA_IOV_DMA
           const uint4 v = *reinterpret_cast<const uint4 *>(my + 1024 * i);
+#else
+          const uint4 v = pre[i];
+#endif
           x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
         }
 #pragma unroll

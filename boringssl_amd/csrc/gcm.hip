@@ -760,12 +760,16 @@ template <bool OPEN, int L>
 __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const RecordMeta &m,
                                               const RecState &s, const BatchDesc &b, uint64_t rec,
                                               bool active, bool live, uint8_t *dst,
-                                              const GcmKeyDev *key) {
+                                              const uint32_t (*hp)[4]) {
   static_assert(L == 16, "lanes per record");
   const int q = threadIdx.x & (L - 1);
   const int r = (int)((nb + 1) & (L - 1));
   const int p = (q - r + 1) & (L - 1);
-  Gf128 z = gf_mul(to_gf(acc), gf_load(key->hpow_ct[L - p]));
+#if BSSL_AMD_ABLATE == 9  // diagnostic: no record-end products (wrong tags)
+  Gf128 z = gf_xor(to_gf(acc), gf_load(hp[L - p]));
+#else
+  Gf128 z = gf_mul(to_gf(acc), gf_load(hp[L - p]));
+#endif
 #pragma unroll
   for (int o = L / 2; o >= 1; o >>= 1)
 #pragma unroll
@@ -776,7 +780,9 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
   z.w[1] ^= (uint32_t)(cbits >> 32);
   z.w[2] ^= (uint32_t)abits;
   z.w[3] ^= (uint32_t)(abits >> 32);
-  z = gf_mul(z, gf_load(key->hpow_ct[1]));
+#if BSSL_AMD_ABLATE != 9
+  z = gf_mul(z, gf_load(hp[1]));
+#endif
   const uint4 tag = xor4(from_gf(z), s.ek0);
 
   uint8_t *tagp = batch_tag(b, rec);
@@ -1130,8 +1136,12 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
 #endif
 #if BSSL_AMD_GCM_STAMPS
   g_stamp_loop += stamp() - sl0;
+  const uint64_t tf0 = stamp();
 #endif
-  finish_record<OPEN, L>(acc, nb, m, s, b, rec, active, live, dst, key);
+  finish_record<OPEN, L>(acc, nb, m, s, b, rec, active, live, dst, key->hpow_ct);
+#if BSSL_AMD_GCM_STAMPS
+  stv[5] += stamp() - tf0;
+#endif
 }
 
 // Byte table of H^16 from the key's nibble tables (power 4): entry (e, p) =
@@ -1209,6 +1219,9 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
 #pragma unroll
       for (int c = 0; c < 4; c++) rk.w[r][c] = keys[0].rk[r][c];
     for (;;) {
+#if BSSL_AMD_GCM_STAMPS
+      const uint64_t tu0 = stamp();
+#endif
       uint32_t u = 0;
       if (lane == 0) u = atomicAdd(units, 1u);
       u = __builtin_amdgcn_readfirstlane(__shfl(u, 0, 64));
@@ -1218,12 +1231,19 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
       const bool active = i < n;
       process_records<NR, OPEN, XT, 16, false, IOV>(rk, b, st, active ? rec_at(b, i) : 0, active,
                                                     smem, keys, lc0, lc1, stamps);
+#if BSSL_AMD_GCM_STAMPS
+      stamps.v[3]++;
+      stamps.v[4] += stamp() - tu0;
+#endif
     }
 #if BSSL_AMD_GCM_STAMPS
     if (blockIdx.x < 2 && (tid & 63) == 0)
-      printf("stamps block %d wave %d: iters %llu  cycles/iter %.0f  rounds3..NR/iter %.0f\n",
-             (int)blockIdx.x, wave, (unsigned long long)stamps.v[1],
-             (double)stamps.v[2] / (double)stamps.v[1], (double)stamps.v[0] / (double)stamps.v[1]);
+      printf("stamps block %d wave %d: units %llu iters %llu  cycles/iter %.0f  rounds3..NR/iter "
+             "%.0f  cycles/unit %.0f (loop %.0f finish %.0f)\n",
+             (int)blockIdx.x, wave, (unsigned long long)stamps.v[3],
+             (unsigned long long)stamps.v[1], (double)stamps.v[2] / (double)stamps.v[1],
+             (double)stamps.v[0] / (double)stamps.v[1], (double)stamps.v[4] / stamps.v[3],
+             (double)stamps.v[2] / stamps.v[3], (double)stamps.v[5] / stamps.v[3]);
 #endif
     return;
   }
@@ -1490,7 +1510,7 @@ __device__ __forceinline__ void process_records_bs16(const uint32_t *__restrict_
     m = record_meta(b, rr);
     s = st[rr];
   }
-  finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, key);
+  finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, key->hpow_ct);
 }
 
 // Table-free one-key kernel (BSSL_AMD_GCM_MODE=bs16): 16 waves per CU at 128

@@ -33,6 +33,8 @@ def main():
                     help="bytes between input records (1: record starts at every alignment)")
     ap.add_argument("--out-gap", type=int, default=1, help="the same for the outputs")
     ap.add_argument("--cut1", type=int, default=5, help="length of each record's first chunk")
+    ap.add_argument("--cut2", type=int, default=-1,
+                    help="start of each record's third chunk (default: half the record)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(0)
@@ -48,7 +50,8 @@ def main():
     bin_ = torch.arange(n, dtype=torch.int64, device=dev) * sin
     bout = torch.arange(n, dtype=torch.int64, device=dev) * sout
     cut1 = torch.full((n,), min(a.cut1, L), dtype=torch.int64, device=dev)
-    cut2 = torch.full((n,), max(min(a.cut1, L), L // 2), dtype=torch.int64, device=dev)
+    c2 = L // 2 if a.cut2 < 0 else min(a.cut2, L)
+    cut2 = torch.full((n,), max(min(a.cut1, L), c2), dtype=torch.int64, device=dev)
     offs = torch.stack([torch.zeros_like(cut1), cut1, cut2], 1)       # chunk start in record
     lens = torch.stack([cut1, cut2 - cut1, L - cut2], 1)              # chunk length
     iov = torch.stack([dst.data_ptr() + bout[:, None] + offs,
@@ -88,7 +91,7 @@ def main():
         dt = (time.perf_counter() - t0) / a.steps
         res[name] = {"ms_per_batch": round(dt * 1e3, 3), "gib_per_s": round(n * L / dt / 2**30, 2)}
     print(json.dumps({"aead": a.aead, "records": n, "record_bytes": L, "in_gap": a.in_gap,
-                      "out_gap": a.out_gap, "cut1": a.cut1, "chunks_per_record": 3, **res}))
+                      "out_gap": a.out_gap, "cut1": a.cut1, "cut2": int(cut2[0]), "chunks_per_record": 3, **res}))
 
 
 if __name__ == "__main__":
