@@ -167,6 +167,8 @@ DIGESTS = [
     ("config2_aes128_16k", "aes-128-gcm", 1, 1048576, "16384"),
     ("config3_chacha_1350", "chacha20-poly1305", 1, 1048576, "1350"),
     ("config3x_xchacha_1350", "xchacha20-poly1305", 1, 1048576, "1350"),
+    # bench.py --config configG (AES-128-GCM on config 3's records; round 3)
+    ("configG_aes128_1350", "aes-128-gcm", 1, 1048576, "1350"),
     ("configs_siv128_16k", "aes-128-gcm-siv", 1, 262144, "16384"),
     # bench.py --config configS's own batch (1M records; round 3)
     ("configS_siv128_16k_1m", "aes-128-gcm-siv", 1, 1048576, "16384"),
