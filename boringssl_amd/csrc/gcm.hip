@@ -492,6 +492,46 @@ __device__ __forceinline__ int wave_max(int v) {
   return v;
 }
 
+// BSSL_AMD_GCM_DPP=1: the per-record reductions of the bulk kernel without
+// LDS shuffles (ds_bpermute goes through the LDS queue, which the AES and
+// GHASH lookups of the other waves keep ~84 % busy, and its lane-index
+// operands were spilled and reloaded once per unit).
+#ifndef BSSL_AMD_GCM_DPP
+#define BSSL_AMD_GCM_DPP 1
+#endif
+
+// Maximum over the wave of a value that is uniform within each L-lane group
+// (a record's iteration count): one readlane per group.
+template <int L>
+__device__ __forceinline__ int group_max(int v) {
+#if BSSL_AMD_GCM_DPP
+  int m = __builtin_amdgcn_readlane(v, 0);
+#pragma unroll
+  for (int k = 1; k < 64 / L; k++) m = max(m, __builtin_amdgcn_readlane(v, k * L));
+  return m;
+#else
+  return wave_max(v);
+#endif
+}
+
+// XOR of a word over the 16 lanes of its row, in every lane of the row:
+// rotations by 8 and 4 within the row, then the quad permutations 1032 and
+// 2301 (DPP row_ror / quad_perm; XOR is commutative, so rotations reduce as
+// well as butterflies do).
+__device__ __forceinline__ uint32_t row_xor16(uint32_t v) {
+#if BSSL_AMD_GCM_DPP
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false);  // row_ror:4
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false);   // quad 2301
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false);   // quad 1032
+  return v;
+#else
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) v ^= __shfl_xor(v, o, 16);
+  return v;
+#endif
+}
+
 // len = the record's `in` bytes; xlen = extra bytes sealed after them
 // (BatchDesc::extra), so the message is len + xlen bytes.
 struct RecordMeta {
@@ -771,9 +811,7 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
   Gf128 z = gf_mul(to_gf(acc), gf_load(hp[L - p]));
 #endif
 #pragma unroll
-  for (int o = L / 2; o >= 1; o >>= 1)
-#pragma unroll
-    for (int i = 0; i < 4; i++) z.w[i] ^= __shfl_xor(z.w[i], o, L);
+  for (int i = 0; i < 4; i++) z.w[i] = row_xor16(z.w[i]);
   // Length block be64(AD bits) || be64(message bits) in the reversed domain.
   const uint64_t abits = m.ad_len << 3, cbits = (m.len + m.xlen) << 3;
   z.w[0] ^= (uint32_t)cbits;
@@ -801,7 +839,7 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
       if (b.status) b.status[rec] = ok ? 1 : 0;
     }
   }
-  ok = __shfl(ok, 0, L);
+  if (OPEN) ok = __shfl(ok, 0, L);  // (seal: ok = live, the same in every lane)
   // Zero the output of a failed record (aead.cc.inc:132-139, 539-547; an
   // iovec record's chunks, clear_iovec, :310-333).
   if (active && !ok) {
@@ -884,7 +922,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   const uint32_t k0 = tload<T>(smem, taddr<0>(lc0, c0)) ^ tload<T>(smem, taddr<1>(lc1, c1)) ^
                       rotl(tload<T>(smem, taddr<2>(lc0, c2)) ^ rk.w[1][0], 16);
   WindowCache wc;
-  const int iters = wave_max((int)((nb + L - 1) / L));
+  const int iters = group_max<L>((int)((nb + L - 1) / L));
   // Full 16-byte blocks of this lane's record, at any alignment (one
   // dwordx4 each, load_blk_nt); the partial last block takes the byte path.
   // (iovec records: their own paths below.)
