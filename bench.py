@@ -485,24 +485,41 @@ def build_workload(config, rank, world, records, dev, open_op=False):
     return w
 
 
+def shard_key(aead, length, first, n, rpk):
+    """Identity of a reference digest of records [first, first + n) of the
+    synthetic sequence (key i // rpk, rpk 0 = one key; tests/golden/
+    make_golden.py shard_key, oracle/ref/ref_tool.cc cmd_shard)."""
+    return f"{aead}/{length}/first={first}/n={n}/rpk={rpk}"
+
+
 def golden_entry(w):
-    """The reference digest entry (tests/golden/ref_digests.json) of the
-    rank's batch, or None: the batch must be the whole synthetic sequence of
-    some entry (same AEAD, key count, records per key, length), starting at
-    record 0."""
+    """The reference digest of the rank's batch, or None.  Any shard of any
+    rank: tests/golden/ref_shard_digests.json holds the reference library's
+    digest of every rank's records at N = 2, 4, 8 (matched by first record,
+    record count, records per key, length); tests/golden/ref_digests.json the
+    whole N = 1 workloads (first record 0)."""
+    length = CONFIGS[w.config][3]
+    rpk = RECORDS_PER_KEY.get(w.config, 0)
+    gdir = os.path.join(ROOT, "tests", "golden")
+    try:
+        with open(os.path.join(gdir, "ref_shard_digests.json")) as f:
+            shards = json.load(f)
+    except OSError:
+        shards = {}
+    key = shard_key(w.aead, length, w.shard.first, w.nrec, rpk)
+    if key in shards:
+        return key, shards[key]
     if w.shard.first != 0 or w.shard.key_first != 0:
         return None
-    path = os.path.join(ROOT, "tests", "golden", "ref_digests.json")
     try:
-        with open(path) as f:
+        with open(os.path.join(gdir, "ref_digests.json")) as f:
             golden = json.load(f)
     except OSError:
         return None
-    length = CONFIGS[w.config][3]
-    rpk = RECORDS_PER_KEY.get(w.config, w.nrec)
+    rpk_full = rpk or w.nrec
     for name, g in sorted(golden.items()):
         if (g["aead"] == w.aead and int(g["records"]) == w.nrec and int(g["nkeys"]) == w.nkeys
-                and int(g["records_per_key"]) == rpk and str(g["len"]) == str(length)):
+                and int(g["records_per_key"]) == rpk_full and str(g["len"]) == str(length)):
             return name, g
     return None
 
@@ -540,21 +557,44 @@ def device_digests(d_out, offs, lens, d_tags, uniform_stride=0, chunk=1024, thre
     return hashlib.sha256(tags).hexdigest(), hashlib.sha256(b"".join(parts)).hexdigest()
 
 
+PARITY_MISMATCH, PARITY_UNCHECKED, PARITY_OK = 0, 1, 2
+
+
 def verify_workload(w):
-    """Compare the rank's sealed batch with the reference digest: returns
-    "ref_digest_ok:<entry>" or "not_checked:<reason>"; raises SystemExit on a
-    mismatch (the measured output is wrong)."""
+    """Compare the rank's sealed batch with the reference library's digest of
+    the same records.  Returns (code, text): (PARITY_OK, "ref_digest_ok:<entry>"),
+    (PARITY_UNCHECKED, "not_checked:<reason>") or (PARITY_MISMATCH, "MISMATCH:...")
+    -- the caller reduces the codes over ranks and fails the run on a mismatch."""
     ge = golden_entry(w)
     if ge is None:
-        return "not_checked:no reference digest for this shard"
+        return PARITY_UNCHECKED, "not_checked:no reference digest for this shard"
     name, g = ge
     tags_d, ct_d = device_digests(w.d_ct, w.offs, w.lens, w.d_tags,
                                   uniform_stride=w.stride if w.uniform else 0)
     if tags_d != g["tags_sha256"] or ct_d != g["ct_sha256"]:
-        raise SystemExit(f"bench.py: sealed output differs from the reference digest {name} "
-                         f"(tags {tags_d[:16]} vs {g['tags_sha256'][:16]}, "
-                         f"ct {ct_d[:16]} vs {g['ct_sha256'][:16]})")
-    return f"ref_digest_ok:{name}"
+        return PARITY_MISMATCH, (f"MISMATCH:{name} (tags {tags_d[:16]} vs "
+                                 f"{g['tags_sha256'][:16]}, ct {ct_d[:16]} vs {g['ct_sha256'][:16]})")
+    return PARITY_OK, f"ref_digest_ok:{name}"
+
+
+def reduce_parity(code, text, world, rank):
+    """All ranks' parity results: (min code over ranks, summary string, per-rank
+    list).  "ref_digest_ok:all_ranks" when every rank's shard matched the
+    reference digest (per-GPU digests, combined on the host in
+    rank order)."""
+    if world == 1:
+        return code, text, [text]
+    texts = [None] * world
+    _dist().all_gather_object(texts, f"rank {rank}: {text}")
+    worst = int(round(_reduce(float(code), world, _dist().ReduceOp.MIN)))
+    if worst == PARITY_OK:
+        summary = f"ref_digest_ok:all_ranks({world})"
+    elif worst == PARITY_UNCHECKED:
+        n_un = sum(1 for t in texts if "not_checked" in t)
+        summary = f"not_checked:{n_un}_of_{world}_ranks"
+    else:
+        summary = "MISMATCH:" + "; ".join(t for t in texts if "MISMATCH" in t)
+    return worst, summary, texts
 
 
 def plan_only(args, world, rank):
@@ -662,10 +702,15 @@ def main():
         raise SystemExit(f"{args.op} reported failed records")
     if args.op == "open" and not torch.equal(wl.d_back, wl.d_pt):
         raise SystemExit("open did not return the plaintext")
-    # Bit-exact check of the timed output (seal): the digest of the sealed
-    # records and tags against the reference library's digest of the same
-    # synthetic batch (tests/golden/ref_digests.json), where one exists.
-    parity = verify_workload(wl) if args.op == "seal" and not args.no_parity else "not_checked"
+    # Bit-exact check of the timed output (seal), on every rank: the digest of
+    # the rank's sealed records and tags against the reference library's
+    # digest of the same records (tests/golden/ref_shard_digests.json,
+    # ref_digests.json); reduced over ranks below.
+    if args.op == "seal" and not args.no_parity:
+        p_code, p_text = verify_workload(wl)
+    else:
+        p_code, p_text = PARITY_UNCHECKED, "not_checked"
+    p_code, parity, parity_ranks = reduce_parity(p_code, p_text, world, rank)
     assert len(kernel_ms) == args.steps, kernel_ms
     avg_kernel_ms = float(np.mean(kernel_ms))
     kname = ba.last_kernel_name()
@@ -700,6 +745,7 @@ def main():
                    "plaintext_bytes_all_ranks": int(total_bytes),
                    "parallelism": f"dp{world} (independent record shards, no collective)"},
         "parity": parity,
+        **({"parity_ranks": parity_ranks} if world > 1 else {}),
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "algorithmic_bytes_per_launch": algo_bytes,
@@ -712,6 +758,8 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if p_code == PARITY_MISMATCH:
+        raise SystemExit(f"bench.py: sealed output differs from the reference digest: {parity}")
 
 
 if __name__ == "__main__":

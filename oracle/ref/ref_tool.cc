@@ -10,6 +10,9 @@
 //   ref_tool digest AEAD NKEYS RPK LEN [T] batch digests over the synthetic
 //                                          workload (oracle/synth.h); LEN is a
 //                                          byte count or "mixed"
+//   ref_tool shard AEAD LEN FIRST N RPK [T]  digest of records [FIRST,
+//                                          FIRST+N) (one bench rank's shard;
+//                                          key i/RPK, RPK = 0: one key)
 //   ref_tool bench AEAD LEN NREC T SECS    CPU baseline: T threads seal a
 //                                          resident sample of NREC synthetic
 //                                          records for about SECS seconds
@@ -131,17 +134,18 @@ size_t make_nonce(uint64_t i, size_t nonce_len, uint8_t *out) {
   return nonce_len;
 }
 
-int cmd_digest(int argc, char **argv) {
-  if (argc < 6) return 2;
+// Digest of the records [first, first + n) of the synthetic sequence: record
+// i is sealed under key (rpk ? i / rpk : 0) with len (mixed ? synth_mixed_len(i)
+// : fixed_len), nonce make_nonce(i) and AD synth_ad(i, len) -- exactly what
+// rank r of `bench.py --gpus N` seals for its shard (bench.shard_plan), so a
+// shard's digest is defined independently of which process sealed it.  Chunks
+// of 1024 records count from `first`.
+int digest_range(const char *name, uint64_t first, uint64_t n, uint64_t rpk, const char *len_arg,
+                 int threads, const char *extra_json) {
   size_t key_len;
-  const char *name = argv[2];
   const EVP_AEAD *aead = aead_by_name(name, &key_len);
-  uint64_t nkeys = strtoull(argv[3], nullptr, 0);
-  uint64_t rpk = strtoull(argv[4], nullptr, 0);
-  bool mixed = std::string(argv[5]) == "mixed";
-  uint64_t fixed_len = mixed ? 0 : strtoull(argv[5], nullptr, 0);
-  int threads = argc > 6 ? atoi(argv[6]) : 8;
-  uint64_t n = nkeys * rpk;
+  bool mixed = std::string(len_arg) == "mixed";
+  uint64_t fixed_len = mixed ? 0 : strtoull(len_arg, nullptr, 0);
   const uint64_t kChunk = 1024;
   uint64_t nchunks = (n + kChunk - 1) / kChunk;
   std::vector<uint8_t> tags(n * 16);
@@ -157,8 +161,9 @@ int cmd_digest(int argc, char **argv) {
       SHA256_CTX sha;
       SHA256_Init(&sha);
       uint64_t lo = c * kChunk, hi = lo + kChunk < n ? lo + kChunk : n;
-      for (uint64_t i = lo; i < hi; i++) {
-        uint64_t k = i / rpk;
+      for (uint64_t j = lo; j < hi; j++) {
+        const uint64_t i = first + j;
+        uint64_t k = rpk ? i / rpk : 0;
         if (k != cur_key) {
           std::vector<uint8_t> key(key_len);
           synth_key(k, key_len, key.data());
@@ -174,7 +179,7 @@ int cmd_digest(int argc, char **argv) {
         const size_t nl = make_nonce(i, EVP_AEAD_nonce_length(aead), nonce);
         synth_ad(i, len, ad);
         size_t tag_out = 0;
-        if (!EVP_AEAD_CTX_seal_scatter(ctx.get(), ct.data(), &tags[16 * i], &tag_out, 16, nonce,
+        if (!EVP_AEAD_CTX_seal_scatter(ctx.get(), ct.data(), &tags[16 * j], &tag_out, 16, nonce,
                                        nl, pt.data(), len, nullptr, 0, ad, 13))
           abort();
         SHA256_Update(&sha, ct.data(), len);
@@ -186,13 +191,40 @@ int cmd_digest(int argc, char **argv) {
   uint8_t tags_d[32], ct_d[32];
   SHA256(tags.data(), tags.size(), tags_d);
   SHA256(chunk_digests.data(), chunk_digests.size(), ct_d);
-  printf("{\"aead\": \"%s\", \"nkeys\": %llu, \"records_per_key\": %llu, \"len\": \"%s\", "
-         "\"records\": %llu, \"bytes\": %llu, \"tags_sha256\": \"%s\", \"ct_sha256\": \"%s\", "
-         "\"tag_first\": \"%s\", \"tag_last\": \"%s\"}\n",
-         name, (unsigned long long)nkeys, (unsigned long long)rpk, argv[5],
-         (unsigned long long)n, (unsigned long long)total_bytes, hex(tags_d, 32).c_str(),
-         hex(ct_d, 32).c_str(), hex(&tags[0], 16).c_str(), hex(&tags[16 * (n - 1)], 16).c_str());
+  printf("{\"aead\": \"%s\", %s\"len\": \"%s\", \"records\": %llu, \"bytes\": %llu, "
+         "\"tags_sha256\": \"%s\", \"ct_sha256\": \"%s\", \"tag_first\": \"%s\", "
+         "\"tag_last\": \"%s\"}\n",
+         name, extra_json, len_arg, (unsigned long long)n, (unsigned long long)total_bytes,
+         hex(tags_d, 32).c_str(), hex(ct_d, 32).c_str(), n ? hex(&tags[0], 16).c_str() : "",
+         n ? hex(&tags[16 * (n - 1)], 16).c_str() : "");
   return 0;
+}
+
+// ref_tool digest AEAD NKEYS RPK LEN [T]: the whole sequence of NKEYS keys x
+// RPK records (records [0, NKEYS*RPK), key i / RPK).
+int cmd_digest(int argc, char **argv) {
+  if (argc < 6) return 2;
+  uint64_t nkeys = strtoull(argv[3], nullptr, 0);
+  uint64_t rpk = strtoull(argv[4], nullptr, 0);
+  int threads = argc > 6 ? atoi(argv[6]) : 8;
+  char extra[128];
+  snprintf(extra, sizeof extra, "\"nkeys\": %llu, \"records_per_key\": %llu, ",
+           (unsigned long long)nkeys, (unsigned long long)rpk);
+  return digest_range(argv[2], 0, nkeys * rpk, rpk, argv[5], threads, extra);
+}
+
+// ref_tool shard AEAD LEN FIRST N RPK [T]: records [FIRST, FIRST + N) of the
+// sequence, key i / RPK (RPK = 0: one key, key 0) -- one rank's shard.
+int cmd_shard(int argc, char **argv) {
+  if (argc < 7) return 2;
+  uint64_t first = strtoull(argv[4], nullptr, 0);
+  uint64_t n = strtoull(argv[5], nullptr, 0);
+  uint64_t rpk = strtoull(argv[6], nullptr, 0);
+  int threads = argc > 7 ? atoi(argv[7]) : 8;
+  char extra[160];
+  snprintf(extra, sizeof extra, "\"first\": %llu, \"records_per_key\": %llu, ",
+           (unsigned long long)first, (unsigned long long)rpk);
+  return digest_range(argv[2], first, n, rpk, argv[3], threads, extra);
 }
 
 int cmd_bench(int argc, char **argv) {
@@ -319,6 +351,7 @@ int main(int argc, char **argv) {
   std::string cmd = argv[1];
   if (cmd == "edge") return cmd_edge();
   if (cmd == "digest") return cmd_digest(argc, argv);
+  if (cmd == "shard") return cmd_shard(argc, argv);
   if (cmd == "bench") return cmd_bench(argc, argv);
   if (cmd == "bench1") return cmd_bench1(argc, argv);
   return 2;

@@ -25,8 +25,13 @@ reads the committed JSON.  Three kinds of fixture are produced:
 * ref_digests.json-- batch digests of the synthetic workloads of SURVEY.md
                      section 8(d) sealed by the reference library:
                      `oracle/_ref/ref_tool digest ...`.
+* ref_shard_digests.json -- the same digests for every rank's shard of
+                     `bench.py --gpus N` (N = 2, 4, 8; bench.shard_plan) of the
+                     bench configs: `oracle/_ref/ref_tool shard ...`, so every
+                     rank of a multi-GPU run is checked bit for bit (SURVEY.md
+                     8(e): per-GPU digests, combined in a fixed order).
 
-Usage: python tests/golden/make_golden.py [--skip-full]
+Usage: python tests/golden/make_golden.py [--skip-full] [--shards]
 """
 import argparse
 import json
@@ -182,7 +187,11 @@ def main():
     ap.add_argument("--skip-full", action="store_true")
     ap.add_argument("--only", default="", help="regenerate just this digest entry")
     ap.add_argument("--tls-only", action="store_true", help="regenerate ref_tls.json only")
+    ap.add_argument("--shards", action="store_true",
+                    help="(re)generate ref_shard_digests.json only")
     args = ap.parse_args()
+    if args.shards:
+        return shard_entries()
     if args.tls_only:
         return write_ref_tls()
     if args.only:
@@ -244,6 +253,78 @@ def digest_entries(want):
             [REF_TOOL, "digest", aead_name, str(nkeys), str(rpk), length, "8"]))
         digests[name] = res
         print(name, res["tags_sha256"][:16], res["ct_sha256"][:16], flush=True)
+        with open(path, "w") as f:
+            json.dump(digests, f, indent=1, sort_keys=True)
+
+
+# bench.py configs whose multi-GPU shards get reference digests, and the GPU
+# counts of the driver's scaling run.
+SHARD_CONFIGS = ["config2", "config3", "config3x", "configG", "configS", "config4", "config5"]
+SHARD_WORLDS = [2, 4, 8]
+
+
+def shard_key(aead, length, first, n, rpk):
+    """Identity of a shard digest: records [first, first + n) of the synthetic
+    sequence, key i // rpk (rpk 0: one key), lengths `length` or "mixed"."""
+    return f"{aead}/{length}/first={first}/n={n}/rpk={rpk}"
+
+
+def bench_shards():
+    """(key, aead, length, first, n, rpk, [(config, world, rank), ...]) for
+    every rank's shard of bench.py --gpus N, N in SHARD_WORLDS."""
+    sys.path.insert(0, ROOT)
+    import bench
+    shards = {}
+    for config in SHARD_CONFIGS:
+        aead, _, _, length, _, _ = bench.CONFIGS[config]
+        rpk = bench.RECORDS_PER_KEY.get(config, 0)
+        for world in SHARD_WORLDS:
+            for rank in range(world):
+                sh = bench.shard_plan(config, rank, world)
+                key = shard_key(aead, length, sh.first, sh.n, rpk)
+                ent = shards.setdefault(key, [key, aead, str(length), sh.first, sh.n, rpk, []])
+                ent[6].append((config, world, rank))
+    return list(shards.values())
+
+
+# Small shards at a non-zero first record (and key), checked against the CPU
+# oracle by tests/test_shard_digests.py: they pin the shard definition that
+# the multi-GPU digests above use.
+PIN_SHARDS = [
+    ("aes-128-gcm", "16384", 320, 192, 64),
+    ("aes-256-gcm", "mixed", 1000, 3000, 0),
+    ("chacha20-poly1305", "1350", 5000, 2048, 0),
+    ("xchacha20-poly1305", "1350", 7, 1500, 0),
+    ("aes-128-gcm-siv", "16384", 1100, 300, 0),
+]
+
+
+def shard_entries():
+    if not os.path.exists(REF_TOOL):
+        subprocess.check_call(["make", "-j8", "-C", os.path.join(ROOT, "oracle", "ref")])
+    path = os.path.join(HERE, "ref_shard_digests.json")
+    digests = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            digests = json.load(f)
+    for key, aead, length, first, n, rpk, users in bench_shards():
+        if key in digests:
+            continue
+        res = json.loads(subprocess.check_output(
+            [REF_TOOL, "shard", aead, length, str(first), str(n), str(rpk), "8"]))
+        res["used_by"] = [f"{c} N={w} rank {r}" for c, w, r in users]
+        digests[key] = res
+        print(key, res["tags_sha256"][:16], res["ct_sha256"][:16], flush=True)
+        with open(path, "w") as f:
+            json.dump(digests, f, indent=1, sort_keys=True)
+    for aead, length, first, n, rpk in PIN_SHARDS:
+        key = shard_key(aead, length, first, n, rpk)
+        if key in digests:
+            continue
+        res = json.loads(subprocess.check_output(
+            [REF_TOOL, "shard", aead, length, str(first), str(n), str(rpk), "8"]))
+        res["used_by"] = ["tests/test_shard_digests.py (oracle pin)"]
+        digests[key] = res
         with open(path, "w") as f:
             json.dump(digests, f, indent=1, sort_keys=True)
 

@@ -59,13 +59,34 @@ def test_bench_workload_full_size(config):
     if bench.CONFIGS[config][3] != "mixed":
         assert w.batch.offsets is None and w.batch.lengths is None  # uniform layout
         assert w.stride % 128 == 0
-    parity = bench.verify_workload(w)
-    assert parity.startswith("ref_digest_ok"), parity
+    code, parity = bench.verify_workload(w)
+    assert code == bench.PARITY_OK and parity.startswith("ref_digest_ok"), parity
     w.d_status.zero_()
     w.op(w.batch, torch.cuda.current_stream())
     torch.cuda.synchronize()
     assert bool(w.d_status[:w.nrec].all())
     assert torch.equal(w.d_back, w.d_pt)
+    del w
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("config,world,rank", [
+    ("config2", 2, 1), ("config2", 8, 7), ("config3", 8, 7), ("configG", 4, 3),
+    ("config4", 2, 1), ("config4", 8, 7), ("config5", 2, 1), ("config5", 8, 6)])
+def test_bench_shard_of_multi_gpu_run(config, world, rank):
+    """One rank's shard of `bench.py --gpus N`, built and sealed exactly as
+    that rank builds and seals it (bench.build_workload with rank/world), on
+    this one GPU: its digest equals the reference library's digest of the same
+    records (tests/golden/ref_shard_digests.json) -- the bit-exact check every
+    rank of a multi-GPU run performs (bench.verify_workload)."""
+    dev = torch.device(DEV)
+    w = bench.build_workload(config, rank, world, 0, dev)
+    assert w.shard.first > 0
+    w.op(w.batch, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert bool(w.d_status[:w.nrec].all())
+    code, parity = bench.verify_workload(w)
+    assert code == bench.PARITY_OK and "first=" in parity, parity
     del w
     torch.cuda.empty_cache()
 

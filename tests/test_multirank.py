@@ -151,3 +151,40 @@ def test_launcher_weak_config_per_gpu_shards():
     plan = sorted(r["plan"], key=lambda x: x["rank"])
     assert r["scaling"] == "weak"
     assert [(p["first"], p["n"]) for p in plan] == [(0, 1000), (1000, 1000)]
+
+
+def _parity_worker(rank, world, port, codes, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    code = codes[rank]
+    text = {bench.PARITY_OK: f"ref_digest_ok:shard{rank}",
+            bench.PARITY_UNCHECKED: "not_checked:none",
+            bench.PARITY_MISMATCH: f"MISMATCH:shard{rank}"}[code]
+    q.put((rank,) + bench.reduce_parity(code, text, world, rank))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("codes,expect", [
+    ((2, 2, 2), "ref_digest_ok:all_ranks(3)"),
+    ((2, 1, 2), "not_checked:1_of_3_ranks"),
+    ((2, 1, 0), "MISMATCH:rank 2: MISMATCH:shard2")])
+def test_parity_reduced_over_ranks(codes, expect):
+    """bench.py's per-rank digest results are reduced over all ranks: the line
+    says all_ranks only when every rank's shard matched its reference digest,
+    and any mismatch (on any rank) is reported and fails the run."""
+    world = len(codes)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_parity_worker, args=(r, world, port, codes, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, worst, summary, per_rank in res:
+        assert worst == min(codes) and summary == expect
+        assert len(per_rank) == world and per_rank[rank].startswith(f"rank {rank}:")
