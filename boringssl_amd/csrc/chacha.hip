@@ -33,30 +33,20 @@
 namespace bssl_amd {
 namespace {
 
-#ifndef BSSL_AMD_CHACHA_THREADS
-#define BSSL_AMD_CHACHA_THREADS 256
-#endif
-constexpr int kThreads = BSSL_AMD_CHACHA_THREADS;
+constexpr int kThreads = 256;
 // Wave priority during a record group's start-up (loads, first ChaCha
 // block): waves that start mid-kernel otherwise lose every issue arbitration
 // to older waves and sit 60-100 K cycles before their first block (stamps,
 // DESIGN.md 4.3).  Priority 2 for that phase: +2-5 % on config 3 (40-step
-// runs, 1,061/1,072 -> 1,122/1,092 GiB/s); 0 = off.
-#ifndef BSSL_AMD_CHACHA_PRIO
-#define BSSL_AMD_CHACHA_PRIO 2
-#endif
+// runs, 1,061/1,072 -> 1,122/1,092 GiB/s).
+constexpr int kStartPrio = 2;
 // Lanes per record (round 3: 2 for every AEAD and layout, 32 records per
 // wave, 3 waves per SIMD at ~150-170 VGPRs without spills).  Against 4 lanes
 // (128 VGPRs, 4 waves, 27-43 spills), same box (profiles/r03/s13/): config 3
 // at 128-byte alignment 1,192 vs 1,069-1,079 GiB/s, config3x 1,110-1,124 vs
 // 999; the per-record work (key block, powers of r, lane tree, tag; for
 // XChaCha one HChaCha20) is spread over twice the blocks per lane.
-#ifndef BSSL_AMD_CHACHA_LANES
-#define BSSL_AMD_CHACHA_LANES 2
-#endif
-#ifndef BSSL_AMD_CHACHA_UNROLL
-#define BSSL_AMD_CHACHA_UNROLL 10
-#endif
+constexpr int kLanes = 2;
 #define CHACHA_PRAGMA_(x) _Pragma(#x)
 #define CHACHA_PRAGMA(x) CHACHA_PRAGMA_(x)
 constexpr uint32_t kM26 = 0x3ffffff;
@@ -72,22 +62,8 @@ struct ChaState {
 // d = rotl(d ^ a, 16) as two SDWA XORs (one per 16-bit half, the halves
 // swapped) instead of an XOR and a v_alignbit_b32 (diagnostic knob; the
 // alignbit is one of the slow-issue VALU instructions).
-#ifndef BSSL_AMD_CHACHA_SDWA
-#define BSSL_AMD_CHACHA_SDWA 0
-#endif
 __device__ __forceinline__ uint32_t xor_rot16(uint32_t d, uint32_t a) {
-#if BSSL_AMD_CHACHA_SDWA
-  uint32_t t;
-  asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 "
-      "src1_sel:WORD_0\n\t"
-      "v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 "
-      "src1_sel:WORD_1"
-      : "=&v"(t)
-      : "v"(d), "v"(a));
-  return t;
-#else
   return rotl(d ^ a, 16);
-#endif
 }
 
 #define QR(a, b, c, d)                 \
@@ -113,7 +89,7 @@ __device__ __forceinline__ void chacha_block_raw(const uint32_t key[8], uint32_t
   uint32_t x4 = key[0], x5 = key[1], x6 = key[2], x7 = key[3];
   uint32_t x8 = key[4], x9 = key[5], x10 = key[6], x11 = key[7];
   uint32_t x12 = ctr, x13 = nonce[0], x14 = nonce[1], x15 = nonce[2];
-  CHACHA_PRAGMA(unroll BSSL_AMD_CHACHA_UNROLL)
+  CHACHA_PRAGMA(unroll 10)
   for (int i = 0; i < 10; i++) {
     QR(x0, x4, x8, x12) QR(x1, x5, x9, x13) QR(x2, x6, x10, x14) QR(x3, x7, x11, x15)
     QR(x0, x5, x10, x15) QR(x1, x6, x11, x12) QR(x2, x7, x8, x13) QR(x3, x4, x9, x14)
@@ -151,7 +127,7 @@ __device__ __forceinline__ void hchacha20(uint32_t key[8], const uint32_t n[4]) 
   uint32_t x4 = key[0], x5 = key[1], x6 = key[2], x7 = key[3];
   uint32_t x8 = key[4], x9 = key[5], x10 = key[6], x11 = key[7];
   uint32_t x12 = n[0], x13 = n[1], x14 = n[2], x15 = n[3];
-  CHACHA_PRAGMA(unroll BSSL_AMD_CHACHA_UNROLL)
+  CHACHA_PRAGMA(unroll 10)
   for (int i = 0; i < 10; i++) {
     QR(x0, x4, x8, x12) QR(x1, x5, x9, x13) QR(x2, x6, x10, x14) QR(x3, x7, x11, x15)
     QR(x0, x5, x10, x15) QR(x1, x6, x11, x12) QR(x2, x7, x8, x13) QR(x3, x4, x9, x14)
@@ -352,19 +328,6 @@ __device__ __forceinline__ void pmac_s(PAcc &acc, const P &a, const uint32_t *r,
               mul64(a.h[3], r[1]) + mul64(a.h[4], r[0]);
 }
 
-__device__ __forceinline__ void pmac(PAcc &acc, const P &a, const P &r) {
-  const uint32_t s1 = r.h[1] * 5, s2 = r.h[2] * 5, s3 = r.h[3] * 5, s4 = r.h[4] * 5;
-  acc.d[0] += mul64(a.h[0], r.h[0]) + mul64(a.h[1], s4) + mul64(a.h[2], s3) +
-              mul64(a.h[3], s2) + mul64(a.h[4], s1);
-  acc.d[1] += mul64(a.h[0], r.h[1]) + mul64(a.h[1], r.h[0]) + mul64(a.h[2], s4) +
-              mul64(a.h[3], s3) + mul64(a.h[4], s2);
-  acc.d[2] += mul64(a.h[0], r.h[2]) + mul64(a.h[1], r.h[1]) + mul64(a.h[2], r.h[0]) +
-              mul64(a.h[3], s4) + mul64(a.h[4], s3);
-  acc.d[3] += mul64(a.h[0], r.h[3]) + mul64(a.h[1], r.h[2]) + mul64(a.h[2], r.h[1]) +
-              mul64(a.h[3], r.h[0]) + mul64(a.h[4], s4);
-  acc.d[4] += mul64(a.h[0], r.h[4]) + mul64(a.h[1], r.h[3]) + mul64(a.h[2], r.h[2]) +
-              mul64(a.h[3], r.h[1]) + mul64(a.h[4], r.h[0]);
-}
 
 // Carry-propagate a lazy sum (at most 4 products of limbs < 2^27.1 and
 // powers < 2^26.01: every d_i < 2^60).
@@ -427,62 +390,23 @@ __device__ __forceinline__ void crypt_block_x(const uint8_t *src, uint8_t *dst, 
 // [Y_A, U_0, U_1, ...] of 4-block units, element v = u in lane u mod L, with
 // Horner's rule in R = r^4 at stride L (multiplier R^L), then the rotation +
 // log2(L)-level tree of gcm.hip's lane algebra.
-#ifndef BSSL_AMD_CHACHA_WPE
-#define BSSL_AMD_CHACHA_WPE 4
-#endif
 // iovec records: the lane's whole block comes by LDS-DMA into the wave's
 // staging area (1) or by four dwordx4 loads held in VGPRs across the rounds (0).
-#ifndef BSSL_AMD_CHACHA_IOV_DMA
-#define BSSL_AMD_CHACHA_IOV_DMA 1
-#endif
-#if BSSL_AMD_CHACHA_WPE
-#ifndef BSSL_AMD_CHACHA_WPE2
-#define BSSL_AMD_CHACHA_WPE2 3
-#endif
-#define CHACHA_OCC __attribute__((amdgpu_waves_per_eu(L == 2 ? BSSL_AMD_CHACHA_WPE2 : BSSL_AMD_CHACHA_WPE)))
-#else
-#define CHACHA_OCC
-#endif
+#define CHACHA_OCC __attribute__((amdgpu_waves_per_eu(L == 2 ? 3 : 4)))
 // Coalesced record I/O for L = 4 (default): a wave's loads and stores move
 // 256 contiguous bytes per record per instruction (lane = 16-byte chunk of a
 // record's 4-block run), staged through LDS to the lane that owns each
 // 64-byte block.  With the lane-per-block pattern (0) each 16-byte access
 // sits at a 64-byte lane stride: the same copy costs 1.32x the time and
 // 1.3x the counted HBM bytes (tools/micro/calib_copy.hip).
-#ifndef BSSL_AMD_CHACHA_COAL
-#define BSSL_AMD_CHACHA_COAL 1
-#endif
 // Slot shift for 128-byte-aligned records (see `sh` in chacha_group).
-#ifndef BSSL_AMD_CHACHA_SHIFT
-#define BSSL_AMD_CHACHA_SHIFT 1
-#endif
 // Ciphertext stores with the non-temporal hint: +2.3 % on config 3 (same-box
 // A/B); NT_LOAD sets the non-temporal cache policy on the LDS-DMA loads.
-#ifndef BSSL_AMD_CHACHA_NT_STORE
-#define BSSL_AMD_CHACHA_NT_STORE 1
-#endif
-#ifndef BSSL_AMD_CHACHA_NT_LOAD
-#define BSSL_AMD_CHACHA_NT_LOAD 0
-#endif
-#ifndef BSSL_AMD_CHACHA_META_BRANCH
-#define BSSL_AMD_CHACHA_META_BRANCH 0
-#endif
-#ifndef BSSL_AMD_CHACHA_STAMPS
-#define BSSL_AMD_CHACHA_STAMPS 0
-#endif
 // Diagnostic ablations (wrong output; selected builds only): 1 = no input
 // loads in the block loop, 2 = no Poly1305 absorb in the loop, 3 = no ChaCha
 // rounds in the loop, 4 = no stores in the loop (lane-per-block I/O); with
 // the record-contiguous I/O: 7 = no loads, 8 = no global stores in the loop
 // (the staged values are still read back).
-#ifndef BSSL_AMD_CHACHA_ABLATE
-#define BSSL_AMD_CHACHA_ABLATE 0
-#endif
-#if BSSL_AMD_CHACHA_STAMPS  // diagnostic build: per-phase cycles of sample waves
-#define CSTAMP(i) ts[i] = __builtin_amdgcn_s_memtime()
-#else
-#define CSTAMP(i)
-#endif
 // Per-record metadata without branches: a missing array (null pointer, the
 // uniform-layout fields apply) is read at kMetaZero instead, so every load is
 // issued unconditionally and they are all in flight together.  (Under the
@@ -504,11 +428,7 @@ __device__ __forceinline__ T meta_load(const T *arr, uint64_t i, bool active) {
 template <bool OPEN, int L, bool XT, bool XC, bool IOV, bool COAL, bool ANY>
 __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ keys,
                                              const BatchDesc &b, uint64_t grp) {
-#if BSSL_AMD_CHACHA_STAMPS
-  uint64_t ts[5] = {0, 0, 0, 0, 0};
-#endif
-  CSTAMP(0);
-  if (BSSL_AMD_CHACHA_PRIO) __builtin_amdgcn_s_setprio(BSSL_AMD_CHACHA_PRIO);
+  __builtin_amdgcn_s_setprio(kStartPrio);
   static_assert(L == 2 || L == 4 || L == 8 || L == 16, "lanes per record");
   static_assert(!(IOV && XT), "iovec records carry no extra bytes");
   constexpr int kLog = L == 2 ? 1 : L == 4 ? 2 : L == 8 ? 3 : 4;
@@ -516,19 +436,6 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   const int q = lane & (L - 1);
   const uint64_t pos = grp * (64 / L) + lane / L;
   const bool active = pos < b.num_records;
-#if BSSL_AMD_CHACHA_META_BRANCH  // (the round-1 form, for A/B)
-  const uint64_t rec = active && b.order ? b.order[pos] : pos;  // sched.hip order
-  RecordMeta m = {0, 0, 0, 0};
-  uint32_t kidx = 0;
-  if (active) {
-    m.off = b.offsets ? b.offsets[rec] : rec * b.record_stride;
-    m.len = b.lengths ? b.lengths[rec] : b.record_len;
-    m.ad_off = b.ad_offsets ? b.ad_offsets[rec] : rec * b.ad_stride;
-    m.ad_len = b.ad_lengths ? b.ad_lengths[rec] : b.ad_len;
-    kidx = b.key_index ? b.key_index[rec] : 0u;
-  }
-  const uint8_t vld = active && b.valid ? b.valid[rec] : 1;
-#else
   uint8_t vld = 1;
   const uint64_t rec = active && b.order ? (uint64_t)b.order[pos] : pos;  // sched.hip order
   RecordMeta m = {0, 0, 0, 0};
@@ -555,7 +462,6 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
       kidx = b.key_index ? ki : 0u;
     }
   }
-#endif
   // e_chacha20poly1305.cc:127-142: 12-byte nonce, < 2^32 - 1 blocks
   // (XChaCha20-Poly1305: 24-byte nonce, :241-244).
   constexpr uint32_t kNonceLen = XC ? 24 : 12;
@@ -633,7 +539,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   // both ends (the other half written one iteration later); the Poly1305
   // element order then starts with a zero element (Y_A at v = sh).
   constexpr bool kCoalL = COAL && (L == 4 || L == 2);
-  constexpr bool kCoalSh = BSSL_AMD_CHACHA_COAL && BSSL_AMD_CHACHA_SHIFT && kCoalL && !IOV;
+  constexpr bool kCoalSh = kCoalL && !IOV;
   // (Wave-uniform: 1 only if every live record of the wave is 128-byte
   // aligned, so the slot arithmetic stays scalar.)
   const uint64_t live_mask = __ballot(live);
@@ -647,7 +553,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   // chunk j at + 16 ((j + q + r) mod 4) -- conflict-free both for the 16
   // chunks of a record and for the 4 chunks a lane reads of its own block).
   __shared__ uint4 s_c0[kThreads][4];
-  constexpr bool kCoal = BSSL_AMD_CHACHA_COAL && kCoalL && !IOV;
+  constexpr bool kCoal = kCoalL && !IOV;
   // Per record slot: byte offset and the number of full 64-byte blocks the
   // coalesced path moves (0 unless the record is live and 16-byte aligned).
   __shared__ uint4 s_rinfo[kThreads / L];
@@ -712,7 +618,6 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
           }
         }
         if (gp) {
-#if BSSL_AMD_CHACHA_IOV_DMA
 #pragma unroll
           for (int i = 0; i < 4; i++)
             __builtin_amdgcn_global_load_lds(
@@ -720,10 +625,6 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
                 reinterpret_cast<__attribute__((address_space(3))) void *>(
                     reinterpret_cast<uintptr_t>(stage + 1024 * i)),
                 16, 0, 0);
-#else
-#pragma unroll
-          for (int i = 0; i < 4; i++) pre[i] = load16_any(gp + 16 * i);
-#endif
           pre_ok = true;
         }
       }
@@ -738,13 +639,6 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
       return;
     }
     if (u >= 1 + sh && d < nblk && aligned && m.len >= 64 * d + 64) {
-#if BSSL_AMD_CHACHA_ABLATE == 1
-      if (u >= (uint64_t)L) {
-#pragma unroll
-        for (int i = 0; i < 4; i++) pre[i] = make_uint4((uint32_t)u, i, 3, 4);
-        return;
-      }
-#endif
       const uint4 *sp = reinterpret_cast<const uint4 *>(src + 64 * d);
 #pragma unroll
       for (int i = 0; i < 4; i++) pre[i] = sp[i];
@@ -764,11 +658,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
         // Whole block from the LDS-DMA staging (the caller waited for it).
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-#if BSSL_AMD_CHACHA_IOV_DMA
           const uint4 v = *reinterpret_cast<const uint4 *>(my + 1024 * i);
-#else
-          const uint4 v = pre[i];
-#endif
           x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
         }
 #pragma unroll
@@ -918,9 +808,6 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
       }
 #pragma unroll
       for (int i = 0; i < 16; i++) y[i] = x[i] ^ ks[i];
-#if BSSL_AMD_CHACHA_ABLATE == 4
-      if (u < (uint64_t)L || y[0] == 0x12345678u)
-#endif
 #pragma unroll
       for (int i = 0; i < 4; i++)
         dp[i] = make_uint4(y[4 * i], y[4 * i + 1], y[4 * i + 2], y[4 * i + 3]);
@@ -974,8 +861,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   const bool have0 = (uint32_t)q >= 1 + sh && (uint64_t)q - sh <= nblk;
   if constexpr (IOV) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (LDS-DMA, prefetch)
   if (have0) crypt_block((uint64_t)q, ks, pre, c0, false);
-  CSTAMP(1);
-  if (BSSL_AMD_CHACHA_PRIO) __builtin_amdgcn_s_setprio(0);
+  __builtin_amdgcn_s_setprio(0);
   uint32_t kw[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) kw[i] = __shfl(ks[i], 0, L);
@@ -1125,7 +1011,6 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     }
     absorb((uint64_t)q, c0);
   }
-  CSTAMP(2);
   // Coalesced I/O: in instruction k, lane l moves 16-byte chunk cj = l mod 4
   // of the block of wave lane t = 16 k + l / 4 (record slot t / L, block
   // t mod L of the iteration: data block it L + t mod L - 1 - sh), so the 64
@@ -1159,22 +1044,17 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
         uint64_t a;
         const int t = 16 * k + (lane >> 2);
         const int j = (cj - (t & 3) - (t >> 2)) & 3;
-        if (BSSL_AMD_CHACHA_ABLATE != 7 && coal_addr(k, it, a))
+        if (coal_addr(k, it, a))
           __builtin_amdgcn_global_load_lds(
               reinterpret_cast<const void *>(b.in + a - 16 * cj + 16 * j),
               reinterpret_cast<__attribute__((address_space(3))) void *>(
                   reinterpret_cast<uintptr_t>(stage + 1024 * k)),
-              16, 0, BSSL_AMD_CHACHA_NT_LOAD ? 2 : 0);  // aux 2: nt (gfx950 CPol)
+              16, 0, 0);
       }
     } else {
       prefetch(u, pre);
     }
-#if BSSL_AMD_CHACHA_ABLATE == 3
-#pragma unroll
-    for (int i = 0; i < 16; i++) ks[i] = key[i & 7] ^ (uint32_t)u ^ nonce[i % 3];
-#else
     chacha_block_raw(kl, (uint32_t)(u - sh), nonce, ks);
-#endif
     if constexpr (kCoal || IOV) {
       // vmcnt(0): the LDS-DMA loads have landed.  The keystream words are
       // inputs so the rounds stay ahead of the wait (hipcc otherwise sinks
@@ -1187,9 +1067,6 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     if (u - sh <= nblk) {
       uint32_t c[16];
       crypt_block(u, ks, pre, c, true);
-#if BSSL_AMD_CHACHA_ABLATE == 2
-      if (c[0] == 0x12345678u)
-#endif
       absorb(u, c);
     }
     if constexpr (kCoal) {
@@ -1199,26 +1076,18 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
         uint64_t a;
         if (coal_addr(k, it, a)) {
           const uint4 v = *reinterpret_cast<const uint4 *>(stage + saddr(16 * k + (lane >> 2), cj));
-          if (BSSL_AMD_CHACHA_ABLATE == 8)
-            asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-          else
           {
-#if BSSL_AMD_CHACHA_NT_STORE  // non-temporal ciphertext stores
             uint4 *o = reinterpret_cast<uint4 *>(b.out + a);
             __builtin_nontemporal_store(v.x, &o->x);
             __builtin_nontemporal_store(v.y, &o->y);
             __builtin_nontemporal_store(v.z, &o->z);
             __builtin_nontemporal_store(v.w, &o->w);
-#else
-            *reinterpret_cast<uint4 *>(b.out + a) = v;
-#endif
           }
         }
       }
     }
   }
 
-  CSTAMP(3);
   // Combine the lanes: M = nunits + 1 virtual elements; lane p takes the
   // accumulator of lane (p + M mod L) and the tree weights position p by
   // R^(L-1-p).
@@ -1292,15 +1161,6 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     if (q == 0)
       for (uint32_t i = 0; i < xlen; i++) xout[i] = 0;
   }
-#if BSSL_AMD_CHACHA_STAMPS
-  __builtin_amdgcn_s_waitcnt(0);
-  CSTAMP(4);
-  if ((blockIdx.x & 2047) == 5 && threadIdx.x == 64)
-    printf("cstamps blk %d: start->blk0 %llu setup %llu loop %llu finish %llu total %llu\n",
-           (int)blockIdx.x, (unsigned long long)(ts[1] - ts[0]), (unsigned long long)(ts[2] - ts[1]),
-           (unsigned long long)(ts[3] - ts[2]), (unsigned long long)(ts[4] - ts[3]),
-           (unsigned long long)(ts[4] - ts[0]));
-#endif
 }
 
 // One wave group per wave.  (A persistent form -- 4 or 8 workgroups per CU
@@ -1315,7 +1175,7 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
 
 template <bool OPEN, bool XT, bool XC, bool IOV, bool COAL, bool ANY>
 void launch_one(const ChaChaKeyDev *keys, const BatchDesc &b, hipStream_t s) {
-  constexpr int L = BSSL_AMD_CHACHA_LANES;
+  constexpr int L = kLanes;
   const uint64_t blocks = (b.num_records * L + kThreads - 1) / kThreads;
   hipLaunchKernelGGL((chacha_poly_kernel<OPEN, L, XT, XC, IOV, COAL, ANY>), dim3((unsigned)blocks),
                      dim3(kThreads), 0, s, keys, b);
@@ -1354,7 +1214,7 @@ int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, bool 
                   void *stream, const KernelEvents *ev) {
   if (b.num_records == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if ((b.num_records * BSSL_AMD_CHACHA_LANES + kThreads - 1) / kThreads > 0x7fffffffu) return 1;
+  if ((b.num_records * kLanes + kThreads - 1) / kThreads > 0x7fffffffu) return 1;
   BatchDesc bo = b;  // with the processing order of a ragged batch
   uint32_t *order = nullptr;
   if (wants_length_order(b)) {

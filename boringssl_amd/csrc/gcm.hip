@@ -39,72 +39,16 @@
 #include "bs16_aes.h"
 #include "gf128_ct.h"
 
-#ifndef BSSL_AMD_ABLATE
-#define BSSL_AMD_ABLATE 0
-#endif
 
 namespace bssl_amd {
 namespace {
 
-// Waves per workgroup (one workgroup per CU: the LDS tables take 104 KiB); a
-// build-time knob for tuning (-DBSSL_AMD_GCM_WAVES=..).
-#ifndef BSSL_AMD_GHASH_GROUP
-#define BSSL_AMD_GHASH_GROUP 1
-#endif
-#ifndef BSSL_AMD_GCM_PREFETCH
-#define BSSL_AMD_GCM_PREFETCH 1
-#endif
-#ifndef BSSL_AMD_GCM_WAVES
-#define BSSL_AMD_GCM_WAVES 16
-#endif
-constexpr int kWaves = BSSL_AMD_GCM_WAVES;
-#ifndef BSSL_AMD_GCM_STAMPS
-#define BSSL_AMD_GCM_STAMPS 0
-#endif
-// Plaintext loads and ciphertext stores with the non-temporal hint (each byte
-// is touched once): +1.7 % on config 2 (same-box A/B, 3 rounds).
-#ifndef BSSL_AMD_GCM_NT_STORE
-#define BSSL_AMD_GCM_NT_STORE 1
-#endif
-#ifndef BSSL_AMD_GCM_NT_LOAD
-#define BSSL_AMD_GCM_NT_LOAD 1
-#endif
-// Plaintext loads under the block's branch (1) or unconditional with a
-// clamped address (0, which lets hipcc count the outstanding memory
-// operations instead of draining them with vmcnt(0) once per iteration pair;
-// measured 0.6 % slower on config 2 -- the drain is not what binds).
-#ifndef BSSL_AMD_GCM_COND_LOAD
-#define BSSL_AMD_GCM_COND_LOAD 1
-#endif
-#if BSSL_AMD_GCM_STAMPS
-// Diagnostic build: per-wave cycle counts of the T-table kernel's loop and
-// AES rounds (s_memtime, with its own lgkmcnt wait), printed per wave 0.
-__device__ __forceinline__ uint64_t stamp() {
-  uint64_t t;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  return t;
-}
-#define g_stamp_rounds stv[0]
-#define g_stamp_iters stv[1]
-#define g_stamp_loop stv[2]
-#endif
-// Per-wave diagnostic counters (stamps build only; see BSSL_AMD_GCM_STAMPS).
-struct StampVec {
-  uint64_t v[8];  // rounds, iters, loop; tile path: tiles, plan, build, process
-};
+// Waves per workgroup: one workgroup per CU (the LDS tables take 128 KiB),
+// 16 waves at 128 VGPRs (4 -> 573, 8 -> 981, 16 -> 1,156 GiB/s, DESIGN.md
+// §4.2).  Plaintext loads and ciphertext stores carry the non-temporal hint
+// (each byte is touched once: +1.7 % on config 2).
+constexpr int kWaves = 16;
 constexpr int kRecPerWave = 4;
-// Tiled (multi-key) path: rotating wave priorities (process_records RP).
-#ifndef BSSL_AMD_GCM_TILE_RP
-#define BSSL_AMD_GCM_TILE_RP 1
-#endif
-// VALU GHASH on every second iteration (diagnostic knob, see process_records).
-#ifndef BSSL_AMD_GCM_VGHASH
-#define BSSL_AMD_GCM_VGHASH 0
-#endif
-// Tiled path: workgroup barrier every N iterations (0 = off; even N).
-#ifndef BSSL_AMD_GCM_TILE_SYNC
-#define BSSL_AMD_GCM_TILE_SYNC 0
-#endif
 
 // ---------------------------------------------------------------------------
 // Compile-time AES tables.
@@ -161,7 +105,8 @@ constexpr uint32_t kG8Bytes = 256 * 256;
 constexpr uint32_t kLdsAes = kG8Bytes;
 constexpr uint32_t kAesLdsBytes = 256 * 256;
 constexpr uint32_t kLdsPlan = kLdsAes + kAesLdsBytes;
-constexpr uint32_t kLdsBytes = kLdsPlan + 64 * 16 + 16;  // (+4: TILE_SYNC minimum)
+constexpr uint32_t kLdsBasis = kLdsPlan + 64 * 16 + 16;  // 128 x 16 B (build_gpow)
+constexpr uint32_t kLdsBytes = kLdsBasis + 128 * 16;
 
 __device__ __forceinline__ uint32_t rotl(uint32_t v, int n) {
   return __builtin_amdgcn_alignbit(v, v, 32 - n);
@@ -290,6 +235,45 @@ __device__ __forceinline__ uint4 aes_rounds(uint32_t s0, uint32_t s1, uint32_t s
   return o;
 }
 
+// E_K(J0) by the 4 lanes of a quad, one state column each (gcm.cc.inc:340-343):
+// DPP quad permutations hand each lane the three other columns, so a round
+// costs a lane 4 table lookups instead of 16 -- every lane of a record needs
+// the same block, and the LDS cost is per wave-instruction.  In: the round-0
+// state (J0 ^ rk0); out: column (lane & 3) of E_K(J0).
+__device__ __forceinline__ uint32_t quad_rot(uint32_t v, int k) {
+  // lane i of the quad gets lane (i + k) & 3: quad_perm [1,2,3,0] / [2,3,0,1] / [3,0,1,2]
+  return k == 1 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x39, 0xf, 0xf, false)
+       : k == 2 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false)
+                : (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x93, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t quad_sel(uint32_t c, uint32_t a, uint32_t b, uint32_t d,
+                                             uint32_t e) {
+  return (c & 2) ? ((c & 1) ? e : d) : ((c & 1) ? b : a);
+}
+template <int NR, uint32_t TB>
+__device__ __forceinline__ uint32_t ek0_quad(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+                                             const RoundKeys &rk, const uint8_t *smem,
+                                             uint32_t lc0, uint32_t lc1) {
+  const uint32_t c = threadIdx.x & 3;
+  uint32_t w = quad_sel(c, s0, s1, s2, s3);
+#pragma unroll
+  for (int r = 1; r < NR; r++) {
+    const uint32_t w1 = quad_rot(w, 1), w2 = quad_rot(w, 2), w3 = quad_rot(w, 3);
+    const uint32_t kx = quad_sel(c, rk.w[r][0], rk.w[r][1], rk.w[r][2], rk.w[r][3]);
+    w = round_col<TB>(smem, lc0, lc1, w, w1, w2, w3, kx);
+  }
+  const uint32_t w1 = quad_rot(w, 1), w2 = quad_rot(w, 2), w3 = quad_rot(w, 3);
+  return last_col<TB>(smem, lc0, w, w1, w2, w3,
+                      quad_sel(c, rk.w[NR][0], rk.w[NR][1], rk.w[NR][2], rk.w[NR][3]));
+}
+// All four columns of a quad's block in every lane of the quad.
+__device__ __forceinline__ uint4 quad_gather(uint32_t w) {
+  return make_uint4((uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x00, 0xf, 0xf, false),
+                    (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x55, 0xf, 0xf, false),
+                    (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0xaa, 0xf, 0xf, false),
+                    (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0xff, 0xf, 0xf, false));
+}
+
 // ---------------------------------------------------------------------------
 // GHASH multiply by H^16 with the lane-rotated byte table (kLdsG8), spread
 // over the AES rounds of the same iteration.  Lane q (its index within the
@@ -386,9 +370,6 @@ constexpr uint32_t g8_sel() {
 // AES-192/256 spread 2 per round over the first 8.
 template <int NR>
 constexpr int g_steps(int i) {
-#if BSSL_AMD_ABLATE == 8  // diagnostic: no GHASH lookups at all (wrong tags)
-  return 0 * i;
-#endif
   if (NR == 10) return i < 2 ? 3 : 2;
   return i < 8 ? 2 : 0;
 }
@@ -409,14 +390,14 @@ __device__ __forceinline__ uint32_t gh_word(const Gh8 &h) {
 // next block of the lane, its cached rounds 1 and 2 (software pipelining:
 // the next iteration starts at round 3): round i = 0 issues the round-1
 // lookup of `xs` (its round-0 word 3), round i = 1 the four round-2 lookups.
-template <int I, int NR, bool NOG = false>
+template <int I, int NR>
 __device__ __forceinline__ void rounds_s1(uint32_t (&a)[4], const RoundKeys &rk, uint32_t lc0,
                                           uint32_t lc1, Gh8 &h, const uint32_t (&P)[4],
                                           uint32_t &xs, const WindowCache &wc, uint32_t k0,
                                           uint32_t (&nx)[4]) {
   constexpr int R = I + 3;
   if constexpr (R < NR) {
-    constexpr int NG = NOG ? 0 : g_steps<NR>(I);  // NOG: this block's GHASH step on the VALU
+    constexpr int NG = g_steps<NR>(I);
     constexpr int T = g_first<NR>(I);
     constexpr int X = I == 0 ? 1 : I == 1 ? 4 : 0;
     uint32_t xo[X > 0 ? X : 1];
@@ -468,19 +449,11 @@ __device__ __forceinline__ void rounds_s1(uint32_t (&a)[4], const RoundKeys &rk,
       nx[2] = xo[2];
       nx[3] = xo[3];
     }
-    rounds_s1<I + 1, NR, NOG>(a, rk, lc0, lc1, h, P, xs, wc, k0, nx);
+    rounds_s1<I + 1, NR>(a, rk, lc0, lc1, h, P, xs, wc, k0, nx);
   }
 }
 
-__device__ __forceinline__ uint4 shfl4(uint4 v, int src, int width) {
-  return make_uint4(__shfl(v.x, src, width), __shfl(v.y, src, width),
-                    __shfl(v.z, src, width), __shfl(v.w, src, width));
-}
 
-__device__ __forceinline__ uint4 shfl_down4(uint4 v, int d, int width) {
-  return make_uint4(__shfl_down(v.x, d, width), __shfl_down(v.y, d, width),
-                    __shfl_down(v.z, d, width), __shfl_down(v.w, d, width));
-}
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t v) {
   return __builtin_amdgcn_perm(0, v, 0x00010203u);
@@ -492,26 +465,19 @@ __device__ __forceinline__ int wave_max(int v) {
   return v;
 }
 
-// BSSL_AMD_GCM_DPP=1: the per-record reductions of the bulk kernel without
+// The per-record reductions of the bulk kernel use readlane / DPP rather than
 // LDS shuffles (ds_bpermute goes through the LDS queue, which the AES and
 // GHASH lookups of the other waves keep ~84 % busy, and its lane-index
 // operands were spilled and reloaded once per unit).
-#ifndef BSSL_AMD_GCM_DPP
-#define BSSL_AMD_GCM_DPP 1
-#endif
 
 // Maximum over the wave of a value that is uniform within each L-lane group
 // (a record's iteration count): one readlane per group.
 template <int L>
 __device__ __forceinline__ int group_max(int v) {
-#if BSSL_AMD_GCM_DPP
   int m = __builtin_amdgcn_readlane(v, 0);
 #pragma unroll
   for (int k = 1; k < 64 / L; k++) m = max(m, __builtin_amdgcn_readlane(v, k * L));
   return m;
-#else
-  return wave_max(v);
-#endif
 }
 
 // XOR of a word over the 16 lanes of its row, in every lane of the row:
@@ -519,17 +485,11 @@ __device__ __forceinline__ int group_max(int v) {
 // 2301 (DPP row_ror / quad_perm; XOR is commutative, so rotations reduce as
 // well as butterflies do).
 __device__ __forceinline__ uint32_t row_xor16(uint32_t v) {
-#if BSSL_AMD_GCM_DPP
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false);  // row_ror:4
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false);   // quad 2301
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false);   // quad 1032
   return v;
-#else
-#pragma unroll
-  for (int o = 8; o >= 1; o >>= 1) v ^= __shfl_xor(v, o, 16);
-  return v;
-#endif
 }
 
 // len = the record's `in` bytes; xlen = extra bytes sealed after them
@@ -613,27 +573,16 @@ __device__ __forceinline__ uint4 crypt_partial_x(const uint8_t *src, uint8_t *ds
 
 __device__ __forceinline__ uint4 load_blk_nt(const uint8_t *p) {
   const u32_any *ip = reinterpret_cast<const u32_any *>(p);
-#if BSSL_AMD_GCM_NT_LOAD
   return make_uint4(__builtin_nontemporal_load(ip), __builtin_nontemporal_load(ip + 1),
                     __builtin_nontemporal_load(ip + 2), __builtin_nontemporal_load(ip + 3));
-#else
-  return make_uint4(ip[0], ip[1], ip[2], ip[3]);
-#endif
 }
 
 __device__ __forceinline__ void store_blk_nt(uint8_t *p, uint4 y) {
   u32_any *o = reinterpret_cast<u32_any *>(p);
-#if BSSL_AMD_GCM_NT_STORE
   __builtin_nontemporal_store(y.x, o);
   __builtin_nontemporal_store(y.y, o + 1);
   __builtin_nontemporal_store(y.z, o + 2);
   __builtin_nontemporal_store(y.w, o + 3);
-#else
-  o[0] = y.x;
-  o[1] = y.y;
-  o[2] = y.z;
-  o[3] = y.w;
-#endif
 }
 
 // Record at processing position i (sched.hip's length order, if any).
@@ -641,6 +590,20 @@ __device__ __forceinline__ uint64_t rec_at(const BatchDesc &b, uint64_t i) {
   return b.order ? (uint64_t)b.order[i] : i;  // (one load; no order array: none)
 }
 
+
+// XOR of a word over the L lanes of its group (L = 16: row_xor16; L = 8:
+// row_half_mirror then the quad permutations; L = 4: the quad permutations),
+// in every lane of the group.
+template <int L>
+__device__ __forceinline__ uint32_t row_xor(uint32_t v) {
+  static_assert(L == 16 || L == 8 || L == 4, "lanes per record");
+  if constexpr (L == 16) return row_xor16(v);
+  if constexpr (L == 8)
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false);  // half mirror
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false);    // quad 2301
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false);    // quad 1032
+  return v;
+}
 
 // Per-record state handed from the prologue to the bulk kernel (64 bytes).
 struct alignas(16) RecState {
@@ -784,6 +747,85 @@ __global__ __launch_bounds__(256) void gcm_prologue(const GcmKeyDev *__restrict_
   st[rec] = s;
 }
 
+// ---------------------------------------------------------------------------
+// Record start inside the bulk kernel (round 4: no prologue kernel, no
+// per-record state in HBM): the per-record constant work of
+// CRYPTO_gcm128_init_ctx / _aad (gcm.cc.inc:298-398), done by the record's
+// L lanes at the start of their unit.
+
+// Whether record `rec` is sealed/opened at all: a valid key index, a nonce
+// (e_aes.cc.inc:790), the length limits (gcm.cc.inc:368,409) and the
+// tls12/tls13 nonce check (tls_scan.hip, BatchDesc::valid).
+__device__ __forceinline__ bool record_live(const BatchDesc &b, uint64_t rec,
+                                            const RecordMeta &m) {
+  return (!b.key_index || b.key_index[rec] < b.num_keys) && b.nonce_len != 0 &&
+         m.len + m.xlen <= ((uint64_t(1) << 36) - 32) && m.ad_len <= (uint64_t(1) << 61) &&
+         (!b.valid || b.valid[rec]);
+}
+
+// Pre-counter block J0 (gcm.cc.inc:316-338): nonce || be32(1) for 96-bit
+// nonces, else GHASH(N || 0^s || [len(N)]_64), computed by every lane of the
+// record (constant-time VALU products by H).
+__device__ __forceinline__ uint4 record_j0(const BatchDesc &b, uint64_t rec,
+                                           const uint32_t (*hp)[4]) {
+  const uint8_t *nonce = b.nonces + rec * b.nonce_len;
+  if (b.nonce_len == 12) {
+    uint4 j0 = load_partial(nonce, 12);
+    j0.w = 0x01000000u;  // be32(1)
+    return j0;
+  }
+  const Gf128 h1 = gf_load(hp[1]);
+  Gf128 y = {{0, 0, 0, 0}};
+  for (uint64_t o = 0; o < b.nonce_len; o += 16)
+    y = gf_mul(gf_xor(y, to_gf(load_partial(nonce + o,
+                                            (uint32_t)min<uint64_t>(b.nonce_len - o, 16)))),
+               h1);
+  const uint64_t bits = b.nonce_len << 3;
+  y.w[0] ^= (uint32_t)bits;
+  y.w[1] ^= (uint32_t)(bits >> 32);
+  return from_gf(gf_mul(y, h1));
+}
+
+// Block k (16 bytes, zero-padded) of record rec's AD.
+__device__ __forceinline__ uint4 ad_block(const BatchDesc &b, uint64_t rec, const RecordMeta &m,
+                                          uint64_t k) {
+  const uint64_t o = 16 * k;
+  const uint32_t n = (uint32_t)min<uint64_t>(m.ad_len - o, 16);
+  return b.aadvecs ? ivec_load16(b.aadvecs, b.aadvec_start[rec], b.aadvec_start[rec + 1], o, n)
+                   : load_partial(b.ad + m.ad_off + o, n);
+}
+
+// Exclusive GHASH of the AD, Y_A = sum_k A_k H^(m-1-k) (m AD blocks), in
+// every lane of the record's L.  A one-block AD (TLS: 13 bytes) is its own
+// hash; longer ADs are shared out like the message: lane q folds blocks
+// k = q, q + L, ... by Horner in H^L, weighs its sum by H^(m-1-k_last) and
+// the L lanes XOR-reduce (row_xor).  `many`: some record of the wave has a
+// multi-block AD (wave-uniform, so the loop below is).
+template <int L>
+__device__ __forceinline__ uint4 record_ad_hash(const BatchDesc &b, uint64_t rec,
+                                                const RecordMeta &m, bool live, bool many,
+                                                const uint32_t (*hp)[4]) {
+  const uint64_t nad = live ? (m.ad_len + 15) / 16 : 0;
+  if (!many) return nad ? ad_block(b, rec, m, 0) : make_uint4(0, 0, 0, 0);
+  const uint32_t q = threadIdx.x & (L - 1);
+  const Gf128 hl = gf_load(hp[L]);
+  Gf128 acc = {{0, 0, 0, 0}};
+  uint64_t last = 0;
+  const int rounds = group_max<L>((int)((nad + L - 1) / L));
+  for (int i = 0; i < rounds; i++) {
+    const uint64_t k = q + (uint64_t)L * i;
+    if (k < nad) {
+      acc = gf_xor(i ? gf_mul(acc, hl) : acc, to_gf(ad_block(b, rec, m, k)));
+      last = k;
+    }
+  }
+  const uint32_t e = (uint32_t)(nad - 1 - last) & (L - 1);  // (lanes with no block: acc = 0)
+  Gf128 z = e ? gf_mul(acc, gf_load(hp[e])) : acc;
+#pragma unroll
+  for (int i = 0; i < 4; i++) z.w[i] = row_xor<L>(z.w[i]);
+  return from_gf(z);
+}
+
 // End of a record (all bulk kernels): combine the 16 lanes' GHASH
 // accumulators, form the tag, check it (open), write tag/status, and zero the
 // output of a failed record.  Lane algebra: lane q holds the
@@ -798,30 +840,23 @@ __global__ __launch_bounds__(256) void gcm_prologue(const GcmKeyDev *__restrict_
 // and record length only; no table is indexed by a secret.
 template <bool OPEN, int L>
 __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const RecordMeta &m,
-                                              const RecState &s, const BatchDesc &b, uint64_t rec,
+                                              uint4 ek0, const BatchDesc &b, uint64_t rec,
                                               bool active, bool live, uint8_t *dst,
                                               const uint32_t (*hp)[4]) {
-  static_assert(L == 16, "lanes per record");
   const int q = threadIdx.x & (L - 1);
   const int r = (int)((nb + 1) & (L - 1));
   const int p = (q - r + 1) & (L - 1);
-#if BSSL_AMD_ABLATE == 9  // diagnostic: no record-end products (wrong tags)
-  Gf128 z = gf_xor(to_gf(acc), gf_load(hp[L - p]));
-#else
   Gf128 z = gf_mul(to_gf(acc), gf_load(hp[L - p]));
-#endif
 #pragma unroll
-  for (int i = 0; i < 4; i++) z.w[i] = row_xor16(z.w[i]);
+  for (int i = 0; i < 4; i++) z.w[i] = row_xor<L>(z.w[i]);
   // Length block be64(AD bits) || be64(message bits) in the reversed domain.
   const uint64_t abits = m.ad_len << 3, cbits = (m.len + m.xlen) << 3;
   z.w[0] ^= (uint32_t)cbits;
   z.w[1] ^= (uint32_t)(cbits >> 32);
   z.w[2] ^= (uint32_t)abits;
   z.w[3] ^= (uint32_t)(abits >> 32);
-#if BSSL_AMD_ABLATE != 9
   z = gf_mul(z, gf_load(hp[1]));
-#endif
-  const uint4 tag = xor4(from_gf(z), s.ek0);
+  const uint4 tag = xor4(from_gf(z), ek0);
 
   uint8_t *tagp = batch_tag(b, rec);
   int ok = live;
@@ -861,6 +896,41 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
 
 
 // ---------------------------------------------------------------------------
+// A unit's record inputs (one record per L-lane group), issued together at
+// the unit's start: layout, liveness, nonce, the first AD block and the
+// lane's first plaintext block.  (Loading them one unit ahead, before the
+// previous unit's record end, measured slower: the extra live registers
+// spilled, configG 687 vs 743 GiB/s; so did claiming the next unit two
+// iterations early, 729 vs 758, profiles/r04/.)
+struct UnitIn {
+  uint64_t rec;
+  RecordMeta m;
+  uint4 nonce;  // 12-byte nonces: J0 = nonce || be32(1) (words 0..2)
+  uint4 ad0;    // AD block 0, zero-padded
+  uint4 x0;     // the lane's first plaintext block (full blocks only)
+  bool active, live;
+};
+
+template <bool XT, bool IOV>
+__device__ __forceinline__ void unit_load(UnitIn &u, const BatchDesc &b, uint64_t i, int q) {
+  u.active = i < b.num_records;
+  u.rec = u.active ? rec_at(b, i) : 0;
+  u.m = {0, 0, 0, 0, 0};
+  u.live = false;
+  if (u.active) {
+    u.m = record_meta(b, u.rec);
+    u.live = record_live(b, u.rec, u.m);
+  }
+  if constexpr (!XT) u.m.xlen = 0;  // (the launcher picks XT iff extra_len != 0)
+  // (Left undefined when not loaded, as load_full's blocks.)
+  if (u.live && b.nonce_len == 12) u.nonce = load_partial(b.nonces + u.rec * 12, 12);
+  u.ad0 = make_uint4(0, 0, 0, 0);
+  if (u.live && u.m.ad_len) u.ad0 = ad_block(b, u.rec, u.m, 0);
+  if constexpr (!IOV)
+    if (u.live && (uint64_t)q < u.m.len / 16) u.x0 = load_blk_nt(b.in + u.m.off + 16 * q);
+}
+
+// ---------------------------------------------------------------------------
 // Bulk kernel: CTR keystream + GHASH + tag for the (up to) 4 records of a
 // wave, 16 lanes per record.  `active` is per group (record in this key pass).
 // `key` = the batch key (record-end products, finish_record).
@@ -872,46 +942,53 @@ __device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const Reco
 // of each SIMD ~1.9x slower than the oldest.
 template <int NR, bool OPEN, bool XT, int L = 16, bool RP = false, bool IOV = false>
 __device__ __forceinline__ void process_records(const RoundKeys &rk, const BatchDesc &b,
-                                                const RecState *__restrict__ st, uint64_t rec,
-                                                bool active, const uint8_t *smem,
+                                                const UnitIn &in, const uint8_t *smem,
                                                 const GcmKeyDev *key, uint32_t lc0, uint32_t lc1,
-                                                StampVec &stamps, int prio_base = 0) {
-  (void)stamps;
-#if BSSL_AMD_GCM_STAMPS
-  uint64_t *stv = stamps.v;
-#endif
-  static_assert(L == 16 || L == 32, "lanes per record");
+                                                int prio_base = 0) {
+  static_assert(L == 16 || L == 8, "lanes per record");
+  static_assert(!(IOV && L != 16), "iovec records: 16 lanes");
   const int q = threadIdx.x & (L - 1);
-  RecordMeta m = {0, 0, 0, 0, 0};
-  RecState s;
-  s.j0 = s.ek0 = s.ya = make_uint4(0, 0, 0, 0);
-  s.live = 0;
-  if (active) {
-    m = record_meta(b, rec);
-    s = st[rec];
+  const uint64_t rec = in.rec;
+  const bool active = in.active, live = in.live;
+  const RecordMeta m = in.m;
+  // J0 and the AD hash (gcm.cc.inc:298-398), in the record's lanes.
+  uint4 j0 = make_uint4(0, 0, 0, 0);
+  if (live) {
+    if (b.nonce_len == 12)
+      j0 = make_uint4(in.nonce.x, in.nonce.y, in.nonce.z, 0x01000000u);  // nonce || be32(1)
+    else
+      j0 = record_j0(b, rec, key->hpow_ct);
   }
-  const bool live = active && s.live;
-  if constexpr (!XT) m.xlen = 0;  // (the launcher picks XT iff extra_len != 0)
-  const uint64_t nb = live ? (m.len + m.xlen + 15) / 16 : 0;
-  const uint32_t ctr0 = bswap32(s.j0.w);
+  const bool many_ad = __ballot(live && m.ad_len > 16) != 0;
+  const uint4 ya = many_ad ? record_ad_hash<L>(b, rec, m, live, true, key->hpow_ct) : in.ad0;
+  // (< 2^32: the GCM length limit holds for a live record)
+  const uint32_t nb = live ? (uint32_t)((m.len + m.xlen + 15) / 16) : 0u;
+  const uint32_t ctr0 = bswap32(j0.w);
   // Extra bytes after the record (TLS 1.3 inner type, XT kernels): read from /
   // written to their own arrays by the byte path (BatchDesc::extra).
   const uint8_t *xin = XT ? batch_extra_in(b, rec) : nullptr;
   uint8_t *xout = XT ? batch_extra_out(b, rec) : nullptr;
   // Round 0 of the counter blocks: words 0..2 are constant per record.
-  const uint32_t c0 = s.j0.x ^ rk.w[0][0], c1 = s.j0.y ^ rk.w[0][1], c2 = s.j0.z ^ rk.w[0][2];
+  const uint32_t c0 = j0.x ^ rk.w[0][0], c1 = j0.y ^ rk.w[0][1], c2 = j0.z ^ rk.w[0][2];
+  // E_K(J0), one column per lane of each quad (from the same bank-replicated
+  // LDS tables; computed while the unit's first block is in flight).
+  const uint32_t ek0w = ek0_quad<NR, 0>(c0, c1, c2, bswap32(ctr0) ^ rk.w[0][3], rk, smem, lc0, lc1);
   const uint8_t *src = b.in + m.off;
   uint8_t *dst = b.out + m.off;
-  uint4 acc = (q == L - 1 && live) ? s.ya : make_uint4(0, 0, 0, 0);
-  // GHASH lane constants (Gh8): rotation by q bytes and the slot offsets.
-  const bool rs1 = (q >> 2) & 1, rs2 = (q >> 3) & 1;  // (rotation by q mod 16)
-  const uint32_t rbs = (uint32_t)q & 3u;
+  uint4 acc = (q == L - 1 && live) ? ya : make_uint4(0, 0, 0, 0);
+  // GHASH lane constants (Gh8): rotation by gq bytes and the slot offsets.
+  // gq = the lane's index in its 16-lane row whatever L is: the 16 lanes of a
+  // ds_read_b128 lane group then always read 16 different slots (the
+  // rotation only orders each lane's own 16 lookups).
+  const int gq = threadIdx.x & 15;
+  const bool rs1 = (gq >> 2) & 1, rs2 = (gq >> 3) & 1;  // (rotation by gq)
+  const uint32_t rbs = (uint32_t)gq & 3u;
   uint32_t P[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     uint32_t v = 0;
 #pragma unroll
-    for (int i = 0; i < 4; i++) v |= (uint32_t)(((4 * k + i + q) & 15) << 4) << (8 * i);
+    for (int i = 0; i < 4; i++) v |= (uint32_t)(((4 * k + i + gq) & 15) << 4) << (8 * i);
     P[k] = v;
   }
   // Counter-mode caching (Bernstein-Schwabe): within a 256-counter window only
@@ -926,7 +1003,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   // Full 16-byte blocks of this lane's record, at any alignment (one
   // dwordx4 each, load_blk_nt); the partial last block takes the byte path.
   // (iovec records: their own paths below.)
-  const uint64_t nfull = !IOV ? m.len / 16 : 0;
+  const uint32_t nfull = !IOV && live ? (uint32_t)(m.len / 16) : 0u;
   // iovec records (IOV): chunk cursors of the loads (one iteration ahead)
   // and of the stores.
   static_assert(!(IOV && XT), "iovec records carry no extra bytes");
@@ -949,9 +1026,6 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   // (Left undefined when not loaded: such a block is never stored or hashed
   // from this value, and a zero-fill would be a VALU write that the waitcnt
   // pass orders after the previous store.)
-  // BSSL_AMD_GCM_COND_LOAD=0 issues the load unconditionally (a block past
-  // the record's full blocks reads the batch's RecState array instead, a
-  // valid 16-byte-aligned address whose value is never used).
   auto load_full = [&](uint64_t j) {
     uint4 v;
     if constexpr (IOV) {
@@ -962,7 +1036,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
       } else {
         v = make_uint4(0, 0, 0, 0);
         const uint64_t p = j * 16;
-        if (p < m.len) {
+        if (live && p < m.len) {  // (a dead record never walks the batch's chunks)
           const uint64_t c_end = b.iovec_start[rec + 1];
           IovCur k;
           iov_at(k, b, ld_c, ld_cs);
@@ -980,24 +1054,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
       }
       return v;
     }
-#if BSSL_AMD_ABLATE == 3 || BSSL_AMD_ABLATE == 4  // diagnostic: no plaintext loads
-    v = make_uint4((uint32_t)j, 1, 2, 3);
-#elif BSSL_AMD_ABLATE == 7
-    // Diagnostic cost probe (wrong output): the plaintext goes to a per-wave
-    // LDS slot by LDS-DMA issued in asm (no wait) and is read back with
-    // ds_read_b128 -- the instruction cost of LDS-DMA staging.
-    {
-      const uint32_t slot = kLdsBytes + (threadIdx.x >> 6) * 1024u;
-      const uint8_t *gp = j < nfull ? src + j * 16 : reinterpret_cast<const uint8_t *>(st);
-      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off nt"
-                   :: "s"(__builtin_amdgcn_readfirstlane(slot)), "v"(gp) : "memory", "m0");
-      v = *reinterpret_cast<const uint4 *>(smem + slot + (threadIdx.x & 63) * 16);
-    }
-#elif BSSL_AMD_GCM_COND_LOAD
-    if (j < nfull) v = load_blk_nt(src + j * 16);
-#else
-    v = load_blk_nt(j < nfull ? src + j * 16 : reinterpret_cast<const uint8_t *>(st));
-#endif
+    if (j < nfull) v = load_blk_nt(src + (uint64_t)j * 16);
     return v;
   };
   // One iteration: block j = it*16 + q, plaintext (if full) already in x,
@@ -1012,14 +1069,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     wc.update<T>(ctr, s3, c0, c1, c2, rk, smem, lc0, lc1);
     wc.rounds12<T>(k0, s3, cur[0], cur[1], cur[2], cur[3], smem, lc0, lc1);
   }
-  // BSSL_AMD_GCM_VGHASH = 2 (diagnostic knob): every second iteration takes
-  // its multiply acc * H^16 on the VALU (gf_mul, constant-time) instead of
-  // the 16 LDS lookups -- the LDS is the binding unit (83 % busy, GHASH 19 %
-  // of it), the VALU ~45 %.
-  const Gf128 h16 = gf_load(key->hpow_ct[16]);
-  (void)h16;
-  auto step = [&](int it, uint4 x, auto vg_tag) {
-    constexpr bool VG = decltype(vg_tag)::value;
+  auto step = [&](int it, uint4 x) {
     if constexpr (RP) {
       switch ((prio_base + it) & 3) {
         case 0: __builtin_amdgcn_s_setprio(0); break;
@@ -1028,42 +1078,16 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
         default: __builtin_amdgcn_s_setprio(3); break;
       }
     }
-    const uint64_t j = (uint64_t)it * L + q;
+    const uint32_t j = (uint32_t)it * L + q;
     const uint32_t ctrn = ctr0 + 1u + (uint32_t)(j + L);  // next block, inc32 mod 2^32
     uint32_t xs = bswap32(ctrn) ^ rk.w[0][3];
     wc.update<T>(ctrn, xs, c0, c1, c2, rk, smem, lc0, lc1);
     Gh8 h;
-    if constexpr (VG) {
-      h.r0 = h.r1 = h.r2 = h.r3 = 0;
-      h.g = from_gf(gf_mul(to_gf(acc), h16));
-    } else {
-      g8_rotate(h, acc, rs1, rs2, rbs);
-      h.g = make_uint4(0, 0, 0, 0);
-    }
+    g8_rotate(h, acc, rs1, rs2, rbs);
+    h.g = make_uint4(0, 0, 0, 0);
     uint32_t sa[4] = {cur[0], cur[1], cur[2], cur[3]};
-#if BSSL_AMD_ABLATE == 2 || BSSL_AMD_ABLATE == 5  // diagnostic: no AES rounds 3..NR
-    wc.rounds12<T>(k0, xs, cur[0], cur[1], cur[2], cur[3], smem, lc0, lc1);
-#if BSSL_AMD_ABLATE == 2  // (GHASH steps kept)
-    h.g = xor4_3(h.g, g8_load<0>(h, P, smem), g8_load<1>(h, P, smem));
-    h.g = xor4_3(h.g, g8_load<2>(h, P, smem), g8_load<3>(h, P, smem));
-    h.g = xor4_3(h.g, g8_load<4>(h, P, smem), g8_load<5>(h, P, smem));
-    h.g = xor4_3(h.g, g8_load<6>(h, P, smem), g8_load<7>(h, P, smem));
-    h.g = xor4_3(h.g, g8_load<8>(h, P, smem), g8_load<9>(h, P, smem));
-    h.g = xor4_3(h.g, g8_load<10>(h, P, smem), g8_load<11>(h, P, smem));
-    h.g = xor4_3(h.g, g8_load<12>(h, P, smem), g8_load<13>(h, P, smem));
-    h.g = xor4_3(h.g, g8_load<14>(h, P, smem), g8_load<15>(h, P, smem));
-#endif
-#else
-#if BSSL_AMD_GCM_STAMPS
-    const uint64_t st0 = stamp();
-#endif
-    rounds_s1<0, NR, VG>(sa, rk, lc0, lc1, h, P, xs, wc, k0, cur);
+    rounds_s1<0, NR>(sa, rk, lc0, lc1, h, P, xs, wc, k0, cur);
     asm_last_s1(sa, rk.w[NR], lc0);
-#if BSSL_AMD_GCM_STAMPS
-    g_stamp_rounds += stamp() - st0;
-    g_stamp_iters++;
-#endif
-#endif
     const uint4 ks = make_uint4(sa[0], sa[1], sa[2], sa[3]);
     uint4 y = xor4(x, ks);
     if constexpr (IOV) {
@@ -1072,7 +1096,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
         st_ptr += 16 * L;
         st_left -= 16 * L;
       } else if (j < nb) {
-        const uint64_t p = j * 16;
+        const uint64_t p = (uint64_t)j * 16;
         const uint32_t n = (uint32_t)min<uint64_t>(m.len - p, 16);
         const uint64_t c_end = b.iovec_start[rec + 1];
         IovCur k;
@@ -1092,29 +1116,20 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
       if (j < nb) acc = xor4(h.g, OPEN ? x : y);
       return;
     }
-#if BSSL_AMD_ABLATE == 4 || BSSL_AMD_ABLATE == 6  // diagnostic: no stores
     if (j < nfull) {
-      asm volatile("" ::"v"(y.x), "v"(y.y), "v"(y.z), "v"(y.w));
-#else
-    if (j < nfull) {
-      store_blk_nt(dst + j * 16, y);
-#endif
+      store_blk_nt(dst + (uint64_t)j * 16, y);
     } else if (j < nb) {
-      const uint32_t n = (uint32_t)min<uint64_t>(m.len + m.xlen - j * 16, 16);
+      const uint32_t n = (uint32_t)min<uint64_t>(m.len + m.xlen - (uint64_t)j * 16, 16);
       if constexpr (XT) {
-        y = crypt_partial_x(src, dst, m.len, xin, xout, j * 16, ks, n, x);
+        y = crypt_partial_x(src, dst, m.len, xin, xout, (uint64_t)j * 16, ks, n, x);
       } else {
-        x = load_partial(src + j * 16, n);
+        x = load_partial(src + (uint64_t)j * 16, n);
         y = mask_block(xor4(x, ks), n);
-        store_partial(dst + j * 16, y, n);
+        store_partial(dst + (uint64_t)j * 16, y, n);
       }
     }
     if (j < nb) {
-#if BSSL_AMD_ABLATE == 1  // diagnostic build: no GHASH multiply (wrong tags)
-      acc = xor4(acc, OPEN ? x : y);
-#else
       acc = xor4(h.g, OPEN ? x : y);
-#endif
     }
   };
   // Plaintext is loaded one iteration ahead into two alternating buffers (the
@@ -1122,64 +1137,21 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   // for iteration it+1 is issued before iteration it's store, so waiting for
   // it never waits for a store (vmcnt counts loads and stores in issue order)
   // and its latency hides under a whole iteration of AES + GHASH.
-#if BSSL_AMD_GCM_STAMPS
-  const uint64_t sl0 = stamp();
-#endif
-#if BSSL_AMD_GCM_PREFETCH == 2
-  // Two iterations ahead (three buffers).
-  uint4 x0 = load_full(q), x1 = load_full(L + q);
-  int it = 0;
-  for (; it + 2 < iters; it += 3) {
-    const uint4 x2 = load_full((uint64_t)(it + 2) * L + q);
-    step(it, x0, std::integral_constant<bool, false>());
-    x0 = load_full((uint64_t)(it + 3) * L + q);
-    step(it + 1, x1, std::integral_constant<bool, false>());
-    x1 = load_full((uint64_t)(it + 4) * L + q);
-    step(it + 2, x2, std::integral_constant<bool, false>());
-  }
-  if (it < iters) step(it, x0, std::integral_constant<bool, false>());
-  if (it + 1 < iters) step(it + 1, x1, std::integral_constant<bool, false>());
-#else
-  int sync_limit = 0;
-#if BSSL_AMD_GCM_TILE_SYNC
-  if constexpr (RP) {  // (RP: the tiled path, where every wave of the workgroup is here)
-    // The tile's minimum iteration count; every wave executes the same
-    // barriers below (those at it + 1 < sync_limit).
-    uint32_t *s_min = const_cast<uint32_t *>(reinterpret_cast<const uint32_t *>(smem + kLdsPlan + 64 * 16 + 4));
-    if (threadIdx.x == 0) *s_min = 0x7fffffffu;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) atomicMin(s_min, (uint32_t)iters);
-    __syncthreads();
-    sync_limit = (int)*s_min;
-    __syncthreads();
-  }
-#endif
-  uint4 x0 = load_full(q);
+  uint4 x0;
+  if constexpr (IOV)
+    x0 = load_full(q);
+  else
+    x0 = in.x0;
   int it = 0;
   for (; it + 1 < iters; it += 2) {
-#if BSSL_AMD_GCM_TILE_SYNC
-    // Tiled path (diagnostic knob): a workgroup barrier every TILE_SYNC
-    // iterations while every wave of the tile still has iterations left
-    // (sync_limit = the tile's minimum), so the SIMD arbiter's favoured waves
-    // cannot run ahead and idle at the end of the tile.  Every wave executes
-    // the same number of barriers.
-    if (RP && it > 0 && it + 1 < sync_limit && it % BSSL_AMD_GCM_TILE_SYNC == 0) __syncthreads();
-#endif
     const uint4 x1 = load_full((uint64_t)(it + 1) * L + q);
-    step(it, x0, std::integral_constant<bool, false>());
+    step(it, x0);
     x0 = load_full((uint64_t)(it + 2) * L + q);
-    step(it + 1, x1, std::integral_constant<bool, (BSSL_AMD_GCM_VGHASH == 2)>());
+    step(it + 1, x1);
   }
-  if (it < iters) step(it, x0, std::integral_constant<bool, false>());
-#endif
-#if BSSL_AMD_GCM_STAMPS
-  g_stamp_loop += stamp() - sl0;
-  const uint64_t tf0 = stamp();
-#endif
-  finish_record<OPEN, L>(acc, nb, m, s, b, rec, active, live, dst, key->hpow_ct);
-#if BSSL_AMD_GCM_STAMPS
-  stv[5] += stamp() - tf0;
-#endif
+  if (it < iters) step(it, x0);
+  finish_record<OPEN, L>(acc, nb, m, quad_gather(ek0w), b, rec, active, live, dst,
+                         key->hpow_ct);
 }
 
 // Byte table of H^16 from the key's nibble tables (power 4): entry (e, p) =
@@ -1203,23 +1175,107 @@ __device__ __forceinline__ void build_g8(uint8_t *smem, const uint4 *__restrict_
     reinterpret_cast<uint4 *>(smem + kLdsG8)[tid + i * THREADS] = xor4(a[i], b);
 }
 
-// W waves per workgroup (one workgroup per CU).
-// Declared for 1024 threads whatever W is, so every variant is compiled
-// into 128 VGPRs (an 8-wave workgroup then leaves half of each SIMD's
-// register file free).
-template <int NR, bool OPEN, bool XT, int W, bool IOV = false>
+// Byte table of H^L (L < 16: the short-record kernels, whose GHASH stride is
+// L) computed in the kernel from the key's prepared H^L (hpow_ct[L]): the
+// 128 basis products (bit `bit` of byte p) x H^L by 128 threads with the
+// constant-time VALU product, then entry (e, p) = XOR of the basis elements
+// of p for the bits of e (e and p are table indices, public).
+template <int THREADS>
+__device__ __forceinline__ void build_gpow(uint8_t *smem, const uint32_t *hl, int tid) {
+  static_assert(THREADS >= 128 && 4096 % THREADS == 0, "table build split");
+  uint4 *basis = reinterpret_cast<uint4 *>(smem + kLdsBasis);
+  if (tid < 128) {
+    const uint32_t p = (uint32_t)tid >> 3, bit = (uint32_t)tid & 7u;
+    uint32_t w[4] = {0, 0, 0, 0};
+    w[p >> 2] = 1u << (8 * (p & 3) + bit);
+    basis[tid] = from_gf(gf_mul(to_gf(make_uint4(w[0], w[1], w[2], w[3])), gf_load(hl)));
+  }
+  __syncthreads();
+  const uint32_t p = (uint32_t)tid & 15u;
+  uint4 bv[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) bv[k] = basis[p * 8 + k];
+#pragma unroll
+  for (int i = 0; i < 4096 / THREADS; i++) {
+    const uint32_t e = ((uint32_t)tid >> 4) + (uint32_t)i * (THREADS / 16);
+    uint4 v = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t msk = 0u - ((e >> k) & 1u);
+      v = make_uint4(v.x ^ (bv[k].x & msk), v.y ^ (bv[k].y & msk), v.z ^ (bv[k].z & msk),
+                     v.w ^ (bv[k].w & msk));
+    }
+    reinterpret_cast<uint4 *>(smem + kLdsG8)[tid + i * THREADS] = v;
+  }
+}
+
+// The AES tables of the bulk kernels, replicated per bank: entry idx, slot t,
+// lane l at kLdsAes + idx*256 + t*128 + l*4.  Slot 1 holds T1 = rotl8(T0).
+template <int THREADS>
+__device__ __forceinline__ void fill_aes_tables(uint8_t *smem, int tid) {
+  for (int e = tid; e < 256 * 64; e += THREADS) {
+    const int idx = e >> 6, slot = (e >> 5) & 1;
+    const uint32_t v = kTables.te0[idx];
+    reinterpret_cast<uint32_t *>(smem + kLdsAes)[e] = slot ? rotl(v, 8) : v;
+  }
+}
+
+// One-key bulk kernel (the ctx API: configs 2, 4, G; no key_index).  One
+// workgroup of W = 16 waves per CU (the LDS tables take 128 KiB; declared for
+// 1024 threads so it compiles into 128 VGPRs).  Each wave takes the next unit
+// of 64 / L records (in processing order) from a grid-wide counter, so waves
+// that the SIMD arbiter favours (older waves issue first) simply process more
+// units instead of waiting at a per-tile barrier for the slowest wave
+// (DESIGN.md §4.2).  L: lanes per record -- 8 (8 records per wave, GHASH
+// stride H^8) for every one-key batch but iovec batches, 16 for those.
+// (A kernel of its own, apart from the keyset kernel, so each gets its own
+// register allocation.)
+template <int NR, bool OPEN, bool XT, int W, bool IOV = false, int L = 16>
 __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__ keys,
-                                                    BatchDesc b,
-                                                    const RecState *__restrict__ st,
-                                                    uint32_t *__restrict__ units) {
+                                                    BatchDesc b, uint32_t *__restrict__ units) {
+  constexpr int kThreads = W * 64;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  fill_aes_tables<kThreads>(smem, tid);
+  const uint32_t lc0 = kLdsAes + (uint32_t)(lane & 31) * 4u;
+  const uint32_t lc1 = lc0 + 128u;
+  const uint64_t n = b.num_records;
+  if constexpr (L == 16)
+    build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab16), tid);
+  else
+    build_gpow<kThreads>(smem, keys[0].hpow_ct[L], tid);
+  __syncthreads();
+  RoundKeys rk;
+#pragma unroll
+  for (int r = 0; r <= NR; r++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) rk.w[r][c] = keys[0].rk[r][c];
+  auto claim = [&]() {
+    uint32_t u = 0;
+    if (lane == 0) u = atomicAdd(units, 1u);
+    return u;
+  };
+  for (;;) {
+    const uint64_t first = (uint64_t)__builtin_amdgcn_readlane(claim(), 0) * (64 / L);
+    if (first >= n) break;
+    UnitIn in;
+    unit_load<XT, IOV>(in, b, first + lane / L, lane & (L - 1));
+    process_records<NR, OPEN, XT, L, false, IOV>(rk, b, in, smem, keys, lc0, lc1);
+  }
+}
+
+// Keyset bulk kernel (key_index per record: BSSL_AMD_KEYSET, config 5): the
+// records are visited in tiles of W * 4; a tile whose records use several
+// keys is processed in one pass per distinct key, since the LDS byte table is
+// per key.
+template <int NR, bool OPEN, bool XT, int W>
+__global__ __launch_bounds__(1024) void gcm_keyset_kernel(const GcmKeyDev *__restrict__ keys,
+                                                           BatchDesc b) {
   constexpr int kThreads = W * 64;
   constexpr int kRecPerTile = W * kRecPerWave;
   static_assert(kRecPerTile <= 64, "one wave plans a tile with ballots");
-#if BSSL_AMD_ABLATE == 7
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes + 16 * 1024];
-#else
   __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
-#endif
   // Pass list of the current tile: key and 64-bit record mask per pass.
   uint32_t *s_pass_key = reinterpret_cast<uint32_t *>(smem + kLdsPlan);
   uint64_t *s_pass_mask = reinterpret_cast<uint64_t *>(smem + kLdsPlan + 64 * 4);
@@ -1228,69 +1284,13 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int g = lane >> 4;
-
-  // AES tables, replicated per bank: entry idx, slot t, lane l at
-  // kLdsAes + idx*256 + t*128 + l*4.  Slot 1 holds T1 = rotl8(T0).
-  for (int e = tid; e < 256 * 64; e += kThreads) {
-    const int idx = e >> 6, slot = (e >> 5) & 1;
-    const uint32_t v = kTables.te0[idx];
-    reinterpret_cast<uint32_t *>(smem + kLdsAes)[e] = slot ? rotl(v, 8) : v;
-  }
+  fill_aes_tables<kThreads>(smem, tid);
   const uint32_t lc0 = kLdsAes + (uint32_t)(lane & 31) * 4u;
   const uint32_t lc1 = lc0 + 128u;
-  const uint32_t mf0 = 0xf0u;
-
   uint32_t loaded = 0xffffffffu;
-  StampVec stamps = {{0, 0, 0, 0, 0, 0, 0, 0}};
   const uint64_t n = b.num_records;
-  if (!b.key_index) {
-    // One key for the whole batch: no tiles or passes.  Each wave takes the
-    // next unit of kRecPerWave records (in processing order) from a
-    // grid-wide counter, so waves that the SIMD arbiter favours (older
-    // waves issue first) simply process more units instead of waiting at a
-    // per-tile barrier for the slowest wave.
-    build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab16), tid);
-    __syncthreads();
-    RoundKeys rk;
-#pragma unroll
-    for (int r = 0; r <= NR; r++)
-#pragma unroll
-      for (int c = 0; c < 4; c++) rk.w[r][c] = keys[0].rk[r][c];
-    for (;;) {
-#if BSSL_AMD_GCM_STAMPS
-      const uint64_t tu0 = stamp();
-#endif
-      uint32_t u = 0;
-      if (lane == 0) u = atomicAdd(units, 1u);
-      u = __builtin_amdgcn_readfirstlane(__shfl(u, 0, 64));
-      const uint64_t first = (uint64_t)u * kRecPerWave;
-      if (first >= n) break;
-      const uint64_t i = first + g;
-      const bool active = i < n;
-      process_records<NR, OPEN, XT, 16, false, IOV>(rk, b, st, active ? rec_at(b, i) : 0, active,
-                                                    smem, keys, lc0, lc1, stamps);
-#if BSSL_AMD_GCM_STAMPS
-      stamps.v[3]++;
-      stamps.v[4] += stamp() - tu0;
-#endif
-    }
-#if BSSL_AMD_GCM_STAMPS
-    if (blockIdx.x < 2 && (tid & 63) == 0)
-      printf("stamps block %d wave %d: units %llu iters %llu  cycles/iter %.0f  rounds3..NR/iter "
-             "%.0f  cycles/unit %.0f (loop %.0f finish %.0f)\n",
-             (int)blockIdx.x, wave, (unsigned long long)stamps.v[3],
-             (unsigned long long)stamps.v[1], (double)stamps.v[2] / (double)stamps.v[1],
-             (double)stamps.v[0] / (double)stamps.v[1], (double)stamps.v[4] / stamps.v[3],
-             (double)stamps.v[2] / stamps.v[3], (double)stamps.v[5] / stamps.v[3]);
-#endif
-    return;
-  }
   for (uint64_t base = (uint64_t)blockIdx.x * kRecPerTile; base < n;
        base += (uint64_t)gridDim.x * kRecPerTile) {
-#if BSSL_AMD_GCM_STAMPS
-    const uint64_t tp0 = stamp();
-    stamps.v[3]++;
-#endif
     __syncthreads();
     if (wave == 0) {
       // Plan the tile: one pass per distinct key, in record order.
@@ -1313,16 +1313,10 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
       if (lane == 0) *s_npass = np;
     }
     __syncthreads();
-#if BSSL_AMD_GCM_STAMPS
-    stamps.v[4] += stamp() - tp0;
-#endif
     const int npass = *s_npass;
     for (int pi = 0; pi < npass; pi++) {
       const uint32_t k = __builtin_amdgcn_readfirstlane(s_pass_key[pi]);
       const uint64_t mask = s_pass_mask[pi];
-#if BSSL_AMD_GCM_STAMPS
-      const uint64_t tb0 = stamp();
-#endif
       if (k != loaded) {
         __syncthreads();
         // Byte table of H^16 from the key's nibble tables (power 4): entry
@@ -1336,30 +1330,14 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
       for (int r = 0; r <= NR; r++)
 #pragma unroll
         for (int c = 0; c < 4; c++) rk.w[r][c] = keys[k].rk[r][c];
-#if BSSL_AMD_GCM_STAMPS
-      const uint64_t tq0 = stamp();
-      stamps.v[5] += tq0 - tb0;
-#endif
       const int t = wave * kRecPerWave + g;
       const bool active = (mask >> t) & 1;
-      process_records<NR, OPEN, XT, 16, BSSL_AMD_GCM_TILE_RP != 0>(
-          rk, b, st, active ? rec_at(b, base + t) : 0, active, smem, keys + k, lc0, lc1, stamps,
-          wave >> 2);
-      if (BSSL_AMD_GCM_TILE_RP) __builtin_amdgcn_s_setprio(0);
-#if BSSL_AMD_GCM_STAMPS
-      stamps.v[6] += stamp() - tq0;
-#endif
+      UnitIn in;
+      unit_load<XT, false>(in, b, active ? base + t : n, lane & 15);
+      process_records<NR, OPEN, XT, 16, true>(rk, b, in, smem, keys + k, lc0, lc1, wave >> 2);
+      __builtin_amdgcn_s_setprio(0);
     }
   }
-#if BSSL_AMD_GCM_STAMPS
-  if (blockIdx.x < 2 && (tid & 63) == 0)
-    printf("tiles block %d wave %d: tiles %llu per tile: plan+barriers %.0f build %.0f process %.0f "
-           "(loop %.0f) cycles/iter %.0f\n",
-           (int)blockIdx.x, wave, (unsigned long long)stamps.v[3],
-           (double)stamps.v[4] / stamps.v[3], (double)stamps.v[5] / stamps.v[3],
-           (double)stamps.v[6] / stamps.v[3], (double)stamps.v[2] / stamps.v[3],
-           (double)stamps.v[2] / (double)stamps.v[1]);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1548,7 +1526,7 @@ __device__ __forceinline__ void process_records_bs16(const uint32_t *__restrict_
     m = record_meta(b, rr);
     s = st[rr];
   }
-  finish_record<OPEN, 16>(acc, nb, m, s, b, rec, active, live, dst, key->hpow_ct);
+  finish_record<OPEN, 16>(acc, nb, m, s.ek0, b, rec, active, live, dst, key->hpow_ct);
 }
 
 // Table-free one-key kernel (BSSL_AMD_GCM_MODE=bs16): 16 waves per CU at 128
@@ -1579,7 +1557,6 @@ __global__ __launch_bounds__(1024) void gcm_bs16_kernel(const GcmKeyDev *__restr
 #pragma unroll
     for (int c = 0; c < 4; c++) rk.w[r][c] = keys[0].rk[r][c];
   const uint32_t lc0 = kLdsAes + (uint32_t)(lane & 31) * 4u, lc1 = lc0 + 128u;
-  StampVec stamps = {{0, 0, 0, 0, 0, 0, 0, 0}};
   for (;;) {
     uint32_t u = 0;
     if (lane == 0) u = atomicAdd(units, 1u);
@@ -1597,7 +1574,11 @@ __global__ __launch_bounds__(1024) void gcm_bs16_kernel(const GcmKeyDev *__restr
     if (__ballot(!ok) == 0)
       process_records_bs16<NR, OPEN>(rkp, b, st, rec, active, m, smem, keys);
     else
-      process_records<NR, OPEN, false>(rk, b, st, rec, active, smem, keys, lc0, lc1, stamps);
+    {
+      UnitIn in;
+      unit_load<false, false>(in, b, i, lane & 15);
+      process_records<NR, OPEN, false>(rk, b, in, smem, keys, lc0, lc1);
+    }
   }
 }
 
@@ -1622,19 +1603,24 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
         hipSuccess)
       return 1;
   }
-  // Per-record state plus one extra entry whose first word is the unit
-  // counter of the one-key kernels.
+  const int mode = gcm_mode(b);
+  // The unit counter of the one-key kernels (64 bytes, zeroed) and, for the
+  // bs16 engine only, its per-record state (RecState, written by its
+  // prologue; the T-table kernel starts its records itself).
+  const uint64_t nst = mode == 1 ? b.num_records : 0;
   RecState *st = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void **>(&st), (b.num_records + 1) * sizeof(RecState), s) !=
+  if (hipMallocAsync(reinterpret_cast<void **>(&st), (nst + 1) * sizeof(RecState), s) !=
       hipSuccess)
     return 2;
-  uint32_t *units = reinterpret_cast<uint32_t *>(st + b.num_records);
+  uint32_t *units = reinterpret_cast<uint32_t *>(st + nst);
   if (hipMemsetAsync(units, 0, sizeof(RecState), s) != hipSuccess) {
     hipFreeAsync(st, s);
     return 2;
   }
-  const uint64_t pblocks = (b.num_records + 255) / 256;
-  hipLaunchKernelGGL((gcm_prologue<NR>), dim3((unsigned)pblocks), dim3(256), 0, s, keys, b, st);
+  if (mode == 1) {
+    const uint64_t pblocks = (b.num_records + 255) / 256;
+    hipLaunchKernelGGL((gcm_prologue<NR>), dim3((unsigned)pblocks), dim3(256), 0, s, keys, b, st);
+  }
   BatchDesc bo = b;  // with the processing order of a ragged batch
   uint32_t *order = nullptr;
   if (wants_length_order(b)) {
@@ -1651,7 +1637,6 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
     }
     bo.order = order;
   }
-  const int mode = gcm_mode(b);
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
   const RecState *cst = st;
   if (mode == 1) {
@@ -1663,15 +1648,23 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
   } else {
     const uint64_t tiles = (b.num_records + kWaves * kRecPerWave - 1) / (kWaves * kRecPerWave);
     const unsigned grid = (unsigned)(tiles < (uint64_t)g_num_cus ? tiles : (uint64_t)g_num_cus);
-    if (b.iovecs)  // (one key: the ctx API)
+    if (b.key_index) {
+      if (b.extra_len)
+        hipLaunchKernelGGL((gcm_keyset_kernel<NR, OPEN, true, kWaves>), dim3(grid),
+                           dim3(kWaves * 64), 0, s, keys, bo);
+      else
+        hipLaunchKernelGGL((gcm_keyset_kernel<NR, OPEN, false, kWaves>), dim3(grid),
+                           dim3(kWaves * 64), 0, s, keys, bo);
+    } else if (b.iovecs) {  // (one key: the ctx API; 16 lanes per record)
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, true>), dim3(grid), dim3(kWaves * 64),
-                         0, s, keys, bo, cst, units);
-    else if (b.extra_len)
-      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, true, kWaves>), dim3(grid), dim3(kWaves * 64), 0, s,
-                         keys, bo, cst, units);
-    else
-      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves>), dim3(grid), dim3(kWaves * 64), 0, s,
-                         keys, bo, cst, units);
+                         0, s, keys, bo, units);
+    } else if (b.extra_len) {
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, true, kWaves, false, 8>), dim3(grid),
+                         dim3(kWaves * 64), 0, s, keys, bo, units);
+    } else {
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, 8>), dim3(grid),
+                         dim3(kWaves * 64), 0, s, keys, bo, units);
+    }
   }
   int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);

@@ -40,35 +40,17 @@ namespace {
 // constant-time argument of gcm.hip's tables; T2/T3 are
 // rot16(T0/T1), one rotate per column.  (Rounds 1/2 used four plain 1 KiB
 // tables, whose bank conflicts depend on the data.)
-// BSSL_AMD_SIV_SPLIT = 1: the per-block multiply by H^16 as four independent
-// Shoup chains (gmul4) instead of one 32-step chain.
-#ifndef BSSL_AMD_SIV_SPLIT
-#define BSSL_AMD_SIV_SPLIT 1
-#endif
-// BSSL_AMD_SIV_GROUP = 1: a record's 16 lanes are the 16 lanes of one
+// Round-1/2 choices kept: the per-block multiply by H^16 as
+// four independent Shoup chains (gmul4d, one reduction per chain) instead of
+// one 32-step chain; a record's 16 lanes are the 16 lanes of one
 // ds_read_b128 lane group ({0-3,12-15,20-27} / {4-11,16-19,28-31}, +32), so
 // the Shoup-table reads of a group all hit one record's 256-byte table:
 // distinct nibbles are distinct banks, equal ones the same address.  With
 // contiguous lanes a group mixes two records' tables and their reads collide.
-#ifndef BSSL_AMD_SIV_GROUP
-#define BSSL_AMD_SIV_GROUP 1
-#endif
-// BSSL_AMD_SIV_DEFER = 1 (with SPLIT): gmul4d, one reduction per chain.
-#ifndef BSSL_AMD_SIV_DEFER
-#define BSSL_AMD_SIV_DEFER 1
-#endif
-// BSSL_AMD_SIV_FASTRED = 1: the Shoup step's 4-bit reduction as shifts of
-// the top nibble (red4_hi) instead of four multiplies.
-#ifndef BSSL_AMD_SIV_FASTRED
-#define BSSL_AMD_SIV_FASTRED 1
-#endif
-// BSSL_AMD_SIV_CTRCACHE = 1: counter-window caching of rounds 1-2 in the
-// seal keystream pass (CtrWindow).  Parity-tested; off because it measured
-// no faster (502-503 vs 505 GiB/s, configS): the keystream pass's lookups are
-// not what binds this kernel.
-#ifndef BSSL_AMD_SIV_CTRCACHE
-#define BSSL_AMD_SIV_CTRCACHE 0
-#endif
+// And the Shoup step's 4-bit reduction as shifts of the top nibble (red4_hi)
+// instead of four multiplies.  (Counter-window caching of rounds 1-2 in the
+// seal keystream pass measured no faster, 502-503 vs 505 GiB/s: the
+// keystream pass's lookups are not what binds this kernel.)
 constexpr int kL = 16;                // lanes per record
 // One persistent 768-thread workgroup per CU (12 waves: the 168-VGPR budget's
 // 3 waves per SIMD; LDS 64 KiB of tables + 48 record slots = 137 KiB).  Each
@@ -224,21 +206,12 @@ __device__ __forceinline__ uint4 mulx(uint4 v) {
                     (v.w >> 1) | (v.z << 31));
 }
 
-// The reduction of the 4 bits shifted out by Z * x^4, at bits 112..127:
-// clmul(r, 0x1c20) (crypto/fipsmodule/aes/gcm_nohw-style rem_4bit values).
-__device__ __forceinline__ uint32_t red4(uint32_t r) {
-  return ((r & 1) * 0x1c20u) ^ ((r & 2) * 0x1c20u) ^ ((r & 4) * 0x1c20u) ^ ((r & 8) * 0x1c20u);
-}
 // red4(z3 & 0xf) << 16 without the multiplies: with u = z3 << 28 (the four
 // bits at the top), clmul(r, 0x1c20) << 16 = r<<28 ^ r<<27 ^ r<<26 ^ r<<21
 // = u ^ u>>1 ^ u>>2 ^ u>>7 (0x1c20 = bits 5, 10, 11, 12).
 __device__ __forceinline__ uint32_t red4_hi(uint32_t z3) {
-#if BSSL_AMD_SIV_FASTRED
   const uint32_t u = z3 << 28;
   return u ^ (u >> 1) ^ (u >> 2) ^ (u >> 7);
-#else
-  return red4(z3 & 0xf) << 16;
-#endif
 }
 
 // X * H^k with M = the 16-entry table of H^k (Shoup 4-bit, nibbles from the
@@ -269,34 +242,6 @@ __device__ __forceinline__ uint4 mulx32(uint4 z) {
                     z.y, z.z);
 }
 
-// gmul as four independent 8-nibble Shoup chains, one per word of X
-// (X * H = sum_g x^(32 g) * (word g of X) * H), joined by Horner in x^32: the
-// same 32 table reads, a quarter of the dependent-latency chain.
-__device__ __forceinline__ uint4 gmul4(uint4 X, const uint4 *M) {
-  uint32_t z[4][4];
-  const uint32_t w[4] = {X.x, X.y, X.z, X.w};
-#pragma unroll
-  for (int g = 0; g < 4; g++) z[g][0] = z[g][1] = z[g][2] = z[g][3] = 0;
-#pragma unroll
-  for (int k = 7; k >= 0; k--) {
-#pragma unroll
-    for (int g = 0; g < 4; g++) {
-      const uint32_t nib = (w[g] >> (28 - 4 * k)) & 0xf;
-      const uint32_t r = red4_hi(z[g][3]);
-      z[g][3] = __builtin_amdgcn_alignbit(z[g][2], z[g][3], 4);
-      z[g][2] = __builtin_amdgcn_alignbit(z[g][1], z[g][2], 4);
-      z[g][1] = __builtin_amdgcn_alignbit(z[g][0], z[g][1], 4);
-      z[g][0] = (z[g][0] >> 4) ^ r;
-      const uint4 m = M[nib];
-      z[g][0] ^= m.x; z[g][1] ^= m.y; z[g][2] ^= m.z; z[g][3] ^= m.w;
-    }
-  }
-  uint4 acc = make_uint4(z[3][0], z[3][1], z[3][2], z[3][3]);
-#pragma unroll
-  for (int g = 2; g >= 0; g--)
-    acc = xor4(mulx32(acc), make_uint4(z[g][0], z[g][1], z[g][2], z[g][3]));
-  return acc;
-}
 
 // gmul4 with the reduction deferred: each 8-step chain shifts its 32
 // spilled bits into a fifth word instead of reducing 4 bits per step, and
@@ -335,7 +280,7 @@ __device__ __forceinline__ uint4 gmul4d(uint4 X, const uint4 *M) {
   return acc;
 }
 
-// Record lanes: lane q of the record in slot `slot` (BSSL_AMD_SIV_GROUP).
+// Record lanes: lane q of the record in slot `slot` (ds_read_b128 lane groups).
 // Lane within the 32-lane half of the record's q-th lane (set B = the
 // {4-11,16-19,28-31} group).
 __device__ __forceinline__ int group_lane(int setb, int q) {
@@ -344,23 +289,17 @@ __device__ __forceinline__ int group_lane(int setb, int q) {
 struct RecLanes {
   int q, slot, setb, half;  // half = lane & 32
   __device__ int src(int i) const {  // wave lane of the record's lane i
-    return BSSL_AMD_SIV_GROUP ? half + group_lane(setb, i) : (threadIdx.x & 63 & ~(kL - 1)) + i;
+    return half + group_lane(setb, i);
   }
 };
 __device__ __forceinline__ RecLanes rec_lanes() {
   RecLanes r;
   const int t = threadIdx.x;
-  if (BSSL_AMD_SIV_GROUP) {
-    const int l = t & 31;
-    r.setb = (l >= 4 && l < 12) || (l >= 16 && l < 20) || l >= 28;
-    r.q = r.setb ? (l < 12 ? l - 4 : l < 20 ? l - 8 : l - 16)
-                 : (l < 4 ? l : l < 16 ? l - 8 : l - 12);
-    r.slot = 2 * (t >> 5) + r.setb;
-  } else {
-    r.setb = 0;
-    r.q = t & (kL - 1);
-    r.slot = t / kL;
-  }
+  const int l = t & 31;
+  r.setb = (l >= 4 && l < 12) || (l >= 16 && l < 20) || l >= 28;
+  r.q = r.setb ? (l < 12 ? l - 4 : l < 20 ? l - 8 : l - 16)
+               : (l < 4 ? l : l < 16 ? l - 8 : l - 12);
+  r.slot = 2 * (t >> 5) + r.setb;
   r.half = t & 32;
   return r;
 }
@@ -399,17 +338,7 @@ __device__ __forceinline__ void store_block(uint8_t *p, uint4 v, uint64_t avail)
 // block (POLYVAL's ByteReverse, e_aesgcmsiv.cc:624-629).
 __device__ __forceinline__ uint4 rev(uint4 x) { return make_uint4(x.w, x.z, x.y, x.x); }
 
-#ifndef BSSL_AMD_SIV_WPE
-#define BSSL_AMD_SIV_WPE 3  // 168 VGPRs, 3 waves per SIMD: +14 % over the unconstrained 190
-#endif
-#if BSSL_AMD_SIV_WPE
-#define SIV_OCC __attribute__((amdgpu_waves_per_eu(BSSL_AMD_SIV_WPE)))
-#else
-#define SIV_OCC
-#endif
-#ifndef BSSL_AMD_SIV_META_BRANCH
-#define BSSL_AMD_SIV_META_BRANCH 0
-#endif
+#define SIV_OCC __attribute__((amdgpu_waves_per_eu(3)))
 __device__ const uint64_t kSivMetaZero[2] = {0, 0};
 
 template <typename T>
@@ -441,16 +370,6 @@ __device__ __forceinline__ void siv_record(const GcmKeyDev *__restrict__ keys, c
   const bool active = rec < b.num_records;
   uint64_t off = 0, len = 0, ad_off = 0, ad_len = 0;
   uint32_t kidx = 0;
-#if BSSL_AMD_SIV_META_BRANCH  // (the round-1 form, for A/B)
-  if (active) {
-    off = b.offsets ? b.offsets[rec] : rec * b.record_stride;
-    len = b.lengths ? b.lengths[rec] : b.record_len;
-    ad_off = b.ad_offsets ? b.ad_offsets[rec] : rec * b.ad_stride;
-    ad_len = b.ad_lengths ? b.ad_lengths[rec] : b.ad_len;
-    kidx = b.key_index ? b.key_index[rec] : 0u;
-  }
-  const uint8_t vld = active && b.valid ? b.valid[rec] : 1;
-#else
   // Branch-free: a missing array is read at kSivMetaZero, so these loads and
   // the nonce's are in flight together (under the null-pointer branches hipcc
   // waited for each before issuing the next).
@@ -476,7 +395,6 @@ __device__ __forceinline__ void siv_record(const GcmKeyDev *__restrict__ keys, c
     }
     vld = siv_meta(b.valid, rec, active);
   }
-#endif
   // e_aesgcmsiv.cc:794-808, 830-846.
   const bool live = active && kidx < b.num_keys && b.nonce_len == 12 && b.tag_len == 16 &&
                     len <= (uint64_t(1) << 36) && ad_len < (uint64_t(1) << 61) &&
@@ -613,13 +531,7 @@ __device__ __forceinline__ void siv_record(const GcmKeyDev *__restrict__ keys, c
       blk = make_uint4((uint32_t)abits, (uint32_t)(abits >> 32), (uint32_t)mbits,
                        (uint32_t)(mbits >> 32));
     }
-#if BSSL_AMD_SIV_SPLIT && BSSL_AMD_SIV_DEFER
     acc = any ? xor4(gmul4d(acc, L.m[slot][kPows - 1]), rev(blk)) : rev(blk);
-#elif BSSL_AMD_SIV_SPLIT
-    acc = any ? xor4(gmul4(acc, L.m[slot][kPows - 1]), rev(blk)) : rev(blk);
-#else
-    acc = any ? xor4(gmul(acc, L.m[slot][kPows - 1]), rev(blk)) : rev(blk);
-#endif
     any = true;
     jlast = j;
   }
@@ -653,11 +565,6 @@ __device__ __forceinline__ void siv_record(const GcmKeyDev *__restrict__ keys, c
     // gcm_siv_crypt from the tag (e_aesgcmsiv.cc:817).
     ctr0 = tag;
     ctr0.w |= 0x80000000u;
-#if BSSL_AMD_SIV_CTRCACHE
-    const uint4 r0 = rk[0];
-    const uint32_t s1 = ctr0.y ^ r0.y, s2 = ctr0.z ^ r0.z, s3 = ctr0.w ^ r0.w;
-    CtrWindow wc;
-#endif
     if constexpr (IOV) {
       iov_walk_init(wl, b, rec);
       iov_walk_init(ws, b, rec);
@@ -669,13 +576,7 @@ __device__ __forceinline__ void siv_record(const GcmKeyDev *__restrict__ keys, c
         x = iov_walk_load(wl, b, rec, 16 * p, pn, 16 * kL);
       else
         x = load_block(src + 16 * p, len - 16 * p);
-#if BSSL_AMD_SIV_CTRCACHE
-      const uint32_t s0 = (ctr0.x + (uint32_t)p) ^ r0.x;
-      wc.update(s0, s1, s2, s3, rk, L);
-      const uint4 ks = wc.block<NR>(s0, rk, L);
-#else
       const uint4 ks = aes_enc<NR>(make_uint4(ctr0.x + (uint32_t)p, ctr0.y, ctr0.z, ctr0.w), rk, L);
-#endif
       if constexpr (IOV)
         iov_walk_store(ws, b, rec, 16 * p, mask_block(xor4(x, ks), pn), pn, 16 * kL);
       else

@@ -2,7 +2,7 @@
 # the current library (main) and each variant build (boringssl_amd/csrc/build/<v>),
 # --no-parity (A/B timing only; parity is tested separately).
 set -e
-mkdir -p gpurun_out/ab
+mkdir -p gpurun_out/ab; rm -f gpurun_out/ab/*.log
 B=boringssl_amd/csrc/build
 for spec in $SPECS; do
   CFG=${spec%%:*}; VARS=$(echo ${spec#*:} | tr ',' ' ')
