@@ -395,8 +395,11 @@ def load_profile(config, kernel_prefix):
         return None, None
     try:
         d = json.load(open(p)).get(config, {})
+        # (the keyset kernel of config 5 is a gcm_kernel for the bench line)
+        family = ("gcm_kernel", "gcm_keyset_kernel") if kernel_prefix == "gcm_kernel" else \
+            (kernel_prefix,)
         for k, v in d.items():
-            if k.startswith(kernel_prefix):
+            if isinstance(v, dict) and k.startswith(family):
                 cb = {x: round(v[x], 3) for x in ("lds_busy", "valu_busy") if x in v}
                 if cb:
                     cb["source"] = f"profiles/traffic.json[{config}] (rocprofv3 PMC)"

@@ -307,12 +307,15 @@ bool check_batch(const EVP_AEAD *aead, const BSSL_AMD_BATCH *b) {
 // ---- single-record helper: host buffers -> one-record device batch --------
 
 // Per-thread staging buffers and stream of the host-buffer calls, one set per
-// device (a thread may use contexts of several GPUs): device memory for the
-// one-record batch and a pinned host mirror of it, so a call is one H2D and
-// one D2H DMA copy (pageable copies cost ~10 us each).
+// device (a thread may use contexts of several GPUs): a pinned, mapped host
+// buffer -- records up to one_record_map_max() are read and written by the
+// kernel in place through its device address (`mapped`), with no DMA copy --
+// and device memory for longer records, which take one H2D and one D2H copy
+// through the pinned buffer (pageable copies cost ~10 us each).
 struct Scratch {
   uint8_t *dev = nullptr;
   uint8_t *host = nullptr;
+  uint8_t *mapped = nullptr;  // device address of `host`
   size_t cap = 0;
   hipStream_t stream = nullptr;
   int device = -1;  // the device that owns dev/stream (set on first use)
@@ -342,17 +345,31 @@ Scratch *scratch(size_t bytes) {
   if (sc.cap < bytes) {
     if (sc.dev) hipFree(sc.dev);
     if (sc.host) hipHostFree(sc.host);
-    sc.dev = sc.host = nullptr;
+    sc.dev = sc.host = sc.mapped = nullptr;
     sc.cap = 0;
     size_t cap = bytes < (1u << 20) ? (1u << 20) : bytes;
     if (hipMalloc(&sc.dev, cap) != hipSuccess) {
       sc.dev = nullptr;
       return nullptr;
     }
-    if (hipHostMalloc(&sc.host, cap, hipHostMallocDefault) != hipSuccess) {
+#ifndef HOSTMEM_FLAGS
+#define HOSTMEM_FLAGS hipHostMallocMapped
+#endif
+#ifndef HOSTMEM_DEVPTR
+#define HOSTMEM_DEVPTR 1
+#endif
+    if (hipHostMalloc(&sc.host, cap, HOSTMEM_FLAGS) != hipSuccess) {
       sc.host = nullptr;
       hipFree(sc.dev);
       sc.dev = nullptr;
+      return nullptr;
+    }
+    if (!HOSTMEM_DEVPTR) sc.mapped = sc.host;
+    else if (hipHostGetDevicePointer(reinterpret_cast<void **>(&sc.mapped), sc.host, 0) !=
+        hipSuccess) {
+      hipHostFree(sc.host);
+      hipFree(sc.dev);
+      sc.host = sc.dev = nullptr;
       return nullptr;
     }
     sc.cap = cap;
@@ -399,7 +416,7 @@ int one_record(const EVP_AEAD_CTX *ctx, bool open, const uint8_t *in, uint8_t *o
   // copies, whose two launches and completions were most of a short record's
   // latency.  Longer records take one H2D and one D2H copy.
   const bool mapped = len <= one_record_map_max();
-  uint8_t *h = sc->host, *d = mapped ? sc->host : sc->dev;
+  uint8_t *h = sc->host, *d = mapped ? sc->mapped : sc->dev;
   if (nonce_len) memcpy(h + o_nonce, nonce, nonce_len);
   if (ad_len) memcpy(h + o_ad, ad, ad_len);
   if (open && tag_len) memcpy(h + o_tag, tag, tag_len);

@@ -3,7 +3,7 @@
 // column h in its low 16 bits (block n in bit n) and for column h + 2 in its
 // high 16 bits (block n in bit 16 + n): 64 VGPRs of state, and every SubBytes
 // / MixColumns operation still works on 32 bit-slots.  See gcm.hip
-// (gcm_mix_kernel) and DESIGN.md §4.2c.
+// (process_records_bs16, gcm_prologue_bs16) and DESIGN.md §4.2b.
 #pragma once
 #include "bs_aes.h"
 
@@ -48,17 +48,19 @@ __device__ __forceinline__ void bs16_mix(const uint32_t a[4][8], uint32_t o[4][8
 // AES rounds 1..NR on the 16-block register pairs (round 0 is in p already).
 // Row r of new pair h comes from old pair (h + r) & 1, half-swapped when
 // ((h + r) >> 1) & 1 (ShiftRows on the column pairs {h, h + 2}).
-// Round keys: the FIPS-197 words of round rd (wave-uniform), spread into the
-// per-register masks on the scalar unit.  (A per-key table of the 64 masks
-// per round, read by scalar loads, measured the same.)
-template <int NR>
+// Round keys: the FIPS-197 words of round rd, wave-uniform (UNIFORM: spread
+// into the per-register masks on the scalar unit; a per-key table of the 64
+// masks per round, read by scalar loads, measured the same) or per lane (the
+// prologue's E_K(J0) of keyset records: masks on the VALU).
+template <int NR, bool UNIFORM = true>
 __device__ __forceinline__ void bs16_cipher(uint32_t (&p)[4][2][8],
                                             const uint32_t *__restrict__ rkp) {
 #pragma unroll 1
   for (int rd = 1; rd <= NR; rd++) {
     uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; i++) w[i] = (uint32_t)__builtin_amdgcn_readfirstlane(rkp[4 * rd + i]);
+    for (int i = 0; i < 4; i++)
+      w[i] = UNIFORM ? (uint32_t)__builtin_amdgcn_readfirstlane(rkp[4 * rd + i]) : rkp[4 * rd + i];
     auto kmask = [&](int r, int h, int b) { return bs16_kmask(w, r, h, b); };
     const bool last = rd == NR;
     uint32_t np[4][2][8];

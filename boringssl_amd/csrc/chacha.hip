@@ -59,15 +59,8 @@ struct ChaState {
   uint32_t x[16];
 };
 
-// d = rotl(d ^ a, 16) as two SDWA XORs (one per 16-bit half, the halves
-// swapped) instead of an XOR and a v_alignbit_b32 (diagnostic knob; the
-// alignbit is one of the slow-issue VALU instructions).
-__device__ __forceinline__ uint32_t xor_rot16(uint32_t d, uint32_t a) {
-  return rotl(d ^ a, 16);
-}
-
 #define QR(a, b, c, d)                 \
-  a += b; d = xor_rot16(d, a);         \
+  a += b; d = rotl(d ^ a, 16);         \
   c += d; b = rotl(b ^ c, 12);         \
   a += b; d = rotl(d ^ a, 8);          \
   c += d; b = rotl(b ^ c, 7);
@@ -391,22 +384,21 @@ __device__ __forceinline__ void crypt_block_x(const uint8_t *src, uint8_t *dst, 
 // Horner's rule in R = r^4 at stride L (multiplier R^L), then the rotation +
 // log2(L)-level tree of gcm.hip's lane algebra.
 // iovec records: the lane's whole block comes by LDS-DMA into the wave's
-// staging area (1) or by four dwordx4 loads held in VGPRs across the rounds (0).
-#define CHACHA_OCC __attribute__((amdgpu_waves_per_eu(L == 2 ? 3 : 4)))
-// Coalesced record I/O for L = 4 (default): a wave's loads and stores move
-// 256 contiguous bytes per record per instruction (lane = 16-byte chunk of a
-// record's 4-block run), staged through LDS to the lane that owns each
-// 64-byte block.  With the lane-per-block pattern (0) each 16-byte access
-// sits at a 64-byte lane stride: the same copy costs 1.32x the time and
-// 1.3x the counted HBM bytes (tools/micro/calib_copy.hip).
-// Slot shift for 128-byte-aligned records (see `sh` in chacha_group).
-// Ciphertext stores with the non-temporal hint: +2.3 % on config 3 (same-box
-// A/B); NT_LOAD sets the non-temporal cache policy on the LDS-DMA loads.
-// Diagnostic ablations (wrong output; selected builds only): 1 = no input
-// loads in the block loop, 2 = no Poly1305 absorb in the loop, 3 = no ChaCha
-// rounds in the loop, 4 = no stores in the loop (lane-per-block I/O); with
-// the record-contiguous I/O: 7 = no loads, 8 = no global stores in the loop
-// (the staged values are still read back).
+// staging area (loading it into VGPRs across the rounds measured the same).
+#ifndef CHACHA_AP_SPLIT
+#define CHACHA_AP_SPLIT 0
+#endif
+#ifndef CHACHA_WPE2
+#define CHACHA_WPE2 3
+#endif
+#define CHACHA_OCC __attribute__((amdgpu_waves_per_eu(L == 2 ? CHACHA_WPE2 : 4)))
+// Record-contiguous I/O (COAL): a wave's loads and stores move whole
+// per-record runs (L = 2: 8 records x 128 bytes per instruction), staged
+// through LDS to the lane that owns each 64-byte block.  With the
+// lane-per-block pattern each 16-byte access sits at a 64-byte lane stride:
+// the same copy costs 1.32x the time and 1.3x the counted HBM bytes
+// (tools/micro/calib_copy.hip).  Ciphertext stores carry the non-temporal
+// hint (+2.3 % on config 3, same-box A/B).
 // Per-record metadata without branches: a missing array (null pointer, the
 // uniform-layout fields apply) is read at kMetaZero instead, so every load is
 // issued unconditionally and they are all in flight together.  (Under the
@@ -975,6 +967,22 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     const uint64_t d = u - 1 - sh;
     if (d < nunits) {
       PAcc t = pacc_zero();
+#if CHACHA_AP_SPLIT
+      uint32_t slot = threadIdx.x / L;
+      asm volatile("" : "+v"(slot));  // re-read per block, not hoisted (registers)
+      const uint32_t *apw32 = reinterpret_cast<const uint32_t *>(s_apow[slot]);
+      auto mult = [&](int k, const P &a) {
+        uint32_t ap[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) ap[i] = apw32[9 * k + i];
+        pmac_s(t, a, ap, ap + 5);
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      mult(0, acc);
+      mult(1, pblock(c[0], c[1], c[2], c[3]));
+      mult(2, pblock(c[4], c[5], c[6], c[7]));
+      mult(3, pblock(c[8], c[9], c[10], c[11]));
+#else
       uint32_t ap[36];
       {
         uint32_t slot = threadIdx.x / L;
@@ -989,6 +997,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
       pmac_s(t, pblock(c[0], c[1], c[2], c[3]), ap + 9, ap + 14);
       pmac_s(t, pblock(c[4], c[5], c[6], c[7]), ap + 18, ap + 23);
       pmac_s(t, pblock(c[8], c[9], c[10], c[11]), ap + 27, ap + 32);
+#endif
       acc = padd(preduce(t), pblock(c[12], c[13], c[14], c[15]));
     } else {
       P tt = pblock(c[0], c[1], c[2], c[3]);

@@ -605,7 +605,9 @@ __device__ __forceinline__ uint32_t row_xor(uint32_t v) {
   return v;
 }
 
-// Per-record state handed from the prologue to the bulk kernel (64 bytes).
+// Per-record state handed from the bs16 engine's prologue (gcm_prologue_bs16)
+// to its bulk kernels (64 bytes; the T-table kernels start their records
+// themselves).
 struct alignas(16) RecState {
   uint4 j0;   // pre-counter block J0 (gcm.cc.inc:316-338)
   uint4 ek0;  // E_K(J0)
@@ -641,7 +643,7 @@ __device__ __forceinline__ Gf128 gf_xor(Gf128 a, Gf128 b) {
 }
 
 // ---------------------------------------------------------------------------
-// One AES block with T0 alone, replicated once per LDS bank (prologue):
+// One AES block with T0 alone, replicated once per LDS bank (one-record kernel):
 // entry x for lane l at tab[x * 32 + (l & 31)] (32 KiB), so every lookup of a
 // wave is bank-conflict free whatever the index -- the same constant-time
 // argument as the bulk kernel's tables, at half their size
@@ -679,72 +681,6 @@ __device__ __forceinline__ uint4 aes_block_rep(uint4 in, const RoundKeys &rk, co
   };
   return make_uint4(last(s0, s1, s2, s3, rk.w[NR][0]), last(s1, s2, s3, s0, rk.w[NR][1]),
                     last(s2, s3, s0, s1, rk.w[NR][2]), last(s3, s0, s1, s2, rk.w[NR][3]));
-}
-
-// ---------------------------------------------------------------------------
-// Prologue: one thread per record.  J0 (incl. the GHASH-derived J0 of a
-// non-96-bit nonce), E_K(J0) and the AD hash -- the per-record constant work
-// of CRYPTO_gcm128_init_ctx / _aad (gcm.cc.inc:298-398).  Constant time: AES
-// from the bank-replicated T0, GHASH products by gf_mul (gf128_ct.h).
-template <int NR>
-__global__ __launch_bounds__(256) void gcm_prologue(const GcmKeyDev *__restrict__ keys,
-                                                    BatchDesc b, RecState *__restrict__ st) {
-  __shared__ uint32_t t0tab[256 * 32];
-  for (int e = threadIdx.x; e < 256 * 32; e += blockDim.x) t0tab[e] = kTables.te0[e >> 5];
-  __syncthreads();
-  const uint64_t rec = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (rec >= b.num_records) return;
-  const RecordMeta m = record_meta(b, rec);
-  const uint32_t k = b.key_index ? b.key_index[rec] : 0u;
-  // e_aes.cc.inc:790 (empty nonce), gcm.cc.inc:368,409 (length limits).
-  const bool live = k < b.num_keys && b.nonce_len != 0 &&
-                    m.len + m.xlen <= ((uint64_t(1) << 36) - 32) &&
-                    m.ad_len <= (uint64_t(1) << 61) &&
-                    (!b.valid || b.valid[rec]);  // tls12/tls13 nonce check (tls_scan.hip)
-  RecState s;
-  s.live = live;
-  s.pad[0] = s.pad[1] = s.pad[2] = 0;
-  s.j0 = s.ek0 = s.ya = make_uint4(0, 0, 0, 0);
-  if (live) {
-    const GcmKeyDev *kp = keys + k;
-    const Gf128 h1 = gf_load(kp->hpow_ct[1]);
-    RoundKeys rk;
-#pragma unroll
-    for (int r = 0; r <= NR; r++)
-#pragma unroll
-      for (int c = 0; c < 4; c++) rk.w[r][c] = kp->rk[r][c];
-    const uint8_t *nonce = b.nonces + rec * b.nonce_len;
-    uint4 j0;
-    if (b.nonce_len == 12) {
-      j0 = load_partial(nonce, 12);
-      j0.w = 0x01000000u;  // be32(1)
-    } else {
-      // GHASH(N || 0^s || [len(N)]_64) (gcm.cc.inc:320-338).
-      Gf128 y = {{0, 0, 0, 0}};
-      for (uint64_t o = 0; o < b.nonce_len; o += 16)
-        y = gf_mul(gf_xor(y, to_gf(load_partial(nonce + o,
-                                                (uint32_t)min<uint64_t>(b.nonce_len - o, 16)))),
-                   h1);
-      const uint64_t bits = b.nonce_len << 3;
-      y.w[0] ^= (uint32_t)bits;
-      y.w[1] ^= (uint32_t)(bits >> 32);
-      j0 = from_gf(gf_mul(y, h1));
-    }
-    s.j0 = j0;
-    s.ek0 = aes_block_rep<NR>(j0, rk, t0tab);
-    // Exclusive GHASH of the AD, sum A_k H^(m-1-k) (the lanes' element 0).
-    const uint8_t *ad = b.ad + m.ad_off;
-    Gf128 ya = {{0, 0, 0, 0}};
-    for (uint64_t o = 0; o < m.ad_len; o += 16) {
-      const uint32_t n = (uint32_t)min<uint64_t>(m.ad_len - o, 16);
-      const Gf128 blk = to_gf(b.aadvecs ? ivec_load16(b.aadvecs, b.aadvec_start[rec],
-                                                      b.aadvec_start[rec + 1], o, n)
-                                        : load_partial(ad + o, n));
-      ya = o ? gf_xor(gf_mul(ya, h1), blk) : blk;
-    }
-    s.ya = from_gf(ya);
-  }
-  st[rec] = s;
 }
 
 // ---------------------------------------------------------------------------
@@ -946,7 +882,6 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
                                                 const GcmKeyDev *key, uint32_t lc0, uint32_t lc1,
                                                 int prio_base = 0) {
   static_assert(L == 16 || L == 8, "lanes per record");
-  static_assert(!(IOV && L != 16), "iovec records: 16 lanes");
   const int q = threadIdx.x & (L - 1);
   const uint64_t rec = in.rec;
   const bool active = in.active, live = in.live;
@@ -1227,7 +1162,7 @@ __device__ __forceinline__ void fill_aes_tables(uint8_t *smem, int tid) {
 // that the SIMD arbiter favours (older waves issue first) simply process more
 // units instead of waiting at a per-tile barrier for the slowest wave
 // (DESIGN.md §4.2).  L: lanes per record -- 8 (8 records per wave, GHASH
-// stride H^8) for every one-key batch but iovec batches, 16 for those.
+// stride H^8) for every one-key batch; the keyset kernel keeps 16.
 // (A kernel of its own, apart from the keyset kernel, so each gets its own
 // register allocation.)
 template <int NR, bool OPEN, bool XT, int W, bool IOV = false, int L = 16>
@@ -1341,6 +1276,149 @@ __global__ __launch_bounds__(1024) void gcm_keyset_kernel(const GcmKeyDev *__res
 }
 
 // ---------------------------------------------------------------------------
+// One record: the host-buffer calls (EVP_AEAD_CTX_seal / open / seal_scatter,
+// aead.cc.inc:163-209 -- SSLAEADContext::SealScatter makes them one record at
+// a time, ssl/ssl_aead_ctx.cc:299-381) as one launch of one workgroup with no
+// unit counter and no 128 KiB table build.  Thread t encrypts counter block t
+// (records up to kOneMaxBlocks), every load in flight at once (the record may
+// sit in mapped host memory); AES from T0 replicated per bank (32 KiB, as the
+// prologue's); GHASH by lanes 0..15 at stride 16 with the key's nibble table
+// of H^16 in LDS (8 KiB): in each lookup all 16 lanes read the same nibble
+// position, so a lane's bank is its nibble value's and equal values share an
+// address -- conflict-free whatever the data.  Open computes the tag first and
+// writes the plaintext (or zeros) after the check.
+constexpr int kOneMaxBlocks = 1024;  // 16 KiB: threads per workgroup
+
+// x * H^16 from the nibble table (key_setup.cc layout: position 2k = the high
+// nibble of byte k, 2k + 1 the low one).
+__device__ __forceinline__ uint4 nib_mul16(uint4 x, const uint4 *htab) {
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+  uint4 r = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const uint32_t byte = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+    r = xor4_3(r, htab[(2 * k) * 16 + (byte >> 4)], htab[(2 * k + 1) * 16 + (byte & 15u)]);
+  }
+  return r;
+}
+
+template <int NR, bool OPEN>
+__global__ __launch_bounds__(kOneMaxBlocks) void gcm_one_kernel(const GcmKeyDev *__restrict__ keys,
+                                                                BatchDesc b) {
+  __shared__ uint32_t t0tab[256 * 32];
+  __shared__ uint4 htab[32 * 16];
+  __shared__ uint4 cblk[kOneMaxBlocks];
+  __shared__ uint4 s_lh;  // len block x H ^ E_K(J0), from wave 1
+  __shared__ uint32_t s_ok;
+  const int t = threadIdx.x;
+  const GcmKeyDev *key = keys;
+  const RecordMeta m = record_meta(b, 0);
+  const bool live = record_live(b, 0, m);
+  const uint8_t *src = b.in + m.off;
+  uint8_t *dst = b.out + m.off;
+  // Every load of the record (it may sit in mapped host memory, one PCIe
+  // round trip each) is issued first, together: this thread's block, and for
+  // wave 0 the nonce and the first AD block.
+  const uint32_t nbytes = (uint32_t)m.len;  // (<= 16 KiB: the launcher checks)
+  const uint32_t nb = (nbytes + 15) / 16;
+  const uint32_t n = (uint32_t)t < nb ? min(nbytes - 16u * t, 16u) : 0u;
+  uint4 x = make_uint4(0, 0, 0, 0);
+  if (n == 16)
+    x = load16_any(src + 16 * t);
+  else if (n)
+    x = load_partial(src + 16 * t, n);
+  uint4 ad0 = make_uint4(0, 0, 0, 0), nonce = make_uint4(0, 0, 0, 0);
+  if (t < 128) {
+    if (live && m.ad_len) ad0 = ad_block(b, 0, m, 0);
+    if (live && b.nonce_len == 12) nonce = load_partial(b.nonces, 12);
+  }
+  for (int e = t; e < 256 * 32; e += kOneMaxBlocks) t0tab[e] = kTables.te0[e >> 5];
+  if (t < 32 * 16) htab[t] = reinterpret_cast<const uint4 *>(key->htab16)[t];
+  RoundKeys rk;
+#pragma unroll
+  for (int r = 0; r <= NR; r++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) rk.w[r][c] = key->rk[r][c];
+  const uint4 j0 = !live ? make_uint4(0, 0, 0, 0)
+                   : b.nonce_len == 12 ? make_uint4(nonce.x, nonce.y, nonce.z, 0x01000000u)
+                                       : record_j0(b, 0, key->hpow_ct);
+  const uint32_t ctr0 = bswap32(j0.w);
+  __syncthreads();
+  const uint4 ks =
+      aes_block_rep<NR>(make_uint4(j0.x, j0.y, j0.z, bswap32(ctr0 + 1u + (uint32_t)t)), rk, t0tab);
+  const uint4 y = mask_block(xor4(x, ks), n);
+  if (!OPEN && n) {  // seal: the ciphertext (zeros for a dead record, aead.cc.inc:170-179)
+    if (n == 16)
+      store16_any(dst + 16 * t, live ? y : make_uint4(0, 0, 0, 0));
+    else
+      store_partial(dst + 16 * t, live ? y : make_uint4(0, 0, 0, 0), n);
+  }
+  cblk[t] = OPEN ? x : y;  // the GHASH input is the ciphertext
+  uint4 ya = make_uint4(0, 0, 0, 0);
+  if (t < 64) {
+    ya = m.ad_len > 16 ? record_ad_hash<16>(b, 0, m, live, true, key->hpow_ct) : ad0;
+  } else if (t < 128) {
+    // Wave 1, meanwhile: the tag's record-independent part, len block x H ^
+    // E_K(J0) (gcm.cc.inc:576-604, 340-343).
+    Gf128 lb = {{(uint32_t)(m.len << 3), (uint32_t)(m.len >> 29), (uint32_t)(m.ad_len << 3),
+                 (uint32_t)(m.ad_len >> 29)}};
+    const uint4 lh = xor4(from_gf(gf_mul(lb, gf_load(key->hpow_ct[1]))),
+                          aes_block_rep<NR>(j0, rk, t0tab));
+    if (t == 64) s_lh = lh;
+  }
+  __syncthreads();
+  if (t < 16) {
+    const int q = t;
+    uint4 acc = (q == 15 && live) ? ya : make_uint4(0, 0, 0, 0);
+    const uint32_t iters = live ? (nb + 15) / 16 : 0u;
+    for (uint32_t it = 0; it < iters; it++) {
+      const uint32_t j = 16 * it + q;
+      const uint4 h = nib_mul16(acc, htab);
+      if (j < nb) acc = xor4(h, cblk[j]);
+    }
+    // Record end (finish_record's algebra) with the tag's last x H folded into
+    // the lane weights: tag = sum_q acc_q H^(17-p) ^ len x H ^ E_K(J0).
+    const int r = (int)((nb + 1) & 15);
+    const int p = (q - r + 1) & 15;
+    Gf128 z = gf_mul(to_gf(acc), gf_load(key->hpow_ct[17 - p]));
+#pragma unroll
+    for (int i = 0; i < 4; i++) z.w[i] = row_xor16(z.w[i]);
+    const uint4 tag = xor4(from_gf(z), s_lh);
+    if (q == 0) {
+      uint8_t *tagp = batch_tag(b, 0);
+      int ok = live;
+      if (OPEN && live) {
+        // CRYPTO_memcmp (e_aes.cc.inc:860-864)
+        const uint4 tr = load_partial(tagp, b.tag_len);
+        const uint4 mine = mask_block(tag, b.tag_len);
+        ok = ((tr.x ^ mine.x) | (tr.y ^ mine.y) | (tr.z ^ mine.z) | (tr.w ^ mine.w)) == 0;
+      }
+      if (!OPEN) store_partial(tagp, ok ? tag : make_uint4(0, 0, 0, 0), b.tag_len);
+      if (b.status) b.status[0] = ok ? 1 : 0;
+      s_ok = (uint32_t)ok;
+    }
+  }
+  if (OPEN) {
+    __syncthreads();
+    if (n) {  // the plaintext, or zeros after a failed check (aead.cc.inc:539-547)
+      const uint4 o = s_ok ? y : make_uint4(0, 0, 0, 0);
+      if (n == 16)
+        store16_any(dst + 16 * t, o);
+      else
+        store_partial(dst + 16 * t, o, n);
+    }
+  }
+}
+
+// Batches the one-record kernel takes: one record of at most 16 KiB, one key,
+// contiguous, no extra bytes.
+bool one_record_batch(const BatchDesc &b) {
+  if (b.num_records != 1 || b.key_index || b.iovecs || b.extra_len) return false;
+  const uint64_t len = b.lengths ? ~uint64_t(0) : b.record_len;  // (arrays: device-resident)
+  return len <= 16u * kOneMaxBlocks;
+}
+
+// ---------------------------------------------------------------------------
 // Table-free engine (opt-in, BSSL_AMD_GCM_MODE=bs16): AES on
 // the VALU only, bitsliced 16 blocks per lane (bs16_aes.h), sharing the
 // T-table kernel's lane algebra, GHASH byte table and finish_record.
@@ -1420,32 +1498,39 @@ __device__ __forceinline__ v32u bs16_words(const uint32_t (&p)[4][2][8], int h) 
 // The (up to) 4 records of a wave with the bs16 engine.  Lane q owns blocks
 // j = 256*c + 16*n + q (n = 0..15) of chunk c -- the T-table role's lane
 // algebra, so GHASH (multiplier H^16, the LDS byte table) and finish_record
-// are shared.  Records must be 16-byte aligned multiples of 16 bytes (the
-// caller checks; no extra bytes).
-template <int NR, bool OPEN>
+// are shared.  Every record shape the T-table kernel takes: any length
+// (a chunk's slots past the record are computed and dropped), any alignment,
+// extra bytes (XT) and iovec records walked in place (IOV, the T-table
+// kernel's cursors at the same 256-byte lane stride).  J0, E_K(J0) (by the
+// bitsliced prologue) and the AD hash come from RecState.
+template <int NR, bool OPEN, bool XT, bool IOV>
 __device__ __forceinline__ void process_records_bs16(const uint32_t *__restrict__ rkp,
                                                      const BatchDesc &b,
-                                                     const RecState *__restrict__ st, uint64_t rec,
-                                                     bool active, const RecordMeta &m0,
-                                                     const uint8_t *smem, const GcmKeyDev *key) {
+                                                     const RecState *__restrict__ st,
+                                                     const UnitIn &in, const uint8_t *smem,
+                                                     const GcmKeyDev *key) {
   // Register budget: the rounds need ~100 VGPRs, so little else may stay live
   // across them -- the per-lane GHASH constants, J0 and the record metadata
   // are re-derived (laundered through empty asm so they are not hoisted)
   // after the rounds and at the end of the record.
-  RecState s;
-  s.j0 = s.ya = make_uint4(0, 0, 0, 0);
-  s.live = 0;
-  if (active) {
-    s.j0 = st[rec].j0;
-    s.ya = st[rec].ya;
-    s.live = st[rec].live;
-  }
-  const bool live = active && s.live;
-  const uint32_t nb = live ? (uint32_t)(m0.len / 16) : 0u;  // nb < 2^32 (GCM length limit)
-  const uint8_t *src = b.in + m0.off;
-  uint8_t *dst = b.out + m0.off;
-  uint4 acc = ((threadIdx.x & 15) == 15 && live) ? s.ya : make_uint4(0, 0, 0, 0);
+  constexpr int L = 16;
+  const uint64_t rec = in.rec;
+  const bool active = in.active;
+  const bool live = active && st[rec].live;
+  const RecordMeta m0 = in.m;
+  const uint32_t nb = live ? (uint32_t)((m0.len + m0.xlen + 15) / 16) : 0u;
+  const uint32_t nfull = live && !IOV ? (uint32_t)(m0.len / 16) : 0u;
+  uint4 acc = ((threadIdx.x & 15) == 15 && live) ? st[rec].ya : make_uint4(0, 0, 0, 0);
   const int nchunks = wave_max((int)((nb + 255) / 256));
+  // iovec cursors (as process_records): chunk index + stream start; between
+  // chunk boundaries only the running pointers move.
+  uint64_t ld_c = 0, ld_cs = 0, st_c = 0, st_cs = 0;
+  const uint8_t *ld_ptr = nullptr;
+  uint8_t *st_ptr = nullptr;
+  int32_t ld_left = -1, st_left = -1;
+  if constexpr (IOV) {
+    if (live) ld_c = st_c = b.iovec_start[rec];
+  }
 #pragma unroll 1
   for (int c = 0; c < nchunks; c++) {
     uint32_t p[4][2][8];
@@ -1490,27 +1575,89 @@ __device__ __forceinline__ void process_records_bs16(const uint32_t *__restrict_
       for (int i = 0; i < 4; i++) v |= (((4u * k + i + q) & 15u) << 4) << (8 * i);
       P[k] = v;
     }
-    auto load_blk = [&](uint32_t j) {
-      return load_blk_nt(src + (uint64_t)(j < nb ? j : 0u) * 16);
-    };
-    uint4 x0 = load_blk(jc);
+    uint64_t rr = rec;
+    asm volatile("" : "+v"(rr));
+    RecordMeta m = m0;
+    asm volatile("" : "+v"(m.off), "+v"(m.len));
+    const uint8_t *src = b.in + m.off;
+    uint8_t *dst = b.out + m.off;
+    const uint8_t *xin = XT ? batch_extra_in(b, rr) : nullptr;
+    uint8_t *xout = XT ? batch_extra_out(b, rr) : nullptr;
     v32u KA = bs16_words(p, 0), KB = bs16_words(p, 1);
     const int nv = (int)min(16u, jc < nb ? (nb - jc + 15u) / 16u : 0u);
-    // Pass 1 (memory): out = in ^ keystream, input one block ahead; the
-    // ciphertext (the output when sealing, the input when opening) replaces
-    // the keystream in KA/KB.
+    // Pass 1 (memory): out = in ^ keystream; the ciphertext (the output when
+    // sealing, the input when opening) replaces the keystream in KA/KB.
 #pragma unroll 1
     for (int n = 0; n < 16; n++) {
       const uint32_t j = jc + 16u * (uint32_t)n;
-      const uint4 x1 = load_blk(j + 16u);  // (past the chunk: clamped, unused)
-      const uint4 y = xor4(x0, make_uint4(KA[n], KB[n], KA[16 + n], KB[16 + n]));
-      if (j < nb) store_blk_nt(dst + (uint64_t)j * 16, y);
-      const uint4 cb = OPEN ? x0 : y;
-      KA[n] = cb.x;
-      KB[n] = cb.y;
-      KA[16 + n] = cb.z;
-      KB[16 + n] = cb.w;
-      x0 = x1;
+      const uint4 ks = make_uint4(KA[n], KB[n], KA[16 + n], KB[16 + n]);
+      uint4 x = make_uint4(0, 0, 0, 0), y;
+      if constexpr (IOV) {
+        const uint64_t pb = (uint64_t)j * 16;
+        const uint32_t nbytes = j < nb ? (uint32_t)min<uint64_t>(m.len - pb, 16) : 0u;
+        const uint64_t c_end = b.iovec_start[rr + 1];
+        if (nbytes) {
+          if (ld_left >= 16 && nbytes == 16) {
+            x = load_blk_nt(ld_ptr);
+          } else {
+            IovCur k;
+            iov_at(k, b, ld_c, ld_cs);
+            iov_seek(k, b, pb, c_end);
+            if (nbytes == 16 && pb + 16 <= k.ce)
+              x = load_blk_nt(k.in + (pb - k.cs));
+            else if (!iov_load2(b, k, pb, nbytes, c_end, x))
+              x = iov_gather(b, k, pb, nbytes, c_end);
+            ld_c = k.c;
+            ld_cs = k.cs;
+            ld_ptr = k.in + (pb - k.cs);
+            ld_left = (int32_t)min<uint64_t>(k.ce - pb, 1u << 30);
+          }
+          ld_ptr += 16 * L;
+          ld_left -= 16 * L;
+          y = mask_block(xor4(x, ks), nbytes);
+          if (st_left >= 16 && nbytes == 16) {
+            store_blk_nt(st_ptr, y);
+          } else {
+            IovCur k;
+            iov_at(k, b, st_c, st_cs);
+            iov_seek(k, b, pb, c_end);
+            if (nbytes == 16 && pb + 16 <= k.ce)
+              store_blk_nt(k.out + (pb - k.cs), y);
+            else if (!iov_store2(b, k, pb, y, nbytes, c_end))
+              iov_scatter(b, k, pb, y, nbytes, c_end);
+            st_c = k.c;
+            st_cs = k.cs;
+            st_ptr = k.out + (pb - k.cs);
+            st_left = (int32_t)min<uint64_t>(k.ce - pb, 1u << 30);
+          }
+          st_ptr += 16 * L;
+          st_left -= 16 * L;
+        } else {
+          y = make_uint4(0, 0, 0, 0);
+        }
+      } else {
+        if (j < nfull) {
+          x = load_blk_nt(src + (uint64_t)j * 16);
+          y = xor4(x, ks);
+          store_blk_nt(dst + (uint64_t)j * 16, y);
+        } else if (j < nb) {
+          const uint32_t nbytes = (uint32_t)min<uint64_t>(m.len + m.xlen - (uint64_t)j * 16, 16);
+          if constexpr (XT) {
+            y = crypt_partial_x(src, dst, m.len, xin, xout, (uint64_t)j * 16, ks, nbytes, x);
+          } else {
+            x = load_partial(src + (uint64_t)j * 16, nbytes);
+            y = mask_block(xor4(x, ks), nbytes);
+            store_partial(dst + (uint64_t)j * 16, y, nbytes);
+          }
+        } else {
+          y = make_uint4(0, 0, 0, 0);
+        }
+      }
+      const uint4 cbk = OPEN ? x : y;
+      KA[n] = cbk.x;
+      KB[n] = cbk.y;
+      KA[16 + n] = cbk.z;
+      KB[16 + n] = cbk.w;
     }
     // Pass 2 (LDS): acc = acc * H^16 ^ C over the lane's valid blocks.
 #pragma unroll 1
@@ -1521,88 +1668,210 @@ __device__ __forceinline__ void process_records_bs16(const uint32_t *__restrict_
   }
   uint64_t rr = rec;
   asm volatile("" : "+v"(rr));
-  RecordMeta m = {0, 0, 0, 0, 0};
-  if (active) {
-    m = record_meta(b, rr);
-    s = st[rr];
-  }
-  finish_record<OPEN, 16>(acc, nb, m, s.ek0, b, rec, active, live, dst, key->hpow_ct);
+  finish_record<OPEN, 16>(acc, nb, m0, st[rr].ek0, b, rr, active, live, b.out + m0.off,
+                          key->hpow_ct);
 }
 
-// Table-free one-key kernel (BSSL_AMD_GCM_MODE=bs16): 16 waves per CU at 128
-// VGPRs, 4-record units from one grid-wide counter.  A unit whose records are
-// all 16-byte-aligned multiples of 16 bytes of >= 4 KiB runs on the bs16
-// engine; any other unit (short, ragged or unaligned records) falls back to
-// the T-table engine, so the tables are still staged.
-template <int NR, bool OPEN>
+// Record inputs of a bs16 unit: the layout only (J0, E_K(J0) and the AD hash
+// are in RecState).
+template <bool XT>
+__device__ __forceinline__ void unit_meta(UnitIn &u, const BatchDesc &b, uint64_t i) {
+  u.active = i < b.num_records;
+  u.rec = u.active ? rec_at(b, i) : 0;
+  u.m = {0, 0, 0, 0, 0};
+  if (u.active) u.m = record_meta(b, u.rec);
+  if constexpr (!XT) u.m.xlen = 0;
+  u.live = u.active;
+}
+
+// Table-free prologue (bs16 mode): J0 and the AD hash as gcm_prologue
+// (constant-time VALU products), E_K(J0) by the bitsliced engine with each
+// lane's 16 block slots holding 16 consecutive records -- one bs16_cipher per
+// 16 records.  Records of several keys (keysets) take the per-lane-key cipher,
+// once per distinct key among the lane's 16 records.
+template <int NR>
+__global__ __launch_bounds__(256) void gcm_prologue_bs16(const GcmKeyDev *__restrict__ keys,
+                                                         BatchDesc b, RecState *__restrict__ st) {
+  const uint64_t r0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  uint4 j0[16];
+  uint32_t kidx[16];
+  bool lv[16];
+#pragma unroll
+  for (int n = 0; n < 16; n++) {
+    const uint64_t rec = r0 + n;
+    lv[n] = false;
+    kidx[n] = 0;
+    j0[n] = make_uint4(0, 0, 0, 0);
+    if (rec < b.num_records) {
+      const RecordMeta m = record_meta(b, rec);
+      lv[n] = record_live(b, rec, m);
+      kidx[n] = lv[n] && b.key_index ? b.key_index[rec] : 0u;
+      if (lv[n]) {
+        const GcmKeyDev *kp = keys + kidx[n];
+        j0[n] = record_j0(b, rec, kp->hpow_ct);
+        // Exclusive GHASH of the AD, sum A_k H^(m-1-k) (the lanes' element 0).
+        const Gf128 h1 = gf_load(kp->hpow_ct[1]);
+        Gf128 ya = {{0, 0, 0, 0}};
+        const uint64_t nad = (m.ad_len + 15) / 16;
+        for (uint64_t k = 0; k < nad; k++)
+          ya = k ? gf_xor(gf_mul(ya, h1), to_gf(ad_block(b, rec, m, k))) : to_gf(ad_block(b, rec, m, k));
+        RecState s;
+        s.live = 1;
+        s.pad[0] = s.pad[1] = s.pad[2] = 0;
+        s.j0 = j0[n];
+        s.ya = from_gf(ya);
+        s.ek0 = make_uint4(0, 0, 0, 0);
+        st[rec] = s;
+      } else {
+        RecState s;
+        s.live = 0;
+        s.pad[0] = s.pad[1] = s.pad[2] = 0;
+        s.j0 = s.ek0 = s.ya = make_uint4(0, 0, 0, 0);
+        st[rec] = s;
+      }
+    }
+  }
+  // E_K(J0) of the live slots, one cipher per distinct key of the lane.
+  uint32_t todo = 0;
+#pragma unroll
+  for (int n = 0; n < 16; n++) todo |= (uint32_t)lv[n] << n;
+  while (__ballot(todo != 0)) {
+    const uint32_t k = todo ? kidx[__builtin_ctz(todo)] : 0u;
+    uint32_t mine = 0;
+#pragma unroll
+    for (int n = 0; n < 16; n++) mine |= (uint32_t)((todo >> n) & 1u && kidx[n] == k) << n;
+    const uint32_t *rkp = &keys[k].rk_plain[0][0];
+    uint32_t p[4][2][8];
+    uint32_t t0[32], t1[32];
+#pragma unroll
+    for (int n = 0; n < 16; n++) {
+      t0[n] = j0[n].x ^ rkp[0];
+      t0[16 + n] = j0[n].z ^ rkp[2];
+      t1[n] = j0[n].y ^ rkp[1];
+      t1[16 + n] = j0[n].w ^ rkp[3];
+    }
+    transpose32_fast(t0);
+    transpose32_fast(t1);
+#pragma unroll
+    for (int q = 0; q < 32; q++) {
+      p[q / 8][0][q % 8] = t0[q];
+      p[q / 8][1][q % 8] = t1[q];
+    }
+    bs16_cipher<NR, false>(p, rkp);
+    const v32u KA = bs16_words(p, 0), KB = bs16_words(p, 1);
+#pragma unroll
+    for (int n = 0; n < 16; n++)
+      if ((mine >> n) & 1u) st[r0 + n].ek0 = make_uint4(KA[n], KB[n], KA[16 + n], KB[16 + n]);
+    todo &= ~mine;
+  }
+}
+
+// Table-free bulk kernels (BSSL_AMD_GCM_MODE=bs16): no AES table anywhere --
+// the LDS holds only the GHASH byte table of H^16.  One-key batches: 16 waves
+// per CU at 128 VGPRs, 4-record units from one grid-wide counter, every unit
+// on the bs16 engine whatever its records' shape.
+template <int NR, bool OPEN, bool XT, bool IOV>
 __global__ __launch_bounds__(1024) void gcm_bs16_kernel(const GcmKeyDev *__restrict__ keys,
                                                         BatchDesc b,
                                                         const RecState *__restrict__ st,
                                                         uint32_t *__restrict__ units) {
   constexpr int kThreads = 1024;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsPlan];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kG8Bytes];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
-  for (int e = tid; e < 256 * 64; e += kThreads) {
-    const int idx = e >> 6, slot = (e >> 5) & 1;
-    const uint32_t v = kTables.te0[idx];
-    reinterpret_cast<uint32_t *>(smem + kLdsAes)[e] = slot ? rotl(v, 8) : v;
-  }
   build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab16), tid);
   __syncthreads();
   const uint32_t *rkp = &keys[0].rk_plain[0][0];
   const uint64_t n = b.num_records;
-  RoundKeys rk;
-#pragma unroll
-  for (int r = 0; r <= NR; r++)
-#pragma unroll
-    for (int c = 0; c < 4; c++) rk.w[r][c] = keys[0].rk[r][c];
-  const uint32_t lc0 = kLdsAes + (uint32_t)(lane & 31) * 4u, lc1 = lc0 + 128u;
   for (;;) {
     uint32_t u = 0;
     if (lane == 0) u = atomicAdd(units, 1u);
-    u = __builtin_amdgcn_readfirstlane(__shfl(u, 0, 64));
-    const uint64_t first = (uint64_t)u * kRecPerWave;
+    const uint64_t first = (uint64_t)__builtin_amdgcn_readlane(u, 0) * kRecPerWave;
     if (first >= n) break;
-    const uint64_t i = first + g;
-    const bool active = i < n;
-    const uint64_t rec = active ? rec_at(b, i) : 0;
-    RecordMeta m = {0, 0, 0, 0, 0};
-    if (active) m = record_meta(b, rec);
-    const bool ok = !active || (((reinterpret_cast<uintptr_t>(b.in + m.off) |
-                                  reinterpret_cast<uintptr_t>(b.out + m.off) | m.len) & 15) == 0 &&
-                                m.len >= 4096);
-    if (__ballot(!ok) == 0)
-      process_records_bs16<NR, OPEN>(rkp, b, st, rec, active, m, smem, keys);
-    else
-    {
+    UnitIn in;
+    unit_meta<XT>(in, b, first + g);
+    process_records_bs16<NR, OPEN, XT, IOV>(rkp, b, st, in, smem, keys);
+  }
+}
+
+// Keyset batches in bs16 mode: gcm_keyset_kernel's tiles and passes, each
+// pass on the bs16 engine with the pass key's round keys.
+template <int NR, bool OPEN, bool XT>
+__global__ __launch_bounds__(1024) void gcm_keyset_bs16_kernel(const GcmKeyDev *__restrict__ keys,
+                                                               BatchDesc b,
+                                                               const RecState *__restrict__ st) {
+  constexpr int kThreads = 1024;
+  constexpr int kRecPerTile = 16 * kRecPerWave;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kG8Bytes + 64 * 16 + 16];
+  uint32_t *s_pass_key = reinterpret_cast<uint32_t *>(smem + kG8Bytes);
+  uint64_t *s_pass_mask = reinterpret_cast<uint64_t *>(smem + kG8Bytes + 64 * 4);
+  int *s_npass = reinterpret_cast<int *>(smem + kG8Bytes + 64 * 16);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  uint32_t loaded = 0xffffffffu;
+  const uint64_t n = b.num_records;
+  for (uint64_t base = (uint64_t)blockIdx.x * kRecPerTile; base < n;
+       base += (uint64_t)gridDim.x * kRecPerTile) {
+    __syncthreads();
+    if (wave == 0) {
+      const uint64_t i = base + lane;
+      uint32_t k = (lane < kRecPerTile && i < n) ? b.key_index[rec_at(b, i)] : 0xffffffffu;
+      if (k != 0xffffffffu && k >= b.num_keys) k = 0;  // (dead: RecState.live = 0)
+      uint64_t pending = __ballot(k != 0xffffffffu);
+      int np = 0;
+      while (pending) {
+        const uint32_t kk = __shfl(k, __builtin_ctzll(pending), 64);
+        const uint64_t mask = __ballot(k == kk) & pending;
+        if (lane == 0) {
+          s_pass_key[np] = kk;
+          s_pass_mask[np] = mask;
+        }
+        pending &= ~mask;
+        np++;
+      }
+      if (lane == 0) *s_npass = np;
+    }
+    __syncthreads();
+    const int npass = *s_npass;
+    for (int pi = 0; pi < npass; pi++) {
+      const uint32_t k = __builtin_amdgcn_readfirstlane(s_pass_key[pi]);
+      const uint64_t mask = s_pass_mask[pi];
+      if (k != loaded) {
+        __syncthreads();
+        build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[k].htab16), tid);
+        __syncthreads();
+        loaded = k;
+      }
+      const int t = wave * kRecPerWave + g;
+      const bool active = (mask >> t) & 1;
       UnitIn in;
-      unit_load<false, false>(in, b, i, lane & 15);
-      process_records<NR, OPEN, false>(rk, b, in, smem, keys, lc0, lc1);
+      unit_meta<XT>(in, b, active ? base + t : n);
+      process_records_bs16<NR, OPEN, XT, false>(&keys[k].rk_plain[0][0], b, st, in, smem,
+                                                keys + k);
     }
   }
 }
 
-int g_num_cus = 0;
 
 
-// Engine for a batch: 0 = T-table kernel (default), 1 = the table-free bs16
-// kernel (BSSL_AMD_GCM_MODE=bs16; one-key batches without extra bytes -- its
-// waves check their units' records themselves).
+// Engine for a batch: 0 = the T-table kernels (default), 1 = the table-free
+// bs16 engine (BSSL_AMD_GCM_MODE=bs16) for every batch: one key or keysets,
+// any record shape, extra bytes, iovecs, single records.
 int gcm_mode(const BatchDesc &b) {
+  (void)b;
   const char *e = getenv("BSSL_AMD_GCM_MODE");
-  if (!e || strcmp(e, "bs16") || b.extra_len || b.key_index || b.iovecs) return 0;
-  return 1;
+  return e && !strcmp(e, "bs16") ? 1 : 0;
 }
 
 template <int NR, bool OPEN>
 int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const KernelEvents *ev) {
-  if (!g_num_cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 1;
-    if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-        hipSuccess)
-      return 1;
+  if (one_record_batch(b) && gcm_mode(b) == 0) {
+    if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
+    hipLaunchKernelGGL((gcm_one_kernel<NR, OPEN>), dim3(1), dim3(kOneMaxBlocks), 0, s, keys, b);
+    const int rc = (int)hipGetLastError();
+    if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
+    return rc;
   }
+  const int num_cus = device_cu_count();
+  if (!num_cus) return 1;
   const int mode = gcm_mode(b);
   // The unit counter of the one-key kernels (64 bytes, zeroed) and, for the
   // bs16 engine only, its per-record state (RecState, written by its
@@ -1617,9 +1886,10 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
     hipFreeAsync(st, s);
     return 2;
   }
-  if (mode == 1) {
-    const uint64_t pblocks = (b.num_records + 255) / 256;
-    hipLaunchKernelGGL((gcm_prologue<NR>), dim3((unsigned)pblocks), dim3(256), 0, s, keys, b, st);
+  if (mode == 1) {  // 16 records per thread
+    const uint64_t pblocks = (b.num_records + 16 * 256 - 1) / (16 * 256);
+    hipLaunchKernelGGL((gcm_prologue_bs16<NR>), dim3((unsigned)pblocks), dim3(256), 0, s, keys, b,
+                       st);
   }
   BatchDesc bo = b;  // with the processing order of a ragged batch
   uint32_t *order = nullptr;
@@ -1641,13 +1911,28 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
   const RecState *cst = st;
   if (mode == 1) {
     const uint64_t units_needed = (b.num_records + 4 * 16 - 1) / (4 * 16);
-    const unsigned grid = (unsigned)(units_needed < (uint64_t)g_num_cus ? units_needed
-                                                                       : (uint64_t)g_num_cus);
-    hipLaunchKernelGGL((gcm_bs16_kernel<NR, OPEN>), dim3(grid), dim3(1024), 0, s, keys, bo, cst,
-                       units);
+    const unsigned grid = (unsigned)(units_needed < (uint64_t)num_cus ? units_needed
+                                                                       : (uint64_t)num_cus);
+    if (b.key_index) {
+      if (b.extra_len)
+        hipLaunchKernelGGL((gcm_keyset_bs16_kernel<NR, OPEN, true>), dim3(grid), dim3(1024), 0, s,
+                           keys, bo, cst);
+      else
+        hipLaunchKernelGGL((gcm_keyset_bs16_kernel<NR, OPEN, false>), dim3(grid), dim3(1024), 0, s,
+                           keys, bo, cst);
+    } else if (b.iovecs) {
+      hipLaunchKernelGGL((gcm_bs16_kernel<NR, OPEN, false, true>), dim3(grid), dim3(1024), 0, s,
+                         keys, bo, cst, units);
+    } else if (b.extra_len) {
+      hipLaunchKernelGGL((gcm_bs16_kernel<NR, OPEN, true, false>), dim3(grid), dim3(1024), 0, s,
+                         keys, bo, cst, units);
+    } else {
+      hipLaunchKernelGGL((gcm_bs16_kernel<NR, OPEN, false, false>), dim3(grid), dim3(1024), 0, s,
+                         keys, bo, cst, units);
+    }
   } else {
     const uint64_t tiles = (b.num_records + kWaves * kRecPerWave - 1) / (kWaves * kRecPerWave);
-    const unsigned grid = (unsigned)(tiles < (uint64_t)g_num_cus ? tiles : (uint64_t)g_num_cus);
+    const unsigned grid = (unsigned)(tiles < (uint64_t)num_cus ? tiles : (uint64_t)num_cus);
     if (b.key_index) {
       if (b.extra_len)
         hipLaunchKernelGGL((gcm_keyset_kernel<NR, OPEN, true, kWaves>), dim3(grid),
@@ -1655,9 +1940,9 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
       else
         hipLaunchKernelGGL((gcm_keyset_kernel<NR, OPEN, false, kWaves>), dim3(grid),
                            dim3(kWaves * 64), 0, s, keys, bo);
-    } else if (b.iovecs) {  // (one key: the ctx API; 16 lanes per record)
-      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, true>), dim3(grid), dim3(kWaves * 64),
-                         0, s, keys, bo, units);
+    } else if (b.iovecs) {  // (one key: the ctx API)
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, true, 8>), dim3(grid),
+                         dim3(kWaves * 64), 0, s, keys, bo, units);
     } else if (b.extra_len) {
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, true, kWaves, false, 8>), dim3(grid),
                          dim3(kWaves * 64), 0, s, keys, bo, units);

@@ -626,13 +626,8 @@ int launch_gcm_siv(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr,
                    const KernelEvents *ev) {
   if (b.num_records == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  static int num_cus = 0;
-  if (!num_cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 1;
-  }
+  const int num_cus = device_cu_count();
+  if (!num_cus) return 1;
   uint32_t *units = nullptr;  // the grid-wide unit counter
   if (hipMallocAsync(reinterpret_cast<void **>(&units), 64, s) != hipSuccess) return 2;
   if (hipMemsetAsync(units, 0, 64, s) != hipSuccess) {

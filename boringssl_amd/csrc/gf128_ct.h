@@ -2,8 +2,12 @@
 //
 // GF(2^128) products whose operands are secret (derived from H or from the
 // data) and that the conflict-free LDS byte table of gcm.hip does not cover:
-// the record-end tree and tag (gcm.hip finish_record), the AD hash and the
-// GHASH-derived J0 of the prologue, and their users in gcm_siv.hip.  The
+// the record-end combine and tag (gcm.hip finish_record, the one-record
+// kernel), the multi-block AD hash and the GHASH-derived J0 of non-96-bit
+// nonces, the in-kernel byte tables of H^L (build_gpow) and the host key
+// setup.  (gcm_siv.hip does not use it: its POLYVAL products go through
+// per-record Shoup tables read by one ds_read_b128 lane group, DESIGN.md
+// §4.8.)  The
 // reference computes these on CPUs without carry-less multiply in the same
 // spirit (crypto/fipsmodule/aes/gcm_nohw.cc.inc:38-82): carry-less products
 // from ordinary integer multiplications whose operands are masked to every

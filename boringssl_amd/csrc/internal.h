@@ -2,7 +2,7 @@
 //
 // Device data layout (all resident in HBM, 16-byte aligned):
 //
-//   GcmKeyDev   one per AES-GCM key (8,960 bytes): the AES round keys (T-table
+//   GcmKeyDev   one per AES-GCM key (8,976 bytes): the AES round keys (T-table
 //               and plain forms), the GHASH nibble table of H^16 and the powers
 //               H^1..H^16 as multipliers of the constant-time VALU product
 //               (gf128_ct.h).
@@ -14,8 +14,11 @@
 #ifndef BSSL_AMD_INTERNAL_H
 #define BSSL_AMD_INTERNAL_H
 
+#include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+
+#include <atomic>
 
 namespace bssl_amd {
 
@@ -29,10 +32,11 @@ struct alignas(16) GcmKeyDev {
   uint32_t pad[2];
   // The same schedule unrotated (bitsliced kernel: bit masks per round).
   uint32_t rk_plain[15][4];
-  // H^k for k = 1..16 (index 0 unused) in the reversed domain of gf128_ct.h,
+  // H^k for k = 1..17 (index 0 unused) in the reversed domain of gf128_ct.h,
   // prepared as multipliers (gf_prep): the constant-time VALU products of the
-  // record-end combine, the tag and the prologue's AD / J0 hashes.
-  uint32_t hpow_ct[17][4];
+  // record-end combine, the tag and the AD / J0 hashes (H^17: the one-record
+  // kernel folds the tag's last x H into the lane weights).
+  uint32_t hpow_ct[18][4];
   // htab16[pos][v] = (element with nibble `pos` equal to v) * H^16, as 4
   // little-endian words of the 16 GCM-order bytes.  Nibble position
   // pos = 2*k + 0 is the high nibble of byte k, 2*k + 1 the low nibble.
@@ -40,7 +44,7 @@ struct alignas(16) GcmKeyDev {
   // which is now the constant-time VALU product.)
   uint32_t htab16[32][16][4];
 };
-static_assert(sizeof(GcmKeyDev) == 240 + 16 + 240 + 17 * 16 + 8192, "layout");
+static_assert(sizeof(GcmKeyDev) == 240 + 16 + 240 + 18 * 16 + 8192, "layout");
 
 struct alignas(16) ChaChaKeyDev {
   uint32_t k[8];
@@ -202,6 +206,22 @@ int iov_batch_run(const IovBatchDesc &b, const IovRunner &run, void *stream);
 int launch_synth(uint64_t first, size_t n, const uint64_t *offsets,
                  const uint64_t *lengths, uint8_t *pt, uint8_t *nonces,
                  uint8_t *ads, void *stream);
+
+// Compute units of the current device, cached per device ordinal (launch
+// grids of the persistent kernels; 0 on error).
+inline int device_cu_count() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 0;
+  if (dev < 64) {
+    const int v = cache[dev].load(std::memory_order_relaxed);
+    if (v) return v;
+  }
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (dev < 64) cache[dev].store(v, std::memory_order_relaxed);
+  return v;
+}
 
 // Wipes key material that goes out of scope (reference: OPENSSL_cleanse).
 void secure_zero(void *p, size_t n);

@@ -188,10 +188,10 @@ bool gcm_key_setup(const uint8_t *key, size_t key_len, GcmKeyDev *out) {
   encrypt_block(w, nr, hb, hb);  // H = E_K(0^128), gcm.cc.inc:270-272
   U128 p = load_u128(hb);
   {
-    // H^1 .. H^16 as constant-time multipliers (gf128_ct.h): the reversed
+    // H^1 .. H^17 as constant-time multipliers (gf128_ct.h): the reversed
     // domain is the big-endian integer of the block, i.e. hi:lo.
     U128 hk = p;
-    for (int k = 1; k <= 16; k++) {
+    for (int k = 1; k <= 17; k++) {
       Gf128 g;
       g.w[3] = (uint32_t)(hk.hi >> 32);
       g.w[2] = (uint32_t)hk.hi;

@@ -276,10 +276,9 @@ def test_bitsliced_gcm_path(aead, rlen, mode, monkeypatch):
 @pytest.mark.parametrize("mode", ["bs16"])
 @pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm"])
 def test_mix_kernel_ragged(aead, mode, monkeypatch):
-    """The table-free kernel (gcm_bs16_kernel) on a ragged one-key batch: its
-    waves take the bs16 engine only for units whose 4 records are
-    16-byte-aligned multiples of 16 bytes of >= 4 KiB and the T-table engine
-    otherwise -- every record must match the oracle either way, sealed and
+    """The table-free kernel (gcm_bs16_kernel) on a ragged one-key batch:
+    16-byte-multiple records of 4-19 KiB mixed with records of any length,
+    at two alignments -- every record must match the oracle, sealed and
     opened."""
     monkeypatch.setenv("BSSL_AMD_GCM_MODE", mode)
     rng = random.Random(len(mode) * 7 + len(aead))

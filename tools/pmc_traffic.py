@@ -75,6 +75,8 @@ def main():
     dst = sys.argv[2] if len(sys.argv) > 2 else os.path.join(
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "traffic.json")
     res = {}
+    if os.path.exists(dst):  # merge: configs not profiled in `src` keep their entries
+        res = {k: v for k, v in json.load(open(dst)).items() if k != "calibration"}
     per_cfg = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(list)))
     for sub in sorted(os.listdir(src)):
         m = re.match(r"pmc_(config\w+?)_(fetch|write|sq)$", sub)
@@ -85,6 +87,7 @@ def main():
                 per_cfg[m.group(1)][k][n].extend(v)
     for cfg, kernels in per_cfg.items():
         res[cfg] = {k: summarise(c) for k, c in kernels.items()}
+        res[cfg]["source"] = src
     calib = collections.defaultdict(dict)
     for sub, key in (("calib_fetch", "FETCH_SIZE"), ("calib_write", "WRITE_SIZE")):
         for k, c in load(os.path.join(src, sub)).items():
@@ -105,6 +108,8 @@ def main():
     json.dump(res, open(dst, "w"), indent=1, sort_keys=True)
     for cfg, ks in res.items():
         for k, e in ks.items():
+            if not isinstance(e, dict):
+                continue
             print(cfg, k, {x: (round(y / 1e9, 3) if isinstance(y, float) and y > 1e6 else
                                round(y, 3) if isinstance(y, float) else y)
                            for x, y in e.items() if x != "counters_avg_per_dispatch"})

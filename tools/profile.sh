@@ -24,7 +24,7 @@ step() {
 }
 has() { case " $PASSES " in *" $1 "*) return 0 ;; esac; return 1; }
 for cfg in $CONFIGS; do
-  case $cfg in config3|config3x) K=chacha_poly_kernel ;; configS) K=gcm_siv_kernel ;; *) K=gcm_kernel ;; esac
+  case $cfg in config3|config3x) K=chacha_poly_kernel ;; configS) K=gcm_siv_kernel ;; config5) K=gcm_keyset_kernel ;; *) K=gcm_kernel ;; esac
   if has stats; then
     step stats_$cfg 300 rocprofv3 --kernel-trace --stats -d $O/prof_$cfg -o run --output-format csv -- \
       python3 bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline --no-parity
