@@ -440,7 +440,22 @@ int one_record(const EVP_AEAD_CTX *ctx, bool open, const uint8_t *in, uint8_t *o
   if (!run_batch(st->km, tag_len, &b, open, false, s)) return 0;
   bool ok = mapped || hipMemcpyAsync(h + o_tag, d + o_tag, o_in - o_tag + len,
                                      hipMemcpyDeviceToHost, s) == hipSuccess;
+#ifndef ONE_SYNC
+#define ONE_SYNC 0
+#endif
+#if ONE_SYNC == 1
+  hipError_t qe;
+  while ((qe = hipStreamQuery(s)) == hipErrorNotReady) {
+  }
+  ok &= qe == hipSuccess;
+#elif ONE_SYNC == 2
+  static thread_local hipEvent_t ev = nullptr;
+  if (!ev) ok &= hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+  ok &= hipEventRecord(ev, s) == hipSuccess;
+  ok &= hipEventSynchronize(ev) == hipSuccess;
+#else
   ok &= hipStreamSynchronize(s) == hipSuccess;
+#endif
   if (!ok) {
     PUT_ERROR(ERR_R_INTERNAL_ERROR);
     return 0;

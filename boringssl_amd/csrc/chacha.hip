@@ -690,8 +690,31 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
             st_left = -1;
           }
         }
+      } else if (n < 64 && ld_left >= (int64_t)n && st_left >= (int64_t)n) {
+        // The record's last, partial block inside the chunks of the lane's
+        // previous block (the running pointers): partial loads and stores at
+        // any alignment, no cursor walk.
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const uint32_t ni = n > 16u * i ? min(n - 16u * i, 16u) : 0u;
+          uint4 v = make_uint4(0, 0, 0, 0);
+          if (ni == 16)
+            v = load16_any(ld_ptr + 16 * i);
+          else if (ni)
+            v = load_partial(ld_ptr + 16 * i, ni);
+          const uint4 w = mask_block(make_uint4(v.x ^ ks[4 * i], v.y ^ ks[4 * i + 1],
+                                                v.z ^ ks[4 * i + 2], v.w ^ ks[4 * i + 3]),
+                                     ni);
+          if (ni == 16)
+            store16_any(st_ptr + 16 * i, w);
+          else if (ni)
+            store_partial(st_ptr + 16 * i, w, ni);
+          x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
+          y[4 * i] = w.x; y[4 * i + 1] = w.y; y[4 * i + 2] = w.z; y[4 * i + 3] = w.w;
+        }
       } else {
-        // A block across chunks or the record's last block: 16-byte pieces;
+        // A block across chunks (or a partial block the running pointers do
+        // not cover): 16-byte pieces;
         // the keystream waits in the staging slot and each piece's
         // ciphertext (seal: output, open: input) replaces it there.
 #pragma unroll
@@ -1182,6 +1205,191 @@ __global__ __launch_bounds__(kThreads) CHACHA_OCC void chacha_poly_kernel(
                                 (uint64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6));
 }
 
+// ---------------------------------------------------------------------------
+// One record of at most 16 KiB (the host-buffer EVP_AEAD calls, aead_api.cc
+// one_record): latency, not throughput.  Thread t < 256 takes
+// ChaCha block t + 1 (data block t) and the fifth wave the Poly1305 key block
+// (counter 0); every load of the record -- which may sit in mapped host
+// memory, one PCIe round trip each -- is issued first.  Poly1305 runs on the
+// 16-byte blocks of pad16(AD) || pad16(C) || lengths staged in LDS, front-
+// padded with zero blocks to T * c (which leaves Horner's sum unchanged):
+// thread t < T folds its c consecutive blocks by Horner's rule in r, and a
+// log2(T)-level tree joins the chunk sums, sum_t h_t r^(c (T-1-t)), with
+// multipliers r^c, r^2c, r^4c, ...  (T = 64 chunks, one wave, up to 512
+// blocks; else T = 256.)
+constexpr int kOneBlocks = 256;               // data blocks: 16 KiB
+constexpr int kOneThreads = kOneBlocks + 64;  // + the key-block wave
+constexpr int kOnePoly = 2048;                // staged Poly1305 blocks (32 KiB)
+
+// r^e for 1 <= e <= 8 (e wave-uniform).
+__device__ __forceinline__ P ppow8(const P &r, uint32_t e) {
+  P a = r;
+  for (int k = 31 - __builtin_clz(e) - 1; k >= 0; k--) {
+    a = pmul(a, a);
+    if ((e >> k) & 1) a = pmul(a, r);
+  }
+  return a;
+}
+
+template <bool OPEN, bool XC>
+__global__ __launch_bounds__(kOneThreads) void chacha_one_kernel(
+    const ChaChaKeyDev *__restrict__ keys, BatchDesc b) {
+  __shared__ uint4 s_pb[kOnePoly];
+  __shared__ uint32_t s_r[5], s_s[4];
+  __shared__ P s_part[kOneBlocks / 64];
+  __shared__ int s_ok;
+  const int t = threadIdx.x, lane = t & 63;
+  constexpr uint32_t kNonceLen = XC ? 24 : 12;
+  // (uniform one-record batch, launcher-checked: record 0 at b.in / b.ad)
+  const uint64_t len = b.record_len, ad_len = b.ad_len;
+  const bool live = b.nonce_len == kNonceLen;  // e_chacha20poly1305.cc:127-130, 241-244
+  const uint32_t nad = (uint32_t)((ad_len + 15) / 16), nct = (uint32_t)((len + 15) / 16);
+  const uint8_t *src = b.in;
+  uint8_t *dst = b.out;
+  // Loads first: the lane's 64-byte block, the nonce, the AD blocks.
+  const uint32_t n = t < kOneBlocks && 64u * t < len ? (uint32_t)min<uint64_t>(len - 64u * t, 64)
+                                                     : 0u;
+  uint4 x[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t nk = n > 16u * k ? min(n - 16u * k, 16u) : 0u;
+    x[k] = nk == 16 ? load16_any(src + 64 * t + 16 * k)
+           : nk     ? load_partial(src + 64 * t + 16 * k, nk)
+                    : make_uint4(0, 0, 0, 0);
+  }
+  uint4 nw0 = make_uint4(0, 0, 0, 0), nw1 = make_uint4(0, 0, 0, 0);
+  if (live) {
+    nw0 = load_partial(b.nonces, XC ? 16 : 12);
+    if (XC) nw1 = load_partial(b.nonces + 16, 8);
+  }
+  for (uint32_t a = t; a < nad; a += kOneThreads)
+    s_pb[a] = load_partial(b.ad + 16 * a, (uint32_t)min<uint64_t>(ad_len - 16 * a, 16));
+  uint32_t key[8], nonce[3];
+#pragma unroll
+  for (int i = 0; i < 8; i++) key[i] = keys->k[i];
+  if constexpr (XC) {
+    // key' = HChaCha20(key, nonce[0:16]), nonce' = 0^4 || nonce[16:24]
+    // (e_chacha20poly1305.cc:248-252)
+    const uint32_t n4[4] = {nw0.x, nw0.y, nw0.z, nw0.w};
+    hchacha20(key, n4);
+    nonce[0] = 0;
+    nonce[1] = nw1.x;
+    nonce[2] = nw1.y;
+  } else {
+    nonce[0] = nw0.x;
+    nonce[1] = nw0.y;
+    nonce[2] = nw0.z;
+  }
+  uint32_t ks[16];
+  chacha_block(key, t < kOneBlocks ? (uint32_t)t + 1u : 0u, nonce, ks);
+  uint4 y[4];
+  if (t >= kOneBlocks) {
+    if (t == kOneBlocks) {  // r (clamped, RFC 8439 2.5) and s of the key block
+      const uint32_t t0 = ks[0] & 0x0fffffff, t1 = ks[1] & 0x0ffffffc, t2 = ks[2] & 0x0ffffffc,
+                     t3 = ks[3] & 0x0ffffffc;
+      s_r[0] = t0 & kM26;
+      s_r[1] = ((t0 >> 26) | (t1 << 6)) & kM26;
+      s_r[2] = ((t1 >> 20) | (t2 << 12)) & kM26;
+      s_r[3] = ((t2 >> 14) | (t3 << 18)) & kM26;
+      s_r[4] = t3 >> 8;
+#pragma unroll
+      for (int i = 0; i < 4; i++) s_s[i] = ks[4 + i];
+    }
+  } else if (n) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t nk = n > 16u * k ? min(n - 16u * k, 16u) : 0u;
+      y[k] = mask_block(make_uint4(x[k].x ^ ks[4 * k], x[k].y ^ ks[4 * k + 1],
+                                   x[k].z ^ ks[4 * k + 2], x[k].w ^ ks[4 * k + 3]),
+                        nk);
+      if (nk) {
+        if (!OPEN) {  // the ciphertext (zeros for a dead record, aead.cc.inc:170-179)
+          const uint4 o = live ? y[k] : make_uint4(0, 0, 0, 0);
+          if (nk == 16)
+            store16_any(dst + 64 * t + 16 * k, o);
+          else
+            store_partial(dst + 64 * t + 16 * k, o, nk);
+        }
+        s_pb[nad + 4 * t + k] = OPEN ? x[k] : y[k];  // Poly1305 reads the ciphertext
+      }
+    }
+  }
+  if (t == 0)  // le64(ad_len) || le64(ct_len)
+    s_pb[nad + nct] = make_uint4((uint32_t)ad_len, (uint32_t)(ad_len >> 32), (uint32_t)len,
+                                 (uint32_t)(len >> 32));
+  __syncthreads();
+  const uint32_t nblk = nad + nct + 1;
+  const uint32_t T = nblk <= 512 ? 64u : (uint32_t)kOneBlocks;
+  const uint32_t c = (nblk + T - 1) / T, pad = T * c - nblk;
+  const P r = {{s_r[0], s_r[1], s_r[2], s_r[3], s_r[4]}};
+  P h = pzero();
+  if ((uint32_t)t < T) {
+    for (uint32_t k = 0; k < c; k++) {
+      const int64_t a = (int64_t)t * c + k - pad;  // (front padding: h stays 0)
+      if (a >= 0) {
+        const uint4 m = s_pb[a];
+        h = pmul(padd(h, pblock(m.x, m.y, m.z, m.w)), r);
+      }
+    }
+  }
+  P rp = ppow8(r, c);  // r^(c 2^l) at level l
+#pragma unroll
+  for (int l = 0; l < 6; l++) {
+    const P o = pshfl_down(h, 1 << l, 64);
+    h = padd(pmul(h, rp), o);
+    rp = pmul(rp, rp);
+  }
+  if (T > 64) {  // (block-uniform) the four waves' sums, Horner in r^(64c)
+    if (lane == 0 && t < kOneBlocks) s_part[t >> 6] = h;
+    __syncthreads();
+    if (t == 0) {
+      h = s_part[0];
+#pragma unroll
+      for (int w = 1; w < kOneBlocks / 64; w++) h = padd(pmul(h, rp), s_part[w]);
+    }
+  }
+  if (t == 0) {
+    uint32_t tag[4];
+    poly_finish(h, s_s, tag);
+    uint8_t *tagp = batch_tag(b, 0);
+    int ok = live;
+    if (OPEN && live) {  // CRYPTO_memcmp (e_chacha20poly1305.cc:322-326)
+      const uint4 tr = load_partial(tagp, b.tag_len);
+      const uint4 mine = mask_block(make_uint4(tag[0], tag[1], tag[2], tag[3]), b.tag_len);
+      ok = ((tr.x ^ mine.x) | (tr.y ^ mine.y) | (tr.z ^ mine.z) | (tr.w ^ mine.w)) == 0;
+    }
+    if (!OPEN)
+      store_partial(tagp, ok ? make_uint4(tag[0], tag[1], tag[2], tag[3]) : make_uint4(0, 0, 0, 0),
+                    b.tag_len);
+    if (b.status) b.status[0] = ok ? 1 : 0;
+    s_ok = ok;
+  }
+  if (OPEN) {
+    __syncthreads();
+    if (t < kOneBlocks && n) {  // the plaintext, or zeros after a failed check
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t nk = n > 16u * k ? min(n - 16u * k, 16u) : 0u;
+        const uint4 o = s_ok ? y[k] : make_uint4(0, 0, 0, 0);
+        if (nk == 16)
+          store16_any(dst + 64 * t + 16 * k, o);
+        else if (nk)
+          store_partial(dst + 64 * t + 16 * k, o, nk);
+      }
+    }
+  }
+}
+
+// Batches chacha_one_kernel takes: one contiguous record of at most 16 KiB,
+// one key, no extra bytes, AD + record + lengths within the LDS staging.
+bool one_record_batch(const BatchDesc &b) {
+  if (b.num_records != 1 || b.key_index || b.iovecs || b.extra_len || b.offsets || b.lengths ||
+      b.ad_offsets || b.ad_lengths || b.valid || b.order)
+    return false;
+  return b.record_len <= 64u * kOneBlocks &&
+         (b.ad_len + 15) / 16 + (b.record_len + 15) / 16 + 1 <= (uint64_t)kOnePoly;
+}
+
 template <bool OPEN, bool XT, bool XC, bool IOV, bool COAL, bool ANY>
 void launch_one(const ChaChaKeyDev *keys, const BatchDesc &b, hipStream_t s) {
   constexpr int L = kLanes;
@@ -1223,6 +1431,15 @@ int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, bool 
                   void *stream, const KernelEvents *ev) {
   if (b.num_records == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (one_record_batch(b)) {
+    if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
+    auto kern = xchacha ? (open ? chacha_one_kernel<true, true> : chacha_one_kernel<false, true>)
+                        : (open ? chacha_one_kernel<true, false> : chacha_one_kernel<false, false>);
+    hipLaunchKernelGGL(kern, dim3(1), dim3(kOneThreads), 0, s, keys, b);
+    const int rc = (int)hipGetLastError();
+    if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
+    return rc;
+  }
   if ((b.num_records * kLanes + kThreads - 1) / kThreads > 0x7fffffffu) return 1;
   BatchDesc bo = b;  // with the processing order of a ragged batch
   uint32_t *order = nullptr;

@@ -1318,7 +1318,7 @@ __global__ __launch_bounds__(kOneMaxBlocks) void gcm_one_kernel(const GcmKeyDev 
   uint8_t *dst = b.out + m.off;
   // Every load of the record (it may sit in mapped host memory, one PCIe
   // round trip each) is issued first, together: this thread's block, and for
-  // wave 0 the nonce and the first AD block.
+  // waves 0-1 the nonce and the first AD block, for open the received tag.
   const uint32_t nbytes = (uint32_t)m.len;  // (<= 16 KiB: the launcher checks)
   const uint32_t nb = (nbytes + 15) / 16;
   const uint32_t n = (uint32_t)t < nb ? min(nbytes - 16u * t, 16u) : 0u;
@@ -1327,11 +1327,12 @@ __global__ __launch_bounds__(kOneMaxBlocks) void gcm_one_kernel(const GcmKeyDev 
     x = load16_any(src + 16 * t);
   else if (n)
     x = load_partial(src + 16 * t, n);
-  uint4 ad0 = make_uint4(0, 0, 0, 0), nonce = make_uint4(0, 0, 0, 0);
+  uint4 ad0 = make_uint4(0, 0, 0, 0), nonce = make_uint4(0, 0, 0, 0), tr = ad0;
   if (t < 128) {
     if (live && m.ad_len) ad0 = ad_block(b, 0, m, 0);
     if (live && b.nonce_len == 12) nonce = load_partial(b.nonces, 12);
   }
+  if (OPEN && t == 0 && live) tr = load_partial(batch_tag(b, 0), b.tag_len);  // the received tag
   for (int e = t; e < 256 * 32; e += kOneMaxBlocks) t0tab[e] = kTables.te0[e >> 5];
   if (t < 32 * 16) htab[t] = reinterpret_cast<const uint4 *>(key->htab16)[t];
   RoundKeys rk;
@@ -1355,18 +1356,18 @@ __global__ __launch_bounds__(kOneMaxBlocks) void gcm_one_kernel(const GcmKeyDev 
   }
   cblk[t] = OPEN ? x : y;  // the GHASH input is the ciphertext
   uint4 ya = make_uint4(0, 0, 0, 0);
-  if (t < 64) {
-    ya = m.ad_len > 16 ? record_ad_hash<16>(b, 0, m, live, true, key->hpow_ct) : ad0;
-  } else if (t < 128) {
-    // Wave 1, meanwhile: the tag's record-independent part, len block x H ^
-    // E_K(J0) (gcm.cc.inc:576-604, 340-343).
+  if (t < 64) ya = m.ad_len > 16 ? record_ad_hash<16>(b, 0, m, live, true, key->hpow_ct) : ad0;
+  __syncthreads();
+  if (t >= 64 && t < 128) {
+    // Wave 1, during wave 0's GHASH: the tag's record-independent part, len
+    // block x H ^ E_K(J0) (gcm.cc.inc:576-604, 340-343).
     Gf128 lb = {{(uint32_t)(m.len << 3), (uint32_t)(m.len >> 29), (uint32_t)(m.ad_len << 3),
                  (uint32_t)(m.ad_len >> 29)}};
     const uint4 lh = xor4(from_gf(gf_mul(lb, gf_load(key->hpow_ct[1]))),
                           aes_block_rep<NR>(j0, rk, t0tab));
     if (t == 64) s_lh = lh;
   }
-  __syncthreads();
+  uint4 zs = make_uint4(0, 0, 0, 0);
   if (t < 16) {
     const int q = t;
     uint4 acc = (q == 15 && live) ? ya : make_uint4(0, 0, 0, 0);
@@ -1383,20 +1384,19 @@ __global__ __launch_bounds__(kOneMaxBlocks) void gcm_one_kernel(const GcmKeyDev 
     Gf128 z = gf_mul(to_gf(acc), gf_load(key->hpow_ct[17 - p]));
 #pragma unroll
     for (int i = 0; i < 4; i++) z.w[i] = row_xor16(z.w[i]);
-    const uint4 tag = xor4(from_gf(z), s_lh);
-    if (q == 0) {
-      uint8_t *tagp = batch_tag(b, 0);
-      int ok = live;
-      if (OPEN && live) {
-        // CRYPTO_memcmp (e_aes.cc.inc:860-864)
-        const uint4 tr = load_partial(tagp, b.tag_len);
-        const uint4 mine = mask_block(tag, b.tag_len);
-        ok = ((tr.x ^ mine.x) | (tr.y ^ mine.y) | (tr.z ^ mine.z) | (tr.w ^ mine.w)) == 0;
-      }
-      if (!OPEN) store_partial(tagp, ok ? tag : make_uint4(0, 0, 0, 0), b.tag_len);
-      if (b.status) b.status[0] = ok ? 1 : 0;
-      s_ok = (uint32_t)ok;
+    zs = from_gf(z);
+  }
+  __syncthreads();  // (s_lh)
+  if (t == 0) {
+    const uint4 tag = xor4(zs, s_lh);
+    int ok = live;
+    if (OPEN && live) {  // CRYPTO_memcmp (e_aes.cc.inc:860-864)
+      const uint4 mine = mask_block(tag, b.tag_len);
+      ok = ((tr.x ^ mine.x) | (tr.y ^ mine.y) | (tr.z ^ mine.z) | (tr.w ^ mine.w)) == 0;
     }
+    if (!OPEN) store_partial(batch_tag(b, 0), ok ? tag : make_uint4(0, 0, 0, 0), b.tag_len);
+    if (b.status) b.status[0] = ok ? 1 : 0;
+    s_ok = (uint32_t)ok;
   }
   if (OPEN) {
     __syncthreads();

@@ -143,10 +143,12 @@ def test_kat_single_record(aead):
 
 
 def test_ref_edge_single_record():
-    for c in load("ref_edge.json")[::3]:
+    for c in load("ref_edge.json"):
         key, nonce, ad, pt, ct, tag = (_h(c[k]) for k in ("key", "nonce", "ad", "pt", "ct", "tag"))
         ctx = ba.AEADCtx(c["aead"], key, len(tag))
         assert ctx.seal(nonce, pt, ad) == ct + tag, (c["aead"], len(pt), len(nonce), len(ad))
+        # (the one-record kernels' open: tag checked before the plaintext is written)
+        assert ctx.open(nonce, ct + tag, ad) == pt, (c["aead"], len(pt), len(nonce), len(ad))
 
 
 # ---------------------------------------------------------------------------
