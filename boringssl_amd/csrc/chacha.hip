@@ -712,17 +712,52 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
           x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
           y[4 * i] = w.x; y[4 * i + 1] = w.y; y[4 * i + 2] = w.z; y[4 * i + 3] = w.w;
         }
+      } else if (IovCur k = iov_cur_at(b, ld_c, ld_cs, p, c_end);
+                 p + n <= k.ce + iov_len_at(b, k.c + 1, c_end)) {
+        // A block in this chunk and the next (the usual straddle, or a
+        // partial block the running pointers do not cover): each 16-byte
+        // piece is at most two partial accesses, one per chunk, and all of
+        // them are issued together (the output chunks have the input chunks'
+        // lengths).
+        const IovecDev nx = k.c + 1 < c_end ? b.iovecs[k.c + 1] : IovecDev{nullptr, nullptr, 0};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const uint32_t ni = n > 16u * i ? min(n - 16u * i, 16u) : 0u;
+          const uint64_t pi = p + 16 * i;
+          const uint32_t n1 = pi < k.ce ? (uint32_t)min<uint64_t>(ni, k.ce - pi) : 0u;
+          const uint32_t n2 = ni - n1;
+          const uint8_t *sa = k.in + (pi - k.cs);
+          const uint8_t *sb = n2 ? nx.in + (pi + n1 - k.ce) : nx.in;
+          const uint4 v1 = n1 == 16 ? load16_any(sa) : load_partial(sa, n1);
+          const uint4 v2 = n2 == 16 ? load16_any(sb) : load_partial(sb, n2);
+          const uint4 s2 = bytes_at(make_uint4(0, 0, 0, 0), v2, 16 - n1);  // v2 << 8 n1
+          const uint4 v = make_uint4(v1.x | s2.x, v1.y | s2.y, v1.z | s2.z, v1.w | s2.w);
+          const uint4 w = mask_block(make_uint4(v.x ^ ks[4 * i], v.y ^ ks[4 * i + 1],
+                                                v.z ^ ks[4 * i + 2], v.w ^ ks[4 * i + 3]),
+                                     ni);
+          uint8_t *da = k.out + (pi - k.cs);
+          if (n1 == 16)
+            store16_any(da, w);
+          else if (n1)
+            store_partial(da, w, n1);
+          if (n2)
+            store_partial(nx.out + (pi + n1 - k.ce), bytes_at(w, make_uint4(0, 0, 0, 0), n1), n2);
+          x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
+          y[4 * i] = w.x; y[4 * i + 1] = w.y; y[4 * i + 2] = w.z; y[4 * i + 3] = w.w;
+        }
+        const bool next = p + n > k.ce;  // the block ended in the next chunk
+        ld_c = st_c = next ? k.c + 1 : k.c;
+        ld_cs = st_cs = next ? k.ce : k.cs;
+        ld_left = st_left = -1;
       } else {
-        // A block across chunks (or a partial block the running pointers do
-        // not cover): 16-byte pieces;
+        // A block over three or more chunks: 16-byte pieces;
         // the keystream waits in the staging slot and each piece's
         // ciphertext (seal: output, open: input) replaces it there.
 #pragma unroll
         for (int i = 0; i < 4; i++)
           *reinterpret_cast<uint4 *>(my + 1024 * i) =
               make_uint4(ks[4 * i], ks[4 * i + 1], ks[4 * i + 2], ks[4 * i + 3]);
-        IovCur k;
-        iov_at(k, b, ld_c, ld_cs);
+        // (k: the input cursor, at the chunk holding p)
         IovCur ko;
         iov_at(ko, b, st_c, st_cs);
 #pragma unroll 1

@@ -1317,8 +1317,8 @@ __global__ __launch_bounds__(kOneMaxBlocks) void gcm_one_kernel(const GcmKeyDev 
   const uint8_t *src = b.in + m.off;
   uint8_t *dst = b.out + m.off;
   // Every load of the record (it may sit in mapped host memory, one PCIe
-  // round trip each) is issued first, together: this thread's block, and for
-  // waves 0-1 the nonce and the first AD block, for open the received tag.
+  // round trip each) is issued first, together: this thread's block and the
+  // nonce, for wave 0 the first AD block, for open the received tag.
   const uint32_t nbytes = (uint32_t)m.len;  // (<= 16 KiB: the launcher checks)
   const uint32_t nb = (nbytes + 15) / 16;
   const uint32_t n = (uint32_t)t < nb ? min(nbytes - 16u * t, 16u) : 0u;
@@ -1328,10 +1328,8 @@ __global__ __launch_bounds__(kOneMaxBlocks) void gcm_one_kernel(const GcmKeyDev 
   else if (n)
     x = load_partial(src + 16 * t, n);
   uint4 ad0 = make_uint4(0, 0, 0, 0), nonce = make_uint4(0, 0, 0, 0), tr = ad0;
-  if (t < 128) {
-    if (live && m.ad_len) ad0 = ad_block(b, 0, m, 0);
-    if (live && b.nonce_len == 12) nonce = load_partial(b.nonces, 12);
-  }
+  if (live && b.nonce_len == 12) nonce = load_partial(b.nonces, 12);  // (every thread's J0)
+  if (t < 64 && live && m.ad_len) ad0 = ad_block(b, 0, m, 0);
   if (OPEN && t == 0 && live) tr = load_partial(batch_tag(b, 0), b.tag_len);  // the received tag
   for (int e = t; e < 256 * 32; e += kOneMaxBlocks) t0tab[e] = kTables.te0[e >> 5];
   if (t < 32 * 16) htab[t] = reinterpret_cast<const uint4 *>(key->htab16)[t];

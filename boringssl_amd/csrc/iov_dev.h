@@ -57,9 +57,10 @@ __device__ __forceinline__ uint4 load_partial(const uint8_t *p, uint32_t n) {
 }
 
 // Bytes [0, n) of v to p: one 16-byte store for a whole aligned block,
-// dword (+ short / byte) stores when p is 4-byte aligned, else bytes.
-// (Each narrow store is a memory request of its own; a record's tag and
-// tail otherwise cost up to 31 of them.)
+// dword (+ short / byte) stores when p is 4-byte aligned, else dword stores
+// at the byte address and the last 1-3 bytes.  (Each narrow store is a
+// memory request of its own; a record's tag and tail otherwise cost up to 31
+// of them.)
 __device__ __forceinline__ void store_partial(uint8_t *p, uint4 v, uint32_t n) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
@@ -80,7 +81,17 @@ __device__ __forceinline__ void store_partial(uint8_t *p, uint4 v, uint32_t n) {
       if (r & 1) q[r & 2] = (uint8_t)(last >> (8 * (r & 2)));
     }
   } else {
-    for (uint32_t i = 0; i < n; i++) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    // Unaligned: whole dwords at byte addresses (unaligned mode, as
+    // store16_any), then the last 1-3 bytes.
+    u32_any *pw = reinterpret_cast<u32_any *>(p);
+    uint32_t last = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (4u * i + 4 <= n) pw[i] = w[i];
+      if (n / 4 == (uint32_t)i) last = w[i];
+    }
+    uint8_t *q = p + (n & ~3u);
+    for (uint32_t i = 0; i < (n & 3); i++) q[i] = (uint8_t)(last >> (8 * i));
   }
 }
 
@@ -121,6 +132,20 @@ __device__ __forceinline__ void iov_at(IovCur &k, const BatchDesc &b, uint64_t c
 __device__ __forceinline__ void iov_seek(IovCur &k, const BatchDesc &b, uint64_t p,
                                          uint64_t c_end) {
   while (p >= k.ce && k.c + 1 < c_end) iov_at(k, b, k.c + 1, k.ce);
+}
+
+// The cursor of chunk c (stream start cs), advanced to the chunk holding p.
+__device__ __forceinline__ IovCur iov_cur_at(const BatchDesc &b, uint64_t c, uint64_t cs,
+                                             uint64_t p, uint64_t c_end) {
+  IovCur k;
+  iov_at(k, b, c, cs);
+  iov_seek(k, b, p, c_end);
+  return k;
+}
+
+// Length of chunk c of a record whose chunks end at c_end (0 past the end).
+__device__ __forceinline__ uint64_t iov_len_at(const BatchDesc &b, uint64_t c, uint64_t c_end) {
+  return c < c_end ? b.iovecs[c].len : 0;
 }
 
 // Bytes [a, a + 16) of the 32 bytes A || B (a = 0..16).
