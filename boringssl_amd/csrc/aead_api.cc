@@ -248,7 +248,8 @@ int launch_desc(const KeyMaterial *km, const BatchDesc &d, bool open, void *stre
 
 // Launch a batch over device buffers.  Returns 1 on success.
 int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch, bool open,
-              bool use_key_index, void *stream, const uint8_t *valid = nullptr) {
+              bool use_key_index, void *stream, const uint8_t *valid = nullptr,
+              uint32_t *done = nullptr, uint32_t done_seq = 0) {
   BatchDesc d;
   memset(&d, 0, sizeof(d));
   d.in = batch->in;
@@ -275,6 +276,8 @@ int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch
   d.extra = nullptr;
   d.extra_out = nullptr;
   d.extra_len = d.extra_stride = d.extra_out_stride = d.tag_stride = 0;
+  d.done = done;
+  d.done_seq = done_seq;
   if (launch_desc(km, d, open, stream) != 0) {
     PUT_ERROR(ERR_R_INTERNAL_ERROR);
     return 0;
@@ -352,20 +355,16 @@ Scratch *scratch(size_t bytes) {
       sc.dev = nullptr;
       return nullptr;
     }
-#ifndef HOSTMEM_FLAGS
-#define HOSTMEM_FLAGS hipHostMallocMapped
-#endif
-#ifndef HOSTMEM_DEVPTR
-#define HOSTMEM_DEVPTR 1
-#endif
-    if (hipHostMalloc(&sc.host, cap, HOSTMEM_FLAGS) != hipSuccess) {
+    // Mapped (and, by HIP's default, coherent) pinned memory; the kernels use
+    // its device address.  (Coherent / non-coherent / portable flag variants
+    // measured the same single-record latency, profiles/r04/s10/.)
+    if (hipHostMalloc(&sc.host, cap, hipHostMallocMapped) != hipSuccess) {
       sc.host = nullptr;
       hipFree(sc.dev);
       sc.dev = nullptr;
       return nullptr;
     }
-    if (!HOSTMEM_DEVPTR) sc.mapped = sc.host;
-    else if (hipHostGetDevicePointer(reinterpret_cast<void **>(&sc.mapped), sc.host, 0) !=
+    if (hipHostGetDevicePointer(reinterpret_cast<void **>(&sc.mapped), sc.host, 0) !=
         hipSuccess) {
       hipHostFree(sc.host);
       hipFree(sc.dev);
@@ -387,6 +386,26 @@ size_t one_record_map_max() {
     return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)65536;
   }();
   return v;
+}
+
+// Waits for a single-record launch on stream s.  With `done` (mapped path)
+// the host spins on the completion word the one-record kernels write after
+// their last store -- it lands a few microseconds before the stream's
+// completion signal does -- and checks the stream every 256 polls, so a
+// launch that took another kernel (which does not write the word) or failed
+// still ends.  Otherwise (and for records that took the copies) it syncs the
+// stream.
+bool wait_record(hipStream_t s, const uint32_t *done, uint32_t seq) {
+  if (!done) return hipStreamSynchronize(s) == hipSuccess;
+  for (uint32_t i = 1;; i++) {
+    if (__atomic_load_n(done, __ATOMIC_ACQUIRE) == seq) return true;
+    if ((i & 255) == 0) {
+      const hipError_t e = hipStreamQuery(s);
+      if (e == hipSuccess) return true;
+      if (e != hipErrorNotReady) return false;
+    }
+    __builtin_ia32_pause();
+  }
 }
 
 // Seal or open one record held in host memory.  `in`/`out` may be equal.
@@ -437,25 +456,18 @@ int one_record(const EVP_AEAD_CTX *ctx, bool open, const uint8_t *in, uint8_t *o
   b.ad_len = ad_len;
   b.tags = d + o_tag;
   b.status = d + o_status;
-  if (!run_batch(st->km, tag_len, &b, open, false, s)) return 0;
+  // Completion word (mapped path): the one-record kernels write `seq` there
+  // last (BatchDesc::done).
+  static thread_local uint32_t t_seq = 0;
+  const uint32_t seq = ++t_seq ? t_seq : ++t_seq;  // (never 0)
+  uint32_t *hdone = reinterpret_cast<uint32_t *>(h + o_status + 4);
+  __atomic_store_n(hdone, 0u, __ATOMIC_RELAXED);
+  if (!run_batch(st->km, tag_len, &b, open, false, s, nullptr,
+                 mapped ? reinterpret_cast<uint32_t *>(d + o_status + 4) : nullptr, seq))
+    return 0;
   bool ok = mapped || hipMemcpyAsync(h + o_tag, d + o_tag, o_in - o_tag + len,
                                      hipMemcpyDeviceToHost, s) == hipSuccess;
-#ifndef ONE_SYNC
-#define ONE_SYNC 0
-#endif
-#if ONE_SYNC == 1
-  hipError_t qe;
-  while ((qe = hipStreamQuery(s)) == hipErrorNotReady) {
-  }
-  ok &= qe == hipSuccess;
-#elif ONE_SYNC == 2
-  static thread_local hipEvent_t ev = nullptr;
-  if (!ev) ok &= hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
-  ok &= hipEventRecord(ev, s) == hipSuccess;
-  ok &= hipEventSynchronize(ev) == hipSuccess;
-#else
-  ok &= hipStreamSynchronize(s) == hipSuccess;
-#endif
+  ok = ok && wait_record(s, mapped ? hdone : nullptr, seq);
   if (!ok) {
     PUT_ERROR(ERR_R_INTERNAL_ERROR);
     return 0;

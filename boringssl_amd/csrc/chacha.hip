@@ -385,13 +385,11 @@ __device__ __forceinline__ void crypt_block_x(const uint8_t *src, uint8_t *dst, 
 // log2(L)-level tree of gcm.hip's lane algebra.
 // iovec records: the lane's whole block comes by LDS-DMA into the wave's
 // staging area (loading it into VGPRs across the rounds measured the same).
-#ifndef CHACHA_AP_SPLIT
-#define CHACHA_AP_SPLIT 0
-#endif
-#ifndef CHACHA_WPE2
-#define CHACHA_WPE2 3
-#endif
-#define CHACHA_OCC __attribute__((amdgpu_waves_per_eu(L == 2 ? CHACHA_WPE2 : 4)))
+// Occupancy: 3 waves per SIMD at 2 lanes per record.  (Round 4, same box,
+// config 3, profiles/r04/s10/: 4 waves per SIMD (spills) 1,216 GiB/s, the
+// block loop's multipliers read from LDS per product instead of in one batch
+// 1,193, both 1,183, against 1,246.)
+#define CHACHA_OCC __attribute__((amdgpu_waves_per_eu(L == 2 ? 3 : 4)))
 // Record-contiguous I/O (COAL): a wave's loads and stores move whole
 // per-record runs (L = 2: 8 records x 128 bytes per instruction), staged
 // through LDS to the lane that owns each 64-byte block.  With the
@@ -1025,22 +1023,6 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     const uint64_t d = u - 1 - sh;
     if (d < nunits) {
       PAcc t = pacc_zero();
-#if CHACHA_AP_SPLIT
-      uint32_t slot = threadIdx.x / L;
-      asm volatile("" : "+v"(slot));  // re-read per block, not hoisted (registers)
-      const uint32_t *apw32 = reinterpret_cast<const uint32_t *>(s_apow[slot]);
-      auto mult = [&](int k, const P &a) {
-        uint32_t ap[9];
-#pragma unroll
-        for (int i = 0; i < 9; i++) ap[i] = apw32[9 * k + i];
-        pmac_s(t, a, ap, ap + 5);
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      mult(0, acc);
-      mult(1, pblock(c[0], c[1], c[2], c[3]));
-      mult(2, pblock(c[4], c[5], c[6], c[7]));
-      mult(3, pblock(c[8], c[9], c[10], c[11]));
-#else
       uint32_t ap[36];
       {
         uint32_t slot = threadIdx.x / L;
@@ -1055,7 +1037,6 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
       pmac_s(t, pblock(c[0], c[1], c[2], c[3]), ap + 9, ap + 14);
       pmac_s(t, pblock(c[4], c[5], c[6], c[7]), ap + 18, ap + 23);
       pmac_s(t, pblock(c[8], c[9], c[10], c[11]), ap + 27, ap + 32);
-#endif
       acc = padd(preduce(t), pblock(c[12], c[13], c[14], c[15]));
     } else {
       P tt = pblock(c[0], c[1], c[2], c[3]);
@@ -1411,6 +1392,17 @@ __global__ __launch_bounds__(kOneThreads) void chacha_one_kernel(
         else if (nk)
           store_partial(dst + 64 * t + 16 * k, o, nk);
       }
+    }
+  }
+  if (b.done) {  // completion word (aead_api.cc wait_record): after every store
+    // Every thread waits for its own stores; one system-scope release then
+    // covers them all.
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (t == 0) {
+      __threadfence_system();
+      __builtin_amdgcn_s_waitcnt(0);  // (the L2 write-back has finished)
+      *reinterpret_cast<volatile uint32_t *>(b.done) = b.done_seq;
     }
   }
 }

@@ -1162,7 +1162,8 @@ __device__ __forceinline__ void fill_aes_tables(uint8_t *smem, int tid) {
 // that the SIMD arbiter favours (older waves issue first) simply process more
 // units instead of waiting at a per-tile barrier for the slowest wave
 // (DESIGN.md §4.2).  L: lanes per record -- 8 (8 records per wave, GHASH
-// stride H^8) for every one-key batch; the keyset kernel keeps 16.
+// stride H^8) for aligned one-key batches, 16 for iovec records and unaligned
+// uniform batches (unaligned_uniform); the keyset kernel keeps 16.
 // (A kernel of its own, apart from the keyset kernel, so each gets its own
 // register allocation.)
 template <int NR, bool OPEN, bool XT, int W, bool IOV = false, int L = 16>
@@ -1404,6 +1405,17 @@ __global__ __launch_bounds__(kOneMaxBlocks) void gcm_one_kernel(const GcmKeyDev 
         store16_any(dst + 16 * t, o);
       else
         store_partial(dst + 16 * t, o, n);
+    }
+  }
+  if (b.done) {  // completion word (aead_api.cc wait_record): after every store
+    // Every thread waits for its own stores; one system-scope release then
+    // covers them all (a fence in every wave cost ~4 us here: 16 L2 writebacks).
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (t == 0) {
+      __threadfence_system();
+      __builtin_amdgcn_s_waitcnt(0);  // (the L2 write-back has finished)
+      *reinterpret_cast<volatile uint32_t *>(b.done) = b.done_seq;
     }
   }
 }
@@ -1850,6 +1862,20 @@ __global__ __launch_bounds__(1024) void gcm_keyset_bs16_kernel(const GcmKeyDev *
 
 
 
+// Lanes per record of the one-key kernel: 8 (stride H^8, 8 records per wave)
+// by default; 16 for iovec records and for uniform batches of records of
+// 4 KiB or more that are not 16-byte aligned, where a lane group's 16 L-byte
+// run costs an extra cache line per run -- relatively twice as much at L = 8.
+// 16 KiB records at a 16,385-byte stride: 823 GiB/s at L = 8, 1,076 at L = 16
+// (aligned: 1,146-1,177); 1350-byte records at a 1351-byte stride: 755 at
+// L = 8, 422 at L = 16, where the per-record work dominates; iovec records of
+// 16 KiB 784 / 961 (profiles/r04/s10/, s11/).
+bool unaligned_uniform(const BatchDesc &b) {
+  return !b.offsets && b.record_len >= 4096 &&
+         ((reinterpret_cast<uintptr_t>(b.in) | reinterpret_cast<uintptr_t>(b.out) |
+           b.record_stride) & 15) != 0;
+}
+
 // Engine for a batch: 0 = the T-table kernels (default), 1 = the table-free
 // bs16 engine (BSSL_AMD_GCM_MODE=bs16) for every batch: one key or keysets,
 // any record shape, extra bytes, iovecs, single records.
@@ -1939,10 +1965,13 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
         hipLaunchKernelGGL((gcm_keyset_kernel<NR, OPEN, false, kWaves>), dim3(grid),
                            dim3(kWaves * 64), 0, s, keys, bo);
     } else if (b.iovecs) {  // (one key: the ctx API)
-      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, true, 8>), dim3(grid),
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, true, 16>), dim3(grid),
                          dim3(kWaves * 64), 0, s, keys, bo, units);
     } else if (b.extra_len) {
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, true, kWaves, false, 8>), dim3(grid),
+                         dim3(kWaves * 64), 0, s, keys, bo, units);
+    } else if (unaligned_uniform(b)) {
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, 16>), dim3(grid),
                          dim3(kWaves * 64), 0, s, keys, bo, units);
     } else {
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, 8>), dim3(grid),

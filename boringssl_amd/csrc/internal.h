@@ -118,6 +118,13 @@ struct BatchDesc {
   const uint64_t *iovec_start;
   const IvecDev *aadvecs;
   const uint64_t *aadvec_start;
+  // Single-record host calls (aead_api.cc one_record): when set, the
+  // one-record kernels write done_seq here (mapped host memory) after every
+  // other store of the record has completed, so the host can return as soon
+  // as it sees the value instead of waiting for the stream.  Null otherwise
+  // (the other kernels ignore it).
+  uint32_t *done;
+  uint32_t done_seq;
 };
 
 // Tag / extra addresses of record i.

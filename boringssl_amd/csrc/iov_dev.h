@@ -228,6 +228,10 @@ __device__ __forceinline__ void iov_scatter(const BatchDesc &b, IovCur k, uint64
 // iovec record; n <= 16, zero past n).  Walks from c0: the AD is short.
 __device__ __forceinline__ uint4 ivec_load16(const IvecDev *v, uint64_t c0, uint64_t c1,
                                              uint64_t pos, uint32_t n) {
+  if (c0 < c1) {  // inside the first chunk (TLS: one chunk of 13 bytes): one partial load
+    const IvecDev f = v[c0];
+    if (pos + n <= f.len) return load_partial(f.in + pos, n);
+  }
   uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
   uint64_t c = c0, cs = 0;
   for (uint32_t i = 0; i < n; i++) {
