@@ -1344,16 +1344,21 @@ __global__ __launch_bounds__(kOneMaxBlocks) void gcm_one_kernel(const GcmKeyDev 
                                        : record_j0(b, 0, key->hpow_ct);
   const uint32_t ctr0 = bswap32(j0.w);
   __syncthreads();
-  const uint4 ks =
-      aes_block_rep<NR>(make_uint4(j0.x, j0.y, j0.z, bswap32(ctr0 + 1u + (uint32_t)t)), rk, t0tab);
-  const uint4 y = mask_block(xor4(x, ks), n);
-  if (!OPEN && n) {  // seal: the ciphertext (zeros for a dead record, aead.cc.inc:170-179)
-    if (n == 16)
-      store16_any(dst + 16 * t, live ? y : make_uint4(0, 0, 0, 0));
-    else
-      store_partial(dst + 16 * t, live ? y : make_uint4(0, 0, 0, 0), n);
+  // (Only threads with a block run the rounds: the waves past the record's
+  // end issue no LDS lookups -- for a 1350-byte record 2 of the 16 waves.)
+  uint4 y = make_uint4(0, 0, 0, 0);
+  if (n) {
+    const uint4 ks = aes_block_rep<NR>(
+        make_uint4(j0.x, j0.y, j0.z, bswap32(ctr0 + 1u + (uint32_t)t)), rk, t0tab);
+    y = mask_block(xor4(x, ks), n);
+    if (!OPEN) {  // seal: the ciphertext (zeros for a dead record, aead.cc.inc:170-179)
+      if (n == 16)
+        store16_any(dst + 16 * t, live ? y : make_uint4(0, 0, 0, 0));
+      else
+        store_partial(dst + 16 * t, live ? y : make_uint4(0, 0, 0, 0), n);
+    }
+    cblk[t] = OPEN ? x : y;  // the GHASH input is the ciphertext
   }
-  cblk[t] = OPEN ? x : y;  // the GHASH input is the ciphertext
   uint4 ya = make_uint4(0, 0, 0, 0);
   if (t < 64) ya = m.ad_len > 16 ? record_ad_hash<16>(b, 0, m, live, true, key->hpow_ct) : ad0;
   __syncthreads();

@@ -25,4 +25,6 @@ done
 step bench_config2_open 300 python bench.py --op open --no-cpu-baseline
 step bench_config3_open 300 python bench.py --config config3 --op open --no-cpu-baseline
 step rehearse2 300 env BSSL_AMD_REHEARSE_DEVICES=1 python bench.py --gpus 2 --no-cpu-baseline
+step latency 200 python tools/latency_bench.py
+step latency_2 200 python tools/latency_bench.py
 O=$O/prof CONFIGS="config2 configG config3 config4 config5" PASSES="stats pmc" bash tools/profile.sh
