@@ -107,6 +107,8 @@ def main():
         res["calibration"] = dict(calib)
     json.dump(res, open(dst, "w"), indent=1, sort_keys=True)
     for cfg, ks in res.items():
+        if not isinstance(ks, dict):
+            continue
         for k, e in ks.items():
             if not isinstance(e, dict):
                 continue
