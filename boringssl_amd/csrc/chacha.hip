@@ -576,7 +576,20 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   int64_t ld_left = -1, st_left = -1;
   bool pre_ok = false;  // pre[] holds the lane's whole current block
   if constexpr (IOV) {
-    if (live) ld_c = st_c = b.iovec_start[rec];
+    if (live) {
+      ld_c = st_c = b.iovec_start[rec];
+      // Running pointers for the lane's first data block (d0 = q - 1, lane 0:
+      // L - 1) when the first chunk holds it, so the first load and store
+      // take the pointer path instead of a cursor walk (a descriptor load
+      // each, exposed: one before the rounds, one after).
+      const IovecDev f = ld_c < b.iovec_start[rec + 1] ? b.iovecs[ld_c] : IovecDev{nullptr, nullptr, 0};
+      const uint64_t p0 = 64 * (uint64_t)(q >= 1 ? q - 1 : L - 1);
+      if (p0 + 64 <= f.len) {
+        ld_ptr = f.in + p0;
+        st_ptr = f.out + p0;
+        ld_left = st_left = (int64_t)(f.len - p0);
+      }
+    }
   }
   auto prefetch = [&](uint64_t u, uint4 pre[4]) {
     const uint64_t d = u - 1 - sh;
@@ -746,7 +759,16 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
         const bool next = p + n > k.ce;  // the block ended in the next chunk
         ld_c = st_c = next ? k.c + 1 : k.c;
         ld_cs = st_cs = next ? k.ce : k.cs;
-        ld_left = st_left = -1;
+        // Running pointers for the lane's next block (64 L bytes on) when the
+        // chunk the block ended in holds it: no cursor walk for it.
+        const uint64_t pn = p + 64 * L, ce = next ? k.ce + nx.len : k.ce;
+        if (pn + 64 <= ce) {
+          ld_ptr = (next ? nx.in : k.in) + (pn - ld_cs);
+          st_ptr = (next ? nx.out : k.out) + (pn - st_cs);
+          ld_left = st_left = (int64_t)(ce - pn);
+        } else {
+          ld_left = st_left = -1;
+        }
       } else {
         // A block over three or more chunks: 16-byte pieces;
         // the keystream waits in the staging slot and each piece's

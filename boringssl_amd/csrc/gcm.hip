@@ -1282,32 +1282,36 @@ __global__ __launch_bounds__(1024) void gcm_keyset_kernel(const GcmKeyDev *__res
 // a time, ssl/ssl_aead_ctx.cc:299-381) as one launch of one workgroup with no
 // unit counter and no 128 KiB table build.  Thread t encrypts counter block t
 // (records up to kOneMaxBlocks), every load in flight at once (the record may
-// sit in mapped host memory); AES from T0 replicated per bank (32 KiB, as the
-// prologue's); GHASH by lanes 0..15 at stride 16 with the key's nibble table
-// of H^16 in LDS (8 KiB): in each lookup all 16 lanes read the same nibble
-// position, so a lane's bank is its nibble value's and equal values share an
-// address -- conflict-free whatever the data.  Open computes the tag first and
-// writes the plaintext (or zeros) after the check.
+// sit in mapped host memory); AES from T0 replicated per bank (32 KiB);
+// GHASH by lanes 0..15 at stride 16 with the bulk kernels' lane-rotated byte
+// table of H^16 (64 KiB, built from the key's nibble tables while the record
+// loads are in flight; 16 lookups per block instead of the nibble table's
+// 32).  Open computes the tag first and writes the plaintext (or zeros) after
+// the check.
 constexpr int kOneMaxBlocks = 1024;  // 16 KiB: threads per workgroup
 
-// x * H^16 from the nibble table (key_setup.cc layout: position 2k = the high
-// nibble of byte k, 2k + 1 the low one).
-__device__ __forceinline__ uint4 nib_mul16(uint4 x, const uint4 *htab) {
-  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-  uint4 r = make_uint4(0, 0, 0, 0);
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const uint32_t byte = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
-    r = xor4_3(r, htab[(2 * k) * 16 + (byte >> 4)], htab[(2 * k + 1) * 16 + (byte & 15u)]);
-  }
-  return r;
+// acc * H^16 from the lane-rotated byte table (g8_rotate / g8_load, as the
+// bulk kernels' GHASH: the 16 lanes of a ds_read_b128 lane group read 16
+// different slots in every step, whatever the data).
+__device__ __forceinline__ uint4 g8_mul16(uint4 acc, bool rs1, bool rs2, uint32_t rbs,
+                                          const uint32_t (&P)[4], const uint8_t *g8) {
+  Gh8 h;
+  g8_rotate(h, acc, rs1, rs2, rbs);
+  uint4 r = xor4_3(g8_load<0>(h, P, g8), g8_load<1>(h, P, g8), g8_load<2>(h, P, g8));
+  r = xor4_3(r, g8_load<3>(h, P, g8), g8_load<4>(h, P, g8));
+  r = xor4_3(r, g8_load<5>(h, P, g8), g8_load<6>(h, P, g8));
+  r = xor4_3(r, g8_load<7>(h, P, g8), g8_load<8>(h, P, g8));
+  r = xor4_3(r, g8_load<9>(h, P, g8), g8_load<10>(h, P, g8));
+  r = xor4_3(r, g8_load<11>(h, P, g8), g8_load<12>(h, P, g8));
+  r = xor4_3(r, g8_load<13>(h, P, g8), g8_load<14>(h, P, g8));
+  return xor4(r, g8_load<15>(h, P, g8));
 }
 
 template <int NR, bool OPEN>
 __global__ __launch_bounds__(kOneMaxBlocks) void gcm_one_kernel(const GcmKeyDev *__restrict__ keys,
                                                                 BatchDesc b) {
+  __shared__ __attribute__((aligned(16))) uint8_t g8[kG8Bytes];  // byte table of H^16
   __shared__ uint32_t t0tab[256 * 32];
-  __shared__ uint4 htab[32 * 16];
   __shared__ uint4 cblk[kOneMaxBlocks];
   __shared__ uint4 s_lh;  // len block x H ^ E_K(J0), from wave 1
   __shared__ uint32_t s_ok;
@@ -1333,7 +1337,7 @@ __global__ __launch_bounds__(kOneMaxBlocks) void gcm_one_kernel(const GcmKeyDev 
   if (t < 64 && live && m.ad_len) ad0 = ad_block(b, 0, m, 0);
   if (OPEN && t == 0 && live) tr = load_partial(batch_tag(b, 0), b.tag_len);  // the received tag
   for (int e = t; e < 256 * 32; e += kOneMaxBlocks) t0tab[e] = kTables.te0[e >> 5];
-  if (t < 32 * 16) htab[t] = reinterpret_cast<const uint4 *>(key->htab16)[t];
+  build_g8<kOneMaxBlocks>(g8, reinterpret_cast<const uint4 *>(key->htab16), t);
   RoundKeys rk;
 #pragma unroll
   for (int r = 0; r <= NR; r++)
@@ -1375,10 +1379,20 @@ __global__ __launch_bounds__(kOneMaxBlocks) void gcm_one_kernel(const GcmKeyDev 
   if (t < 16) {
     const int q = t;
     uint4 acc = (q == 15 && live) ? ya : make_uint4(0, 0, 0, 0);
+    const bool rs1 = (q >> 2) & 1, rs2 = (q >> 3) & 1;  // (lane constants of process_records)
+    const uint32_t rbs = (uint32_t)q & 3u;
+    uint32_t P[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) v |= (uint32_t)(((4 * k + i + q) & 15) << 4) << (8 * i);
+      P[k] = v;
+    }
     const uint32_t iters = live ? (nb + 15) / 16 : 0u;
     for (uint32_t it = 0; it < iters; it++) {
       const uint32_t j = 16 * it + q;
-      const uint4 h = nib_mul16(acc, htab);
+      const uint4 h = g8_mul16(acc, rs1, rs2, rbs, P, g8);
       if (j < nb) acc = xor4(h, cblk[j]);
     }
     // Record end (finish_record's algebra) with the tag's last x H folded into
