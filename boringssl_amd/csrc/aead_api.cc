@@ -247,9 +247,11 @@ int launch_desc(const KeyMaterial *km, const BatchDesc &d, bool open, void *stre
 }
 
 // Launch a batch over device buffers.  Returns 1 on success.
+// `one`: the single-record extras of one_record (completion word, inline
+// nonce / AD; BatchDesc::done, ::inl), or null.
 int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch, bool open,
               bool use_key_index, void *stream, const uint8_t *valid = nullptr,
-              uint32_t *done = nullptr, uint32_t done_seq = 0) {
+              const BatchDesc *one = nullptr) {
   BatchDesc d;
   memset(&d, 0, sizeof(d));
   d.in = batch->in;
@@ -276,8 +278,13 @@ int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch
   d.extra = nullptr;
   d.extra_out = nullptr;
   d.extra_len = d.extra_stride = d.extra_out_stride = d.tag_stride = 0;
-  d.done = done;
-  d.done_seq = done_seq;
+  if (one) {
+    d.done = one->done;
+    d.done_seq = one->done_seq;
+    d.inl = one->inl;
+    memcpy(d.inl_nonce, one->inl_nonce, sizeof(d.inl_nonce));
+    memcpy(d.inl_ad, one->inl_ad, sizeof(d.inl_ad));
+  }
   if (launch_desc(km, d, open, stream) != 0) {
     PUT_ERROR(ERR_R_INTERNAL_ERROR);
     return 0;
@@ -462,9 +469,20 @@ int one_record(const EVP_AEAD_CTX *ctx, bool open, const uint8_t *in, uint8_t *o
   const uint32_t seq = ++t_seq ? t_seq : ++t_seq;  // (never 0)
   uint32_t *hdone = reinterpret_cast<uint32_t *>(h + o_status + 4);
   __atomic_store_n(hdone, 0u, __ATOMIC_RELAXED);
-  if (!run_batch(st->km, tag_len, &b, open, false, s, nullptr,
-                 mapped ? reinterpret_cast<uint32_t *>(d + o_status + 4) : nullptr, seq))
-    return 0;
+  BatchDesc one;
+  memset(&one, 0, sizeof(one));
+  one.done = mapped ? reinterpret_cast<uint32_t *>(d + o_status + 4) : nullptr;
+  one.done_seq = seq;
+  // The nonce and a short AD by value (BatchDesc::inl).
+  if (nonce_len == 12) {
+    memcpy(one.inl_nonce, nonce, 12);
+    one.inl |= 1;
+  }
+  if (ad_len <= 16) {
+    if (ad_len) memcpy(one.inl_ad, ad, ad_len);
+    one.inl |= 2;
+  }
+  if (!run_batch(st->km, tag_len, &b, open, false, s, nullptr, &one)) return 0;
   bool ok = mapped || hipMemcpyAsync(h + o_tag, d + o_tag, o_in - o_tag + len,
                                      hipMemcpyDeviceToHost, s) == hipSuccess;
   ok = ok && wait_record(s, mapped ? hdone : nullptr, seq);

@@ -576,20 +576,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   int64_t ld_left = -1, st_left = -1;
   bool pre_ok = false;  // pre[] holds the lane's whole current block
   if constexpr (IOV) {
-    if (live) {
-      ld_c = st_c = b.iovec_start[rec];
-      // Running pointers for the lane's first data block (d0 = q - 1, lane 0:
-      // L - 1) when the first chunk holds it, so the first load and store
-      // take the pointer path instead of a cursor walk (a descriptor load
-      // each, exposed: one before the rounds, one after).
-      const IovecDev f = ld_c < b.iovec_start[rec + 1] ? b.iovecs[ld_c] : IovecDev{nullptr, nullptr, 0};
-      const uint64_t p0 = 64 * (uint64_t)(q >= 1 ? q - 1 : L - 1);
-      if (p0 + 64 <= f.len) {
-        ld_ptr = f.in + p0;
-        st_ptr = f.out + p0;
-        ld_left = st_left = (int64_t)(f.len - p0);
-      }
-    }
+    if (live) ld_c = st_c = b.iovec_start[rec];
   }
   auto prefetch = [&](uint64_t u, uint4 pre[4]) {
     const uint64_t d = u - 1 - sh;
@@ -759,16 +746,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
         const bool next = p + n > k.ce;  // the block ended in the next chunk
         ld_c = st_c = next ? k.c + 1 : k.c;
         ld_cs = st_cs = next ? k.ce : k.cs;
-        // Running pointers for the lane's next block (64 L bytes on) when the
-        // chunk the block ended in holds it: no cursor walk for it.
-        const uint64_t pn = p + 64 * L, ce = next ? k.ce + nx.len : k.ce;
-        if (pn + 64 <= ce) {
-          ld_ptr = (next ? nx.in : k.in) + (pn - ld_cs);
-          st_ptr = (next ? nx.out : k.out) + (pn - st_cs);
-          ld_left = st_left = (int64_t)(ce - pn);
-        } else {
-          ld_left = st_left = -1;
-        }
+        ld_left = st_left = -1;
       } else {
         // A block over three or more chunks: 16-byte pieces;
         // the keystream waits in the staging slot and each piece's
@@ -1295,13 +1273,21 @@ __global__ __launch_bounds__(kOneThreads) void chacha_one_kernel(
            : nk     ? load_partial(src + 64 * t + 16 * k, nk)
                     : make_uint4(0, 0, 0, 0);
   }
+  // (The nonce and a short AD come by value from the single-record host path,
+  // BatchDesc::inl, so the keystream does not wait for them.)
   uint4 nw0 = make_uint4(0, 0, 0, 0), nw1 = make_uint4(0, 0, 0, 0);
-  if (live) {
+  if (!XC && (b.inl & 1)) {
+    nw0 = make_uint4(b.inl_nonce[0], b.inl_nonce[1], b.inl_nonce[2], 0);
+  } else if (live) {
     nw0 = load_partial(b.nonces, XC ? 16 : 12);
     if (XC) nw1 = load_partial(b.nonces + 16, 8);
   }
-  for (uint32_t a = t; a < nad; a += kOneThreads)
-    s_pb[a] = load_partial(b.ad + 16 * a, (uint32_t)min<uint64_t>(ad_len - 16 * a, 16));
+  if (b.inl & 2) {
+    if (t == 0 && nad) s_pb[0] = make_uint4(b.inl_ad[0], b.inl_ad[1], b.inl_ad[2], b.inl_ad[3]);
+  } else {
+    for (uint32_t a = t; a < nad; a += kOneThreads)
+      s_pb[a] = load_partial(b.ad + 16 * a, (uint32_t)min<uint64_t>(ad_len - 16 * a, 16));
+  }
   uint32_t key[8], nonce[3];
 #pragma unroll
   for (int i = 0; i < 8; i++) key[i] = keys->k[i];

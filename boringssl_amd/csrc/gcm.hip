@@ -956,6 +956,9 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   if constexpr (IOV) {
     if (live) {
       ld_c = st_c = b.iovec_start[rec];
+      // (Seeding the running pointers here from the first chunk, so the first
+      // load and store skip the cursor walk, measured neutral: 957-966 vs
+      // 951-966 GiB/s, profiles/r04/s14/.)
     }
   }
   // (Left undefined when not loaded: such a block is never stored or hashed
@@ -1280,14 +1283,18 @@ __global__ __launch_bounds__(1024) void gcm_keyset_kernel(const GcmKeyDev *__res
 // One record: the host-buffer calls (EVP_AEAD_CTX_seal / open / seal_scatter,
 // aead.cc.inc:163-209 -- SSLAEADContext::SealScatter makes them one record at
 // a time, ssl/ssl_aead_ctx.cc:299-381) as one launch of one workgroup with no
-// unit counter and no 128 KiB table build.  Thread t encrypts counter block t
-// (records up to kOneMaxBlocks), every load in flight at once (the record may
-// sit in mapped host memory); AES from T0 replicated per bank (32 KiB);
-// GHASH by lanes 0..15 at stride 16 with the bulk kernels' lane-rotated byte
-// table of H^16 (64 KiB, built from the key's nibble tables while the record
-// loads are in flight; 16 lookups per block instead of the nibble table's
-// 32).  Open computes the tag first and writes the plaintext (or zeros) after
-// the check.
+// unit counter and no 128 KiB table build.  Thread t encrypts counter block t,
+// every load in flight at once (the record may sit in mapped host memory);
+// AES from T0 replicated per bank (32 KiB); GHASH by lanes 0..15 at stride 16.
+// Two shapes (THREADS): records of up to 256 blocks (4 KiB) take 256 threads
+// and the key's nibble table of H^16 copied to LDS (8 KiB; in each lookup the
+// 16 lanes read the same nibble position, so a lane's bank quad is its nibble
+// value's and equal values share an address -- conflict-free whatever the
+// data); longer records take 1024 threads and the bulk kernels' lane-rotated
+// byte table of H^16 (64 KiB, built while the record loads are in flight; 16
+// lookups per GHASH step instead of 32): 16 KiB records 48 -> 39 us, while a
+// 1350-byte record lost 0.5 us to the build (profiles/r04/s13/).  Open
+// computes the tag first and writes the plaintext (or zeros) after the check.
 constexpr int kOneMaxBlocks = 1024;  // 16 KiB: threads per workgroup
 
 // acc * H^16 from the lane-rotated byte table (g8_rotate / g8_load, as the
@@ -1307,12 +1314,27 @@ __device__ __forceinline__ uint4 g8_mul16(uint4 acc, bool rs1, bool rs2, uint32_
   return xor4(r, g8_load<15>(h, P, g8));
 }
 
-template <int NR, bool OPEN>
-__global__ __launch_bounds__(kOneMaxBlocks) void gcm_one_kernel(const GcmKeyDev *__restrict__ keys,
-                                                                BatchDesc b) {
-  __shared__ __attribute__((aligned(16))) uint8_t g8[kG8Bytes];  // byte table of H^16
+// x * H^16 from the nibble table (key_setup.cc layout: position 2k = the high
+// nibble of byte k, 2k + 1 the low one).
+__device__ __forceinline__ uint4 nib_mul16(uint4 x, const uint4 *htab) {
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+  uint4 r = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const uint32_t byte = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+    r = xor4_3(r, htab[(2 * k) * 16 + (byte >> 4)], htab[(2 * k + 1) * 16 + (byte & 15u)]);
+  }
+  return r;
+}
+
+template <int NR, bool OPEN, int THREADS>
+__global__ __launch_bounds__(THREADS) void gcm_one_kernel(const GcmKeyDev *__restrict__ keys,
+                                                          BatchDesc b) {
+  constexpr bool kByte = THREADS == kOneMaxBlocks;  // byte table (else the nibble table)
+  __shared__ __attribute__((aligned(16))) uint8_t g8[kByte ? kG8Bytes : 16];
+  __shared__ uint4 htab[kByte ? 1 : 32 * 16];
   __shared__ uint32_t t0tab[256 * 32];
-  __shared__ uint4 cblk[kOneMaxBlocks];
+  __shared__ uint4 cblk[THREADS];
   __shared__ uint4 s_lh;  // len block x H ^ E_K(J0), from wave 1
   __shared__ uint32_t s_ok;
   const int t = threadIdx.x;
@@ -1321,23 +1343,37 @@ __global__ __launch_bounds__(kOneMaxBlocks) void gcm_one_kernel(const GcmKeyDev 
   const bool live = record_live(b, 0, m);
   const uint8_t *src = b.in + m.off;
   uint8_t *dst = b.out + m.off;
-  // Every load of the record (it may sit in mapped host memory, one PCIe
-  // round trip each) is issued first, together: this thread's block and the
-  // nonce, for wave 0 the first AD block, for open the received tag.
+  // The tables' loads first (device memory), then every load of the record
+  // (it may sit in mapped host memory, one PCIe round trip each), together:
+  // this thread's block, for open the received tag.  The nonce and a short AD
+  // come by value from the single-record host path (BatchDesc::inl), and the
+  // barrier below orders only the LDS writes, so the rounds run while the
+  // record is in flight (vmcnt counts in issue order: the tables' loads, issued
+  // first, complete without waiting for the record's).
   const uint32_t nbytes = (uint32_t)m.len;  // (<= 16 KiB: the launcher checks)
   const uint32_t nb = (nbytes + 15) / 16;
   const uint32_t n = (uint32_t)t < nb ? min(nbytes - 16u * t, 16u) : 0u;
+  for (int e = t; e < 256 * 32; e += THREADS) t0tab[e] = kTables.te0[e >> 5];
+  if constexpr (kByte)
+    build_g8<THREADS>(g8, reinterpret_cast<const uint4 *>(key->htab16), t);
+  else
+    for (int e = t; e < 32 * 16; e += THREADS) htab[e] = reinterpret_cast<const uint4 *>(key->htab16)[e];
+  uint4 ad0 = make_uint4(0, 0, 0, 0), nonce = make_uint4(0, 0, 0, 0), tr = ad0;
+  if (b.inl & 1)
+    nonce = make_uint4(b.inl_nonce[0], b.inl_nonce[1], b.inl_nonce[2], 0);
+  else if (live && b.nonce_len == 12)
+    nonce = load_partial(b.nonces, 12);  // (every thread's J0)
+  if (b.inl & 2)
+    ad0 = make_uint4(b.inl_ad[0], b.inl_ad[1], b.inl_ad[2], b.inl_ad[3]);
+  else if (t < 64 && live && m.ad_len)
+    ad0 = ad_block(b, 0, m, 0);
+  __builtin_amdgcn_sched_barrier(0);
   uint4 x = make_uint4(0, 0, 0, 0);
   if (n == 16)
     x = load16_any(src + 16 * t);
   else if (n)
     x = load_partial(src + 16 * t, n);
-  uint4 ad0 = make_uint4(0, 0, 0, 0), nonce = make_uint4(0, 0, 0, 0), tr = ad0;
-  if (live && b.nonce_len == 12) nonce = load_partial(b.nonces, 12);  // (every thread's J0)
-  if (t < 64 && live && m.ad_len) ad0 = ad_block(b, 0, m, 0);
   if (OPEN && t == 0 && live) tr = load_partial(batch_tag(b, 0), b.tag_len);  // the received tag
-  for (int e = t; e < 256 * 32; e += kOneMaxBlocks) t0tab[e] = kTables.te0[e >> 5];
-  build_g8<kOneMaxBlocks>(g8, reinterpret_cast<const uint4 *>(key->htab16), t);
   RoundKeys rk;
 #pragma unroll
   for (int r = 0; r <= NR; r++)
@@ -1347,7 +1383,10 @@ __global__ __launch_bounds__(kOneMaxBlocks) void gcm_one_kernel(const GcmKeyDev 
                    : b.nonce_len == 12 ? make_uint4(nonce.x, nonce.y, nonce.z, 0x01000000u)
                                        : record_j0(b, 0, key->hpow_ct);
   const uint32_t ctr0 = bswap32(j0.w);
-  __syncthreads();
+  // Barrier over the LDS tables only (no wait for the record's loads).
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
   // (Only threads with a block run the rounds: the waves past the record's
   // end issue no LDS lookups -- for a 1350-byte record 2 of the 16 waves.)
   uint4 y = make_uint4(0, 0, 0, 0);
@@ -1392,7 +1431,11 @@ __global__ __launch_bounds__(kOneMaxBlocks) void gcm_one_kernel(const GcmKeyDev 
     const uint32_t iters = live ? (nb + 15) / 16 : 0u;
     for (uint32_t it = 0; it < iters; it++) {
       const uint32_t j = 16 * it + q;
-      const uint4 h = g8_mul16(acc, rs1, rs2, rbs, P, g8);
+      uint4 h;
+      if constexpr (kByte)
+        h = g8_mul16(acc, rs1, rs2, rbs, P, g8);
+      else
+        h = nib_mul16(acc, htab);
       if (j < nb) acc = xor4(h, cblk[j]);
     }
     // Record end (finish_record's algebra) with the tag's last x H folded into
@@ -1908,7 +1951,11 @@ template <int NR, bool OPEN>
 int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const KernelEvents *ev) {
   if (one_record_batch(b) && gcm_mode(b) == 0) {
     if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
-    hipLaunchKernelGGL((gcm_one_kernel<NR, OPEN>), dim3(1), dim3(kOneMaxBlocks), 0, s, keys, b);
+    if (b.record_len <= 16 * 256)
+      hipLaunchKernelGGL((gcm_one_kernel<NR, OPEN, 256>), dim3(1), dim3(256), 0, s, keys, b);
+    else
+      hipLaunchKernelGGL((gcm_one_kernel<NR, OPEN, kOneMaxBlocks>), dim3(1), dim3(kOneMaxBlocks), 0,
+                         s, keys, b);
     const int rc = (int)hipGetLastError();
     if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
     return rc;

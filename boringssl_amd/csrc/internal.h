@@ -125,6 +125,12 @@ struct BatchDesc {
   // (the other kernels ignore it).
   uint32_t *done;
   uint32_t done_seq;
+  // ... and the record's 12-byte nonce (inl bit 0) and its AD of at most 16
+  // bytes, zero-padded (inl bit 1), passed by value, so the one-record kernels
+  // start the cipher while the record itself is still in flight.  0 otherwise.
+  uint32_t inl;
+  uint32_t inl_nonce[3];
+  uint32_t inl_ad[4];
 };
 
 // Tag / extra addresses of record i.
