@@ -881,7 +881,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
                                                 const UnitIn &in, const uint8_t *smem,
                                                 const GcmKeyDev *key, uint32_t lc0, uint32_t lc1,
                                                 int prio_base = 0) {
-  static_assert(L == 16 || L == 8, "lanes per record");
+  static_assert(L == 16 || L == 8 || L == 4, "lanes per record");
   const int q = threadIdx.x & (L - 1);
   const uint64_t rec = in.rec;
   const bool active = in.active, live = in.live;
@@ -1164,9 +1164,10 @@ __device__ __forceinline__ void fill_aes_tables(uint8_t *smem, int tid) {
 // of 64 / L records (in processing order) from a grid-wide counter, so waves
 // that the SIMD arbiter favours (older waves issue first) simply process more
 // units instead of waiting at a per-tile barrier for the slowest wave
-// (DESIGN.md §4.2).  L: lanes per record -- 8 (8 records per wave, GHASH
-// stride H^8) for aligned one-key batches, 16 for iovec records and unaligned
-// uniform batches (unaligned_uniform); the keyset kernel keeps 16.
+// (DESIGN.md §4.2).  L: lanes per record -- 4 for uniform batches of records
+// up to 4 KiB, 8 (8 records per wave, GHASH stride H^8) for other one-key
+// batches, 16 for iovec records and unaligned uniform batches of long records
+// (unaligned_uniform); the keyset kernel keeps 16.
 // (A kernel of its own, apart from the keyset kernel, so each gets its own
 // register allocation.)
 template <int NR, bool OPEN, bool XT, int W, bool IOV = false, int L = 16>
@@ -1924,9 +1925,12 @@ __global__ __launch_bounds__(1024) void gcm_keyset_bs16_kernel(const GcmKeyDev *
 
 
 
-// Lanes per record of the one-key kernel: 8 (stride H^8, 8 records per wave)
-// by default; 16 for iovec records and for uniform batches of records of
-// 4 KiB or more that are not 16-byte aligned, where a lane group's 16 L-byte
+// Lanes per record of the one-key kernel: 4 (stride H^4, 16 records per
+// wave) for uniform batches of records up to 4 KiB -- config G (1350 bytes)
+// 760-766 GiB/s at 8 lanes, 889-893 at 4, same box (profiles/r04/s19/): a
+// record's start and end are spread over twice the blocks per lane; 8 (stride
+// H^8) for other batches; 16 for iovec records and for uniform batches of
+// records of 4 KiB or more that are not 16-byte aligned, where a lane group's 16 L-byte
 // run costs an extra cache line per run -- relatively twice as much at L = 8.
 // 16 KiB records at a 16,385-byte stride: 823 GiB/s at L = 8, 1,076 at L = 16
 // (aligned: 1,146-1,177); 1350-byte records at a 1351-byte stride: 755 at
@@ -2038,6 +2042,9 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
                          dim3(kWaves * 64), 0, s, keys, bo, units);
     } else if (unaligned_uniform(b)) {
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, 16>), dim3(grid),
+                         dim3(kWaves * 64), 0, s, keys, bo, units);
+    } else if (!b.lengths && b.record_len <= 4096) {
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, 4>), dim3(grid),
                          dim3(kWaves * 64), 0, s, keys, bo, units);
     } else {
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, 8>), dim3(grid),
