@@ -848,8 +848,9 @@ struct UnitIn {
 };
 
 template <bool XT, bool IOV>
-__device__ __forceinline__ void unit_load(UnitIn &u, const BatchDesc &b, uint64_t i, int q) {
-  u.active = i < b.num_records;
+__device__ __forceinline__ void unit_load(UnitIn &u, const BatchDesc &b, uint64_t i, int q,
+                                          uint64_t end) {
+  u.active = i < end;
   u.rec = u.active ? rec_at(b, i) : 0;
   u.m = {0, 0, 0, 0, 0};
   u.live = false;
@@ -1196,11 +1197,17 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
     if (lane == 0) u = atomicAdd(units, 1u);
     return u;
   };
+  // Processing positions of this launch (BatchDesc::split).
+  uint64_t lo = 0, hi = n;
+  if (b.split) {
+    const uint32_t sp = *b.split;
+    if (b.split_side) lo = sp; else hi = sp;
+  }
   for (;;) {
-    const uint64_t first = (uint64_t)__builtin_amdgcn_readlane(claim(), 0) * (64 / L);
-    if (first >= n) break;
+    const uint64_t first = lo + (uint64_t)__builtin_amdgcn_readlane(claim(), 0) * (64 / L);
+    if (first >= hi) break;
     UnitIn in;
-    unit_load<XT, IOV>(in, b, first + lane / L, lane & (L - 1));
+    unit_load<XT, IOV>(in, b, first + lane / L, lane & (L - 1), hi);
     process_records<NR, OPEN, XT, L, false, IOV>(rk, b, in, smem, keys, lc0, lc1);
   }
 }
@@ -1273,7 +1280,7 @@ __global__ __launch_bounds__(1024) void gcm_keyset_kernel(const GcmKeyDev *__res
       const int t = wave * kRecPerWave + g;
       const bool active = (mask >> t) & 1;
       UnitIn in;
-      unit_load<XT, false>(in, b, active ? base + t : n, lane & 15);
+      unit_load<XT, false>(in, b, active ? base + t : n, lane & 15, n);
       process_records<NR, OPEN, XT, 16, true>(rk, b, in, smem, keys + k, lc0, lc1, wave >> 2);
       __builtin_amdgcn_s_setprio(0);
     }
@@ -2046,6 +2053,17 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
     } else if (!b.lengths && b.record_len <= 4096) {
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, 4>), dim3(grid),
                          dim3(kWaves * 64), 0, s, keys, bo, units);
+    } else if (order) {
+      // A ragged batch in length order: the records of 4 KiB or more at 8
+      // lanes, then the shorter ones at 4 (each launch with its own counter).
+      BatchDesc bl = bo, bs = bo;
+      bl.split = bs.split = order + b.num_records + kSplitWord;
+      bl.split_side = 0;
+      bs.split_side = 1;
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, 8>), dim3(grid),
+                         dim3(kWaves * 64), 0, s, keys, bl, units);
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, 4>), dim3(grid),
+                         dim3(kWaves * 64), 0, s, keys, bs, units + 8);
     } else {
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, 8>), dim3(grid),
                          dim3(kWaves * 64), 0, s, keys, bo, units);

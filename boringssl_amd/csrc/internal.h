@@ -93,6 +93,12 @@ struct BatchDesc {
   // Processing order (device, num_records entries) or null for 0..n-1; set by
   // the launchers for ragged batches (sched.hip), never by callers.
   const uint32_t *order;
+  // With `order`: the processing positions one launch covers, [0, *split)
+  // (split_side 0) or [*split, num_records) (split_side 1) -- the records of
+  // 4 KiB or more and the shorter ones of a ragged batch, which take kernels
+  // with different lanes per record (gcm.hip).  Null: every position.
+  const uint32_t *split;
+  uint32_t split_side;
   // Per-record precondition flags (device, 1 = the record may be sealed) or
   // null: the tls12/tls13 nonce checks of tls_scan.hip.  A record with flag 0
   // fails like a reference call that returned 0 (zeroed output, status 0).
@@ -159,6 +165,10 @@ int launch_gcm(const GcmKeyDev *keys, const BatchDesc &b, bool open,
 // `scratch` holds 128 uint32.  Returns 0 or a HIP error code.
 int build_length_order(const uint64_t *lengths, uint64_t n, uint32_t *order, uint32_t *scratch,
                        void *stream);
+// After build_length_order: processing positions [0, scratch[kSplitWord]) hold
+// the records of 4096 bytes or more, the rest the shorter ones (the class
+// cursor that ends at the first class below 4096 bytes, sched.hip).
+constexpr int kSplitWord = 64 + 47;
 // Whether a batch is worth reordering (ragged and large enough).
 inline bool wants_length_order(const BatchDesc &b) {
   return b.lengths && b.num_records >= 4096 && b.num_records < (uint64_t(1) << 32);
