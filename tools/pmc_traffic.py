@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise the rocprofv3 --pmc passes of tools/profile_r02.sh into
+"""Summarise the rocprofv3 --pmc passes of tools/profile.sh into
 profiles/traffic.json: per config, the bulk kernel's HBM bytes per launch and
 its LDS / VALU busy fractions, plus the FETCH/WRITE calibration copies.
 
@@ -36,13 +36,36 @@ def short_name(name):
 
 
 def load(path):
+    # Keyed by (kernel family, instantiation): a step may launch several
+    # instantiations of one family (config 4: the long records at 8 lanes, the
+    # short ones at 4), each once per step.
     out = collections.defaultdict(lambda: collections.defaultdict(list))
     p = os.path.join(path, "run_counter_collection.csv")
     if not os.path.exists(p):
         return out
     for r in csv.DictReader(open(p)):
-        out[short_name(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        full = r["Kernel_Name"].split("(bssl_amd")[0]
+        out[(short_name(r["Kernel_Name"]), full)][r["Counter_Name"]].append(
+            float(r["Counter_Value"]))
     return out
+
+
+def combine(entries):
+    """One family's per-step figures from its instantiations' summaries: bytes
+    summed (each runs once per step), busy and wait fractions weighted by each
+    instantiation's cycles."""
+    if len(entries) == 1:
+        return entries[0]
+    e = {"instantiations": len(entries)}
+    for k in ("fetch_bytes_corrected", "write_bytes", "hbm_bytes_per_launch",
+              "grbm_gui_active_per_xcd"):
+        if all(k in x for x in entries):
+            e[k] = sum(x[k] for x in entries)
+    cyc = [x.get("grbm_gui_active_per_xcd", 0) for x in entries]
+    for k in ("lds_busy", "valu_busy", "sq_wait_any_frac", "sq_wait_inst_any_frac"):
+        if all(k in x for x in entries) and sum(cyc):
+            e[k] = sum(x[k] * c for x, c in zip(entries, cyc)) / sum(cyc)
+    return e
 
 
 def summarise(c):
@@ -86,11 +109,14 @@ def main():
             for n, v in c.items():
                 per_cfg[m.group(1)][k][n].extend(v)
     for cfg, kernels in per_cfg.items():
-        res[cfg] = {k: summarise(c) for k, c in kernels.items()}
+        fam = collections.defaultdict(list)
+        for (family, _), c in sorted(kernels.items()):
+            fam[family].append(summarise(c))
+        res[cfg] = {k: combine(v) for k, v in fam.items()}
         res[cfg]["source"] = src
     calib = collections.defaultdict(dict)
     for sub, key in (("calib_fetch", "FETCH_SIZE"), ("calib_write", "WRITE_SIZE")):
-        for k, c in load(os.path.join(src, sub)).items():
+        for (k, _), c in load(os.path.join(src, sub)).items():
             base = k.split("<")[0]
             name = {"copy_rec4<0>": "copy_chacha", "copy_rec4<1>": "copy_quad"}.get(k, base)
             if name not in CALIB_KNOWN or key not in c:
