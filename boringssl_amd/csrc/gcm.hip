@@ -1166,9 +1166,11 @@ __device__ __forceinline__ void fill_aes_tables(uint8_t *smem, int tid) {
 // that the SIMD arbiter favours (older waves issue first) simply process more
 // units instead of waiting at a per-tile barrier for the slowest wave
 // (DESIGN.md §4.2).  L: lanes per record -- 4 for uniform batches of records
-// up to 4 KiB, 8 (8 records per wave, GHASH stride H^8) for other one-key
-// batches, 16 for iovec records and unaligned uniform batches of long records
-// (unaligned_uniform); the keyset kernel keeps 16.
+// up to 4 KiB on 64-byte runs (runs_in_lines) and the short records of
+// ragged and iovec batches, 8 (8 records per wave, GHASH stride H^8) for other
+// one-key batches and iovec records of 2-4 KiB, 16 for iovec records of 4 KiB
+// or more and unaligned uniform batches of long records (unaligned_uniform);
+// the keyset kernel keeps 16.
 // (A kernel of its own, apart from the keyset kernel, so each gets its own
 // register allocation.)
 template <int NR, bool OPEN, bool XT, int W, bool IOV = false, int L = 16>
@@ -1178,10 +1180,16 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
   __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
+  const uint64_t n = b.num_records;
+  // Processing positions of this launch (BatchDesc::split_lo/_hi); a launch
+  // for an empty length class ends before building its tables.
+  uint64_t lo = 0, hi = n;
+  if (b.split_lo) lo = *b.split_lo;
+  if (b.split_hi) hi = *b.split_hi;
+  if (lo >= hi) return;
   fill_aes_tables<kThreads>(smem, tid);
   const uint32_t lc0 = kLdsAes + (uint32_t)(lane & 31) * 4u;
   const uint32_t lc1 = lc0 + 128u;
-  const uint64_t n = b.num_records;
   if constexpr (L == 16)
     build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab16), tid);
   else
@@ -1197,12 +1205,6 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
     if (lane == 0) u = atomicAdd(units, 1u);
     return u;
   };
-  // Processing positions of this launch (BatchDesc::split).
-  uint64_t lo = 0, hi = n;
-  if (b.split) {
-    const uint32_t sp = *b.split;
-    if (b.split_side) lo = sp; else hi = sp;
-  }
   for (;;) {
     const uint64_t first = lo + (uint64_t)__builtin_amdgcn_readlane(claim(), 0) * (64 / L);
     if (first >= hi) break;
@@ -1949,6 +1951,16 @@ bool unaligned_uniform(const BatchDesc &b) {
            b.record_stride) & 15) != 0;
 }
 
+// 4 lanes per record only when every record starts a 64-byte run (each
+// group's 64-byte run then stays in one 128-byte line): 1M x 1350-byte records
+// at a 1360-byte stride 646-659 GiB/s at 4 lanes against 757-761 at 8, and
+// 4000-byte records 786-804 against 986-993 (profiles/r04/s24/); at a
+// 1408-byte stride (config G) 4 lanes are the faster.
+bool runs_in_lines(const BatchDesc &b) {
+  return ((reinterpret_cast<uintptr_t>(b.in) | reinterpret_cast<uintptr_t>(b.out) |
+           b.record_stride) & 63) == 0;
+}
+
 // Engine for a batch: 0 = the T-table kernels (default), 1 = the table-free
 // bs16 engine (BSSL_AMD_GCM_MODE=bs16) for every batch: one key or keysets,
 // any record shape, extra bytes, iovecs, single records.
@@ -2041,7 +2053,22 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
       else
         hipLaunchKernelGGL((gcm_keyset_kernel<NR, OPEN, false, kWaves>), dim3(grid),
                            dim3(kWaves * 64), 0, s, keys, bo);
-    } else if (b.iovecs) {  // (one key: the ctx API)
+    } else if (b.iovecs && order) {  // (one key: the ctx API)
+      // iovec records in length order (their totals are `lengths`): 16 lanes
+      // for the records of 4 KiB or more, 8 from 2 KiB, 4 below (1M x 1350 B
+      // in three chunks 370 -> 520 GiB/s, 512K x 3000 B 534 -> 680 against
+      // 4 lanes for both; profiles/r04/s24/, s26/).  A launch whose class is
+      // empty ends at once (gcm_kernel).
+      BatchDesc bl = bo, bm = bo, bs = bo;
+      bl.split_hi = bm.split_lo = order + b.num_records + kSplitWord;
+      bm.split_hi = bs.split_lo = order + b.num_records + kSplitWord2k;
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, true, 16>), dim3(grid),
+                         dim3(kWaves * 64), 0, s, keys, bl, units);
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, true, 8>), dim3(grid),
+                         dim3(kWaves * 64), 0, s, keys, bm, units + 4);
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, true, 4>), dim3(grid),
+                         dim3(kWaves * 64), 0, s, keys, bs, units + 8);
+    } else if (b.iovecs) {
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, true, 16>), dim3(grid),
                          dim3(kWaves * 64), 0, s, keys, bo, units);
     } else if (b.extra_len) {
@@ -2050,16 +2077,14 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
     } else if (unaligned_uniform(b)) {
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, 16>), dim3(grid),
                          dim3(kWaves * 64), 0, s, keys, bo, units);
-    } else if (!b.lengths && b.record_len <= 4096) {
+    } else if (!b.lengths && b.record_len <= 4096 && runs_in_lines(b)) {
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, 4>), dim3(grid),
                          dim3(kWaves * 64), 0, s, keys, bo, units);
     } else if (order) {
       // A ragged batch in length order: the records of 4 KiB or more at 8
       // lanes, then the shorter ones at 4 (each launch with its own counter).
       BatchDesc bl = bo, bs = bo;
-      bl.split = bs.split = order + b.num_records + kSplitWord;
-      bl.split_side = 0;
-      bs.split_side = 1;
+      bl.split_hi = bs.split_lo = order + b.num_records + kSplitWord;
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, 8>), dim3(grid),
                          dim3(kWaves * 64), 0, s, keys, bl, units);
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, 4>), dim3(grid),

@@ -93,12 +93,12 @@ struct BatchDesc {
   // Processing order (device, num_records entries) or null for 0..n-1; set by
   // the launchers for ragged batches (sched.hip), never by callers.
   const uint32_t *order;
-  // With `order`: the processing positions one launch covers, [0, *split)
-  // (split_side 0) or [*split, num_records) (split_side 1) -- the records of
-  // 4 KiB or more and the shorter ones of a ragged batch, which take kernels
-  // with different lanes per record (gcm.hip).  Null: every position.
-  const uint32_t *split;
-  uint32_t split_side;
+  // With `order`: the processing positions one launch covers, [*split_lo,
+  // *split_hi) (null: 0 and num_records) -- length classes of a ragged batch
+  // (records of 4 KiB or more, the shorter ones, ...), which take kernels with
+  // different lanes per record (gcm.hip).
+  const uint32_t *split_lo;
+  const uint32_t *split_hi;
   // Per-record precondition flags (device, 1 = the record may be sealed) or
   // null: the tls12/tls13 nonce checks of tls_scan.hip.  A record with flag 0
   // fails like a reference call that returned 0 (zeroed output, status 0).
@@ -169,6 +169,8 @@ int build_length_order(const uint64_t *lengths, uint64_t n, uint32_t *order, uin
 // the records of 4096 bytes or more, the rest the shorter ones (the class
 // cursor that ends at the first class below 4096 bytes, sched.hip).
 constexpr int kSplitWord = 64 + 47;
+// ... and [0, scratch[kSplitWord2k]) the records of 2048 bytes or more.
+constexpr int kSplitWord2k = 64 + 55;
 // Whether a batch is worth reordering (ragged and large enough).
 inline bool wants_length_order(const BatchDesc &b) {
   return b.lengths && b.num_records >= 4096 && b.num_records < (uint64_t(1) << 32);
