@@ -72,7 +72,7 @@ EXPORTED_SYMBOLS = [
     "BSSL_AMD_KEYSET_seal_batch_device", "BSSL_AMD_KEYSET_open_batch_device",
     "BSSL_AMD_set_device", "BSSL_AMD_device_count", "BSSL_AMD_synth_fill_device",
     "BSSL_AMD_set_kernel_timing", "BSSL_AMD_collect_kernel_times", "BSSL_AMD_last_kernel_ms",
-    "BSSL_AMD_last_kernel_name",
+    "BSSL_AMD_last_kernel_name", "BSSL_AMD_set_aes_gcm_engine", "BSSL_AMD_aes_gcm_engine",
     # include/bssl_amd/tls.h
     "BSSL_AMD_TLS_AEAD_new", "BSSL_AMD_TLS_AEAD_free", "BSSL_AMD_TLS_AEAD_prefix_len",
     "BSSL_AMD_TLS_AEAD_suffix_len", "BSSL_AMD_TLS_AEAD_sequence",
@@ -163,6 +163,8 @@ _SIGS = {
     "BSSL_AMD_collect_kernel_times": (_S, [ctypes.POINTER(ctypes.c_double), _S]),
     "BSSL_AMD_last_kernel_ms": (ctypes.c_double, []),
     "BSSL_AMD_last_kernel_name": (ctypes.c_char_p, []),
+    "BSSL_AMD_set_aes_gcm_engine": (_I, [_I]),
+    "BSSL_AMD_aes_gcm_engine": (_I, []),
     "BSSL_AMD_TLS_AEAD_new": (_P, [_I, ctypes.c_uint16, _P, _P, _S, _P, _S, ctypes.c_uint64]),
     "BSSL_AMD_TLS_AEAD_free": (None, [_P]),
     "BSSL_AMD_TLS_AEAD_prefix_len": (_S, [_P]),
@@ -475,6 +477,22 @@ def collect_kernel_times(max_n=4096):
     buf = (ctypes.c_double * max_n)()
     n = _lib.BSSL_AMD_collect_kernel_times(buf, max_n)
     return [buf[i] for i in range(min(n, max_n))]
+
+
+AES_GCM_ENGINES = {"table": 0, "bs": 1}
+
+
+def set_aes_gcm_engine(engine):
+    """Selects the AES-GCM engine ("bs": bitsliced, table-free; "table": LDS
+    T-tables) for every later batch of this process; returns the previous one."""
+    prev = _lib.BSSL_AMD_set_aes_gcm_engine(AES_GCM_ENGINES[engine])
+    if prev < 0:
+        raise ValueError(engine)
+    return {v: k for k, v in AES_GCM_ENGINES.items()}[prev]
+
+
+def aes_gcm_engine():
+    return {v: k for k, v in AES_GCM_ENGINES.items()}[_lib.BSSL_AMD_aes_gcm_engine()]
 
 
 def last_kernel_name():

@@ -1294,6 +1294,9 @@ size_t BSSL_AMD_collect_kernel_times(double *out_ms, size_t max) {
   return n;
 }
 
+int BSSL_AMD_set_aes_gcm_engine(int engine) { return set_gcm_engine(engine); }
+int BSSL_AMD_aes_gcm_engine(void) { return gcm_engine(); }
+
 double BSSL_AMD_last_kernel_ms(void) { return t_timing.last_ms; }
 const char *BSSL_AMD_last_kernel_name(void) { return t_timing.last_name; }
 

@@ -102,4 +102,54 @@ __device__ __forceinline__ void bs16_cipher(uint32_t (&p)[4][2][8],
   }
 }
 
+// Rounds 1..NR with the AddRoundKey masks taken from the key's precomputed
+// table (GcmKeyDev::bsmask: 64 words per round, mask of register (r, h, b)
+// at 32*h + 8*r + b).  `mk` is wave-uniform, so the masks arrive by scalar
+// loads (4 x s_load_dwordx16 per round) instead of ~5 SALU operations each.
+template <int NR>
+__device__ __forceinline__ void bs16_cipher_tab(uint32_t (&p)[4][2][8],
+                                                const uint32_t *__restrict__ mk) {
+#pragma unroll 1
+  for (int rd = 1; rd <= NR; rd++) {
+    const uint32_t *__restrict__ m = mk + 64 * rd;
+    const bool last = rd == NR;
+    uint32_t np[4][2][8];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      uint32_t a[4][8];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        sbox_planes(p[r][(h + r) & 1], a[r]);
+        if (((h + r) >> 1) & 1) {
+#pragma unroll
+          for (int b = 0; b < 8; b++) a[r][b] = swap16(a[r][b]);
+        }
+      }
+      if (!last) {
+        uint32_t km[4][8], o[4][8];
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+          for (int b = 0; b < 8; b++) km[r][b] = m[32 * h + 8 * r + b];
+        bs16_mix(a, o, km);
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+          for (int b = 0; b < 8; b++) np[r][h][b] = o[r][b];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+          for (int b = 0; b < 8; b++) np[r][h][b] = a[r][b] ^ m[32 * h + 8 * r + b];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int b = 0; b < 8; b++) p[r][h][b] = np[r][h][b];
+  }
+}
+
 }  // namespace bssl_amd

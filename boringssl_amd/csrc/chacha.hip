@@ -7,16 +7,16 @@
 // poly1305.cc) / the fused chacha20_poly1305_seal_avx2 (chacha20_poly1305_
 // x86_64.pl:861).  Design:
 //
-// * L = 4 lanes per record, 16 records per wave (8 lanes measured 16 % slower:
-//   the per-record serial Poly1305 work -- powers of r, lane tree, final
-//   reduction -- is amortized over fewer blocks per lane).  The record's ChaCha blocks
-//   u = 0..n (u = 0: the Poly1305 key block, counter 0; u >= 1: data block u-1,
-//   counter u, RFC 8439) are dealt round-robin to the lanes: one lane per
-//   64-byte block, keystream XORed with the input in registers.  Folding the
-//   key block into slot 0 keeps a 1350-byte record at 23 blocks in 24 slots.
-// * Registers: the powers of r live in LDS (per record) and the first
-//   ciphertext block waits in LDS while they are built, so the kernel fits
-//   128 VGPRs (4 waves per SIMD).
+// * L = 2 lanes per record (kLanes below), 32 records per wave, 3 waves per
+//   SIMD at ~150-170 VGPRs (4 lanes at 128 VGPRs / 4 waves spilled and ran
+//   slower: the per-record serial Poly1305 work -- powers of r, lane tree,
+//   final reduction -- is amortized over fewer blocks per lane).  The record's
+//   ChaCha blocks u = 0..n (u = 0: the Poly1305 key block, counter 0; u >= 1:
+//   data block u-1, counter u, RFC 8439) are dealt round-robin to the lanes:
+//   one lane per 64-byte block, keystream XORed with the input in registers.
+// * Registers: the powers of r and the block loop's multipliers live in LDS
+//   (per record); record-aligned batches stage their blocks through LDS by
+//   LDS-DMA (record-contiguous I/O).
 // * Poly1305: the four 16-byte Poly blocks of data block d form one unit
 //   U = M0 r^3 + M1 r^2 + M2 r + M3.  A lane folds its units with Horner's
 //   rule in R = r^4 at stride L (multiplier R^L), one lazily reduced sum of
@@ -493,7 +493,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   // AD block k of an iovec record: bytes of its CRYPTO_IVEC chunks.
   auto ivec_block = [&](uint64_t k, uint32_t w[4]) {
     const uint4 v = ivec_load16(b.aadvecs, b.aadvec_start[rec], b.aadvec_start[rec + 1], 16 * k,
-                                (uint32_t)min<uint64_t>(m.ad_len - 16 * k, 16));
+                                (uint32_t)umin64(m.ad_len - 16 * k, 16));
     w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
   };
   {
@@ -503,7 +503,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
       if constexpr (IOV)
         ivec_block(k, adw);
       else
-        load16_partial(ad + 16 * k, (uint32_t)min<uint64_t>(m.ad_len - 16 * k, 16), adw);
+        load16_partial(ad + 16 * k, (uint32_t)umin64(m.ad_len - 16 * k, 16), adw);
     }
   }
   // Message = the record's `in` bytes then b.extra_len extra bytes
@@ -641,7 +641,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     uint32_t x[16], y[16];
     if constexpr (IOV) {
       const uint64_t p = 64 * d;
-      const uint32_t n = (uint32_t)min<uint64_t>(rem, 64);
+      const uint32_t n = (uint32_t)umin64(rem, 64);
       const uint64_t c_end = b.iovec_start[rec + 1];
       uint8_t *my = stage + 16 * lane;  // piece i at + 1024 i
       if (pre_ok) {
@@ -722,7 +722,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
         for (int i = 0; i < 4; i++) {
           const uint32_t ni = n > 16u * i ? min(n - 16u * i, 16u) : 0u;
           const uint64_t pi = p + 16 * i;
-          const uint32_t n1 = pi < k.ce ? (uint32_t)min<uint64_t>(ni, k.ce - pi) : 0u;
+          const uint32_t n1 = pi < k.ce ? (uint32_t)umin64(ni, k.ce - pi) : 0u;
           const uint32_t n2 = ni - n1;
           const uint8_t *sa = k.in + (pi - k.cs);
           const uint8_t *sb = n2 ? nx.in + (pi + n1 - k.ce) : nx.in;
@@ -810,7 +810,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     } else if constexpr (ANY) {
       static_assert(!XT && !COAL && !IOV, "ANY kernels: plain per-lane records");
       uint8_t *dp = dst + 64 * d;
-      const uint32_t n = (uint32_t)min<uint64_t>(rem, 64);
+      const uint32_t n = (uint32_t)umin64(rem, 64);
       if (n == 64) {
         // A full block at any alignment (one dwordx4 per 16 bytes).
 #pragma unroll
@@ -864,7 +864,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
       // holding record bytes), dword / short / byte stores.
       const uint8_t *sp = src + 64 * d;
       uint8_t *dp = dst + 64 * d;
-      const uint32_t n = (uint32_t)min<uint64_t>(rem, 64);
+      const uint32_t n = (uint32_t)umin64(rem, 64);
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const uint32_t nk = n > 16u * k ? min(n - 16u * k, 16u) : 0u;
@@ -881,7 +881,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     } else if (!XT) {
       const uint8_t *sp = src + 64 * d;
       uint8_t *dp = dst + 64 * d;
-      const uint32_t n = (uint32_t)min<uint64_t>(rem, 64);
+      const uint32_t n = (uint32_t)umin64(rem, 64);
 #pragma unroll
       for (int i = 0; i < 16; i++) {
         x[i] = load_le32_bytes(sp + 4 * i, n > 4u * i ? n - 4u * i : 0);
@@ -892,7 +892,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
       }
       for (uint32_t i = 0; i < n; i++) dp[i] = (uint8_t)(y[i >> 2] >> (8 * (i & 3)));
     } else {
-      crypt_block_x(src, dst, m.len, xin, xout, 64 * d, (uint32_t)min<uint64_t>(rem, 64), ks, x,
+      crypt_block_x(src, dst, m.len, xin, xout, 64 * d, (uint32_t)umin64(rem, 64), ks, x,
                     y);
     }
 #pragma unroll
@@ -982,7 +982,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   {
     const uint8_t *ad = b.ad + (live ? m.ad_off : 0);
     const uint64_t nab = live ? (m.ad_len + 15) / 16 : 0;
-    const int wmax = wave_max((int)min<uint64_t>(nab, 0x7fffffff));
+    const int wmax = wave_max((int)umin64(nab, 0x7fffffff));
     auto ad_block = [&](uint64_t k) {
       if constexpr (IOV) {
         uint32_t w[4];
@@ -1203,7 +1203,7 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
     }
   } else if (active && !ok) {
     for (uint64_t j = q; j * 16 < m.len; j += L) {
-      const uint64_t n = min<uint64_t>(m.len - j * 16, 16);
+      const uint64_t n = umin64(m.len - j * 16, 16);
       for (uint64_t i = 0; i < n; i++) dst[j * 16 + i] = 0;
     }
     if (q == 0)
@@ -1263,7 +1263,7 @@ __global__ __launch_bounds__(kOneThreads) void chacha_one_kernel(
   const uint8_t *src = b.in;
   uint8_t *dst = b.out;
   // Loads first: the lane's 64-byte block, the nonce, the AD blocks.
-  const uint32_t n = t < kOneBlocks && 64u * t < len ? (uint32_t)min<uint64_t>(len - 64u * t, 64)
+  const uint32_t n = t < kOneBlocks && 64u * t < len ? (uint32_t)umin64(len - 64u * t, 64)
                                                      : 0u;
   uint4 x[4];
 #pragma unroll
@@ -1286,7 +1286,7 @@ __global__ __launch_bounds__(kOneThreads) void chacha_one_kernel(
     if (t == 0 && nad) s_pb[0] = make_uint4(b.inl_ad[0], b.inl_ad[1], b.inl_ad[2], b.inl_ad[3]);
   } else {
     for (uint32_t a = t; a < nad; a += kOneThreads)
-      s_pb[a] = load_partial(b.ad + 16 * a, (uint32_t)min<uint64_t>(ad_len - 16 * a, 16));
+      s_pb[a] = load_partial(b.ad + 16 * a, (uint32_t)umin64(ad_len - 16 * a, 16));
   }
   uint32_t key[8], nonce[3];
 #pragma unroll

@@ -32,12 +32,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <type_traits>
 
 #include "internal.h"
 #include "iov_dev.h"
-#include "bs16_aes.h"
-#include "gf128_ct.h"
+#include "gcm_common.h"
 
 
 namespace bssl_amd {
@@ -100,30 +100,11 @@ __constant__ Tables kTables = make_tables();
 //   [65536, 131072)  AES T0/T1, replicated per bank (see header comment); the
 //                    lookup address carries bit 16 (lane constants lc0/lc1)
 //   [131072, ...)    tile plan (keys and record masks of the passes)
-constexpr uint32_t kLdsG8 = 0;
-constexpr uint32_t kG8Bytes = 256 * 256;
 constexpr uint32_t kLdsAes = kG8Bytes;
 constexpr uint32_t kAesLdsBytes = 256 * 256;
 constexpr uint32_t kLdsPlan = kLdsAes + kAesLdsBytes;
 constexpr uint32_t kLdsBasis = kLdsPlan + 64 * 16 + 16;  // 128 x 16 B (build_gpow)
 constexpr uint32_t kLdsBytes = kLdsBasis + 128 * 16;
-
-__device__ __forceinline__ uint32_t rotl(uint32_t v, int n) {
-  return __builtin_amdgcn_alignbit(v, v, 32 - n);
-}
-
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32, gfx950
-}
-
-__device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
-  return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
-}
-
-__device__ __forceinline__ uint4 xor4_3(uint4 a, uint4 b, uint4 c) {
-  return make_uint4(xor3(a.x, b.x, c.x), xor3(a.y, b.y, c.y), xor3(a.z, b.z, c.z),
-                    xor3(a.w, b.w, c.w));
-}
 
 // ---------------------------------------------------------------------------
 // AES.  State: 4 little-endian column words (byte r of word c = row r).
@@ -275,41 +256,6 @@ __device__ __forceinline__ uint4 quad_gather(uint32_t w) {
 }
 
 // ---------------------------------------------------------------------------
-// GHASH multiply by H^16 with the lane-rotated byte table (kLdsG8), spread
-// over the AES rounds of the same iteration.  Lane q (its index within the
-// record's 16 lanes) looks up byte position (t + q) mod 16 in step t, so the
-// 16 lanes of each ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,
-// 28-31}, +32) read 16 different 16-byte slots of the 256-byte row: no bank
-// conflicts, 16 lookups per block instead of 32 nibble lookups.  The input is
-// rotated by q bytes once (r), so step t takes byte t of r with a
-// wave-uniform selector; P[k] byte i holds the slot offset ((4k+i+q) mod 16)*16.
-struct Gh8 {
-  uint32_t r0, r1, r2, r3;  // multiplier input, rotated down by q bytes
-  uint4 g;                  // running sum of the looked-up products
-};
-
-// r byte t = x byte (t + q) mod 16, q = 4*s + bsh (s1 = s&1, s2 = s&2).
-__device__ __forceinline__ void g8_rotate(Gh8 &h, uint4 x, bool s1, bool s2, uint32_t bsh) {
-  const uint32_t e0 = s1 ? x.y : x.x, e1 = s1 ? x.z : x.y, e2 = s1 ? x.w : x.z,
-                 e3 = s1 ? x.x : x.w;
-  const uint32_t d0 = s2 ? e2 : e0, d1 = s2 ? e3 : e1, d2 = s2 ? e0 : e2, d3 = s2 ? e1 : e3;
-  h.r0 = __builtin_amdgcn_alignbyte(d1, d0, bsh);
-  h.r1 = __builtin_amdgcn_alignbyte(d2, d1, bsh);
-  h.r2 = __builtin_amdgcn_alignbyte(d3, d2, bsh);
-  h.r3 = __builtin_amdgcn_alignbyte(d0, d3, bsh);
-}
-
-template <int T>
-__device__ __forceinline__ uint4 g8_load(const Gh8 &h, const uint32_t (&P)[4],
-                                         const uint8_t *smem) {
-  const uint32_t r = T < 4 ? h.r0 : T < 8 ? h.r1 : T < 12 ? h.r2 : h.r3;
-  const uint32_t a =
-      __builtin_amdgcn_perm(r, P[T >> 2], 0x0c0c0000u | ((4u + (T & 3)) << 8) | (T & 3));
-  return *reinterpret_cast<const uint4 *>(smem + kLdsG8 + a);
-}
-
-typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-
 // Counter-mode cache of one AES stream (see process_records).
 struct WindowCache {
   uint32_t win = 0xffffffffu, k1 = 0, k2 = 0, k3 = 0, l0 = 0, l1 = 0, l2 = 0, l3 = 0;
@@ -349,21 +295,6 @@ struct WindowCache {
 };
 
 #include "gcm_rounds.inc"
-
-__device__ __forceinline__ uint4 as_uint4(v4u v) { return make_uint4(v.x, v.y, v.z, v.w); }
-
-// Materializes v here: an empty volatile asm using it keeps hipcc from
-// sinking the XORs that produce it past the following asm rounds (which
-// would keep every round's 16-byte GHASH reads live at once).
-__device__ __forceinline__ void pin4(uint4 &v) {
-  asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
-}
-
-// GHASH byte-table selector of step T (see g8_load).
-template <int T>
-constexpr uint32_t g8_sel() {
-  return 0x0c0c0000u | ((4u + (T & 3)) << 8) | (T & 3);
-}
 
 // GHASH steps carried by middle round i (rounds 3..NR-1 -> i = 0..NR-4) of
 // the one-block-per-lane kernel: AES-128 has 7 such rounds (3,3,2,2,2,2,2),
@@ -455,193 +386,6 @@ __device__ __forceinline__ void rounds_s1(uint32_t (&a)[4], const RoundKeys &rk,
 
 
 
-__device__ __forceinline__ uint32_t bswap32(uint32_t v) {
-  return __builtin_amdgcn_perm(0, v, 0x00010203u);
-}
-
-__device__ __forceinline__ int wave_max(int v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-  return v;
-}
-
-// The per-record reductions of the bulk kernel use readlane / DPP rather than
-// LDS shuffles (ds_bpermute goes through the LDS queue, which the AES and
-// GHASH lookups of the other waves keep ~84 % busy, and its lane-index
-// operands were spilled and reloaded once per unit).
-
-// Maximum over the wave of a value that is uniform within each L-lane group
-// (a record's iteration count): one readlane per group.
-template <int L>
-__device__ __forceinline__ int group_max(int v) {
-  int m = __builtin_amdgcn_readlane(v, 0);
-#pragma unroll
-  for (int k = 1; k < 64 / L; k++) m = max(m, __builtin_amdgcn_readlane(v, k * L));
-  return m;
-}
-
-// XOR of a word over the 16 lanes of its row, in every lane of the row:
-// rotations by 8 and 4 within the row, then the quad permutations 1032 and
-// 2301 (DPP row_ror / quad_perm; XOR is commutative, so rotations reduce as
-// well as butterflies do).
-__device__ __forceinline__ uint32_t row_xor16(uint32_t v) {
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false);  // row_ror:4
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false);   // quad 2301
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false);   // quad 1032
-  return v;
-}
-
-// len = the record's `in` bytes; xlen = extra bytes sealed after them
-// (BatchDesc::extra), so the message is len + xlen bytes.
-struct RecordMeta {
-  uint64_t off, len, ad_off, ad_len;
-  uint32_t xlen;
-};
-
-// Per-record arrays read without branches when the batch has any: a missing
-// array (null pointer, the uniform-layout field applies) is read at kMetaZero
-// instead, so the loads are issued together (under per-array null-pointer
-// branches hipcc waited for each load before issuing the next).  A batch with
-// none of them takes the uniform layout with no loads at all.
-__device__ const uint64_t kMetaZero[2] = {0, 0};
-
-template <typename T>
-__device__ __forceinline__ T meta_load(const T *arr, uint64_t i) {
-  const T *p = arr ? arr + i : reinterpret_cast<const T *>(kMetaZero);
-  return *p;
-}
-
-__device__ __forceinline__ RecordMeta record_meta(const BatchDesc &b, uint64_t i) {
-  RecordMeta m;
-  if (!(b.offsets || b.lengths || b.ad_offsets || b.ad_lengths)) {  // uniform layout: no loads
-    m.off = i * b.record_stride;
-    m.len = b.record_len;
-    m.ad_off = i * b.ad_stride;
-    m.ad_len = b.ad_len;
-    m.xlen = b.extra_len;
-    return m;
-  }
-  const uint64_t off = meta_load(b.offsets, i), len = meta_load(b.lengths, i);
-  const uint64_t ado = meta_load(b.ad_offsets, i), adl = meta_load(b.ad_lengths, i);
-  m.off = b.offsets ? off : i * b.record_stride;
-  m.len = b.lengths ? len : b.record_len;
-  m.ad_off = b.ad_offsets ? ado : i * b.ad_stride;
-  m.ad_len = b.ad_lengths ? adl : b.ad_len;
-  m.xlen = b.extra_len;
-  return m;
-}
-
-// Bytes [p0, p0 + n) of a record's message: `in` bytes below len, then the
-// extra bytes (load), and the same split for the output (store).
-__device__ __forceinline__ uint4 load_partial_x(const uint8_t *src, uint64_t len,
-                                                const uint8_t *x, uint64_t p0, uint32_t n) {
-  uint32_t w[4] = {0, 0, 0, 0};
-  for (uint32_t i = 0; i < n; i++) {
-    const uint64_t k = p0 + i;
-    w[i >> 2] |= (uint32_t)(k < len ? src[k] : x[k - len]) << (8 * (i & 3));
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-__device__ __forceinline__ void store_partial_x(uint8_t *dst, uint64_t len, uint8_t *x,
-                                                uint64_t p0, uint4 v, uint32_t n) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  for (uint32_t i = 0; i < n; i++) {
-    const uint64_t k = p0 + i;
-    const uint8_t c = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
-    if (k < len)
-      dst[k] = c;
-    else
-      x[k - len] = c;
-  }
-}
-
-// The block of a record that reaches into its extra bytes (one per record at
-// most; only in the XT kernels).  Returns the masked output block; `x`
-// receives the input block.
-__device__ __forceinline__ uint4 crypt_partial_x(const uint8_t *src, uint8_t *dst, uint64_t len,
-                                              const uint8_t *xin, uint8_t *xout, uint64_t p0,
-                                              uint4 ks, uint32_t n, uint4 &x) {
-  x = load_partial_x(src, len, xin, p0, n);
-  const uint4 y = mask_block(make_uint4(x.x ^ ks.x, x.y ^ ks.y, x.z ^ ks.z, x.w ^ ks.w), n);
-  store_partial_x(dst, len, xout, p0, y, n);
-  return y;
-}
-
-// 16-byte block loads and stores at any address (u32_any, iov_dev.h).
-
-__device__ __forceinline__ uint4 load_blk_nt(const uint8_t *p) {
-  const u32_any *ip = reinterpret_cast<const u32_any *>(p);
-  return make_uint4(__builtin_nontemporal_load(ip), __builtin_nontemporal_load(ip + 1),
-                    __builtin_nontemporal_load(ip + 2), __builtin_nontemporal_load(ip + 3));
-}
-
-__device__ __forceinline__ void store_blk_nt(uint8_t *p, uint4 y) {
-  u32_any *o = reinterpret_cast<u32_any *>(p);
-  __builtin_nontemporal_store(y.x, o);
-  __builtin_nontemporal_store(y.y, o + 1);
-  __builtin_nontemporal_store(y.z, o + 2);
-  __builtin_nontemporal_store(y.w, o + 3);
-}
-
-// Record at processing position i (sched.hip's length order, if any).
-__device__ __forceinline__ uint64_t rec_at(const BatchDesc &b, uint64_t i) {
-  return b.order ? (uint64_t)b.order[i] : i;  // (one load; no order array: none)
-}
-
-
-// XOR of a word over the L lanes of its group (L = 16: row_xor16; L = 8:
-// row_half_mirror then the quad permutations; L = 4: the quad permutations),
-// in every lane of the group.
-template <int L>
-__device__ __forceinline__ uint32_t row_xor(uint32_t v) {
-  static_assert(L == 16 || L == 8 || L == 4, "lanes per record");
-  if constexpr (L == 16) return row_xor16(v);
-  if constexpr (L == 8)
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false);  // half mirror
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false);    // quad 2301
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false);    // quad 1032
-  return v;
-}
-
-// Per-record state handed from the bs16 engine's prologue (gcm_prologue_bs16)
-// to its bulk kernels (64 bytes; the T-table kernels start their records
-// themselves).
-struct alignas(16) RecState {
-  uint4 j0;   // pre-counter block J0 (gcm.cc.inc:316-338)
-  uint4 ek0;  // E_K(J0)
-  uint4 ya;   // exclusive GHASH of the AD: sum A_k H^(m-1-k)
-  uint32_t live, pad[3];
-};
-
-// Kernel block words (the 16 block bytes as 4 little-endian words) <-> the
-// reversed domain of gf128_ct.h (the big-endian integer of the bytes).
-__device__ __forceinline__ Gf128 to_gf(uint4 v) {
-  Gf128 g;
-  g.w[3] = bswap32(v.x);
-  g.w[2] = bswap32(v.y);
-  g.w[1] = bswap32(v.z);
-  g.w[0] = bswap32(v.w);
-  return g;
-}
-__device__ __forceinline__ uint4 from_gf(Gf128 g) {
-  return make_uint4(bswap32(g.w[3]), bswap32(g.w[2]), bswap32(g.w[1]), bswap32(g.w[0]));
-}
-__device__ __forceinline__ Gf128 gf_load(const uint32_t *p) {
-  const uint4 v = *reinterpret_cast<const uint4 *>(p);
-  Gf128 g;
-  g.w[0] = v.x;
-  g.w[1] = v.y;
-  g.w[2] = v.z;
-  g.w[3] = v.w;
-  return g;
-}
-__device__ __forceinline__ Gf128 gf_xor(Gf128 a, Gf128 b) {
-  for (int i = 0; i < 4; i++) a.w[i] ^= b.w[i];
-  return a;
-}
-
 // ---------------------------------------------------------------------------
 // One AES block with T0 alone, replicated once per LDS bank (one-record kernel):
 // entry x for lane l at tab[x * 32 + (l & 31)] (32 KiB), so every lookup of a
@@ -681,190 +425,6 @@ __device__ __forceinline__ uint4 aes_block_rep(uint4 in, const RoundKeys &rk, co
   };
   return make_uint4(last(s0, s1, s2, s3, rk.w[NR][0]), last(s1, s2, s3, s0, rk.w[NR][1]),
                     last(s2, s3, s0, s1, rk.w[NR][2]), last(s3, s0, s1, s2, rk.w[NR][3]));
-}
-
-// ---------------------------------------------------------------------------
-// Record start inside the bulk kernel (round 4: no prologue kernel, no
-// per-record state in HBM): the per-record constant work of
-// CRYPTO_gcm128_init_ctx / _aad (gcm.cc.inc:298-398), done by the record's
-// L lanes at the start of their unit.
-
-// Whether record `rec` is sealed/opened at all: a valid key index, a nonce
-// (e_aes.cc.inc:790), the length limits (gcm.cc.inc:368,409) and the
-// tls12/tls13 nonce check (tls_scan.hip, BatchDesc::valid).
-__device__ __forceinline__ bool record_live(const BatchDesc &b, uint64_t rec,
-                                            const RecordMeta &m) {
-  return (!b.key_index || b.key_index[rec] < b.num_keys) && b.nonce_len != 0 &&
-         m.len + m.xlen <= ((uint64_t(1) << 36) - 32) && m.ad_len <= (uint64_t(1) << 61) &&
-         (!b.valid || b.valid[rec]);
-}
-
-// Pre-counter block J0 (gcm.cc.inc:316-338): nonce || be32(1) for 96-bit
-// nonces, else GHASH(N || 0^s || [len(N)]_64), computed by every lane of the
-// record (constant-time VALU products by H).
-__device__ __forceinline__ uint4 record_j0(const BatchDesc &b, uint64_t rec,
-                                           const uint32_t (*hp)[4]) {
-  const uint8_t *nonce = b.nonces + rec * b.nonce_len;
-  if (b.nonce_len == 12) {
-    uint4 j0 = load_partial(nonce, 12);
-    j0.w = 0x01000000u;  // be32(1)
-    return j0;
-  }
-  const Gf128 h1 = gf_load(hp[1]);
-  Gf128 y = {{0, 0, 0, 0}};
-  for (uint64_t o = 0; o < b.nonce_len; o += 16)
-    y = gf_mul(gf_xor(y, to_gf(load_partial(nonce + o,
-                                            (uint32_t)min<uint64_t>(b.nonce_len - o, 16)))),
-               h1);
-  const uint64_t bits = b.nonce_len << 3;
-  y.w[0] ^= (uint32_t)bits;
-  y.w[1] ^= (uint32_t)(bits >> 32);
-  return from_gf(gf_mul(y, h1));
-}
-
-// Block k (16 bytes, zero-padded) of record rec's AD.
-__device__ __forceinline__ uint4 ad_block(const BatchDesc &b, uint64_t rec, const RecordMeta &m,
-                                          uint64_t k) {
-  const uint64_t o = 16 * k;
-  const uint32_t n = (uint32_t)min<uint64_t>(m.ad_len - o, 16);
-  return b.aadvecs ? ivec_load16(b.aadvecs, b.aadvec_start[rec], b.aadvec_start[rec + 1], o, n)
-                   : load_partial(b.ad + m.ad_off + o, n);
-}
-
-// Exclusive GHASH of the AD, Y_A = sum_k A_k H^(m-1-k) (m AD blocks), in
-// every lane of the record's L.  A one-block AD (TLS: 13 bytes) is its own
-// hash; longer ADs are shared out like the message: lane q folds blocks
-// k = q, q + L, ... by Horner in H^L, weighs its sum by H^(m-1-k_last) and
-// the L lanes XOR-reduce (row_xor).  `many`: some record of the wave has a
-// multi-block AD (wave-uniform, so the loop below is).
-template <int L>
-__device__ __forceinline__ uint4 record_ad_hash(const BatchDesc &b, uint64_t rec,
-                                                const RecordMeta &m, bool live, bool many,
-                                                const uint32_t (*hp)[4]) {
-  const uint64_t nad = live ? (m.ad_len + 15) / 16 : 0;
-  if (!many) return nad ? ad_block(b, rec, m, 0) : make_uint4(0, 0, 0, 0);
-  const uint32_t q = threadIdx.x & (L - 1);
-  const Gf128 hl = gf_load(hp[L]);
-  Gf128 acc = {{0, 0, 0, 0}};
-  uint64_t last = 0;
-  const int rounds = group_max<L>((int)((nad + L - 1) / L));
-  for (int i = 0; i < rounds; i++) {
-    const uint64_t k = q + (uint64_t)L * i;
-    if (k < nad) {
-      acc = gf_xor(i ? gf_mul(acc, hl) : acc, to_gf(ad_block(b, rec, m, k)));
-      last = k;
-    }
-  }
-  const uint32_t e = (uint32_t)(nad - 1 - last) & (L - 1);  // (lanes with no block: acc = 0)
-  Gf128 z = e ? gf_mul(acc, gf_load(hp[e])) : acc;
-#pragma unroll
-  for (int i = 0; i < 4; i++) z.w[i] = row_xor<L>(z.w[i]);
-  return from_gf(z);
-}
-
-// End of a record (all bulk kernels): combine the 16 lanes' GHASH
-// accumulators, form the tag, check it (open), write tag/status, and zero the
-// output of a failed record.  Lane algebra: lane q holds the
-// virtual elements v = q+1+16i of [Y_A, C_0, ..., C_{nb-1}], Horner'd at
-// stride 16, so its accumulator needs weight H^(15-p), p = (q - r + 1) mod 16
-// with r = (nb + 1) mod 16 (the lane holding the last element gets H^0).
-// Each lane multiplies its accumulator by H^(16-p) -- its weight times the
-// tag's first H -- and the 16 products are XOR-reduced:
-//   tag = ((Z*H) ^ len block) * H ^ E_K(J0)  (gcm.cc.inc:576-604).
-// Both products are constant-time VALU multiplications (gf128_ct.h) by the
-// key's prepared powers H^1..H^16 (key->hpow_ct), indexed by lane position
-// and record length only; no table is indexed by a secret.
-template <bool OPEN, int L>
-__device__ __forceinline__ void finish_record(uint4 acc, uint64_t nb, const RecordMeta &m,
-                                              uint4 ek0, const BatchDesc &b, uint64_t rec,
-                                              bool active, bool live, uint8_t *dst,
-                                              const uint32_t (*hp)[4]) {
-  const int q = threadIdx.x & (L - 1);
-  const int r = (int)((nb + 1) & (L - 1));
-  const int p = (q - r + 1) & (L - 1);
-  Gf128 z = gf_mul(to_gf(acc), gf_load(hp[L - p]));
-#pragma unroll
-  for (int i = 0; i < 4; i++) z.w[i] = row_xor<L>(z.w[i]);
-  // Length block be64(AD bits) || be64(message bits) in the reversed domain.
-  const uint64_t abits = m.ad_len << 3, cbits = (m.len + m.xlen) << 3;
-  z.w[0] ^= (uint32_t)cbits;
-  z.w[1] ^= (uint32_t)(cbits >> 32);
-  z.w[2] ^= (uint32_t)abits;
-  z.w[3] ^= (uint32_t)(abits >> 32);
-  z = gf_mul(z, gf_load(hp[1]));
-  const uint4 tag = xor4(from_gf(z), ek0);
-
-  uint8_t *tagp = batch_tag(b, rec);
-  int ok = live;
-  if (q == 0) {
-    if (OPEN && live) {
-      // CRYPTO_memcmp (e_aes.cc.inc:860-864) of the first tag_len bytes: the
-      // received tag by dword-aligned loads (one memory round trip; a byte
-      // loop cost one round trip per byte), compared as OR of XORs.
-      const uint4 t = load_partial(tagp, b.tag_len);
-      const uint4 mine = mask_block(tag, b.tag_len);
-      ok = ((t.x ^ mine.x) | (t.y ^ mine.y) | (t.z ^ mine.z) | (t.w ^ mine.w)) == 0;
-    }
-    if (active) {
-      if (!OPEN) store_partial(tagp, ok ? tag : make_uint4(0, 0, 0, 0), b.tag_len);
-      if (b.status) b.status[rec] = ok ? 1 : 0;
-    }
-  }
-  if (OPEN) ok = __shfl(ok, 0, L);  // (seal: ok = live, the same in every lane)
-  // Zero the output of a failed record (aead.cc.inc:132-139, 539-547; an
-  // iovec record's chunks, clear_iovec, :310-333).
-  if (active && !ok) {
-    if (b.iovecs) {
-      for (uint64_t c = b.iovec_start[rec]; c < b.iovec_start[rec + 1]; c++) {
-        const IovecDev v = b.iovecs[c];
-        for (uint64_t i = q; i < v.len; i += L) v.out[i] = 0;
-      }
-    } else {
-      for (uint64_t j = q; j * 16 < m.len; j += L) {
-        const uint32_t n = (uint32_t)min<uint64_t>(m.len - j * 16, 16);
-        store_partial(dst + j * 16, make_uint4(0, 0, 0, 0), n);
-      }
-    }
-    if (q == 0)
-      for (uint32_t i = 0; i < m.xlen; i++) batch_extra_out(b, rec)[i] = 0;
-  }
-}
-
-
-// ---------------------------------------------------------------------------
-// A unit's record inputs (one record per L-lane group), issued together at
-// the unit's start: layout, liveness, nonce, the first AD block and the
-// lane's first plaintext block.  (Loading them one unit ahead, before the
-// previous unit's record end, measured slower: the extra live registers
-// spilled, configG 687 vs 743 GiB/s; so did claiming the next unit two
-// iterations early, 729 vs 758, profiles/r04/.)
-struct UnitIn {
-  uint64_t rec;
-  RecordMeta m;
-  uint4 nonce;  // 12-byte nonces: J0 = nonce || be32(1) (words 0..2)
-  uint4 ad0;    // AD block 0, zero-padded
-  uint4 x0;     // the lane's first plaintext block (full blocks only)
-  bool active, live;
-};
-
-template <bool XT, bool IOV>
-__device__ __forceinline__ void unit_load(UnitIn &u, const BatchDesc &b, uint64_t i, int q,
-                                          uint64_t end) {
-  u.active = i < end;
-  u.rec = u.active ? rec_at(b, i) : 0;
-  u.m = {0, 0, 0, 0, 0};
-  u.live = false;
-  if (u.active) {
-    u.m = record_meta(b, u.rec);
-    u.live = record_live(b, u.rec, u.m);
-  }
-  if constexpr (!XT) u.m.xlen = 0;  // (the launcher picks XT iff extra_len != 0)
-  // (Left undefined when not loaded, as load_full's blocks.)
-  if (u.live && b.nonce_len == 12) u.nonce = load_partial(b.nonces + u.rec * 12, 12);
-  u.ad0 = make_uint4(0, 0, 0, 0);
-  if (u.live && u.m.ad_len) u.ad0 = ad_block(b, u.rec, u.m, 0);
-  if constexpr (!IOV)
-    if (u.live && (uint64_t)q < u.m.len / 16) u.x0 = load_blk_nt(b.in + u.m.off + 16 * q);
 }
 
 // ---------------------------------------------------------------------------
@@ -980,7 +540,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
           IovCur k;
           iov_at(k, b, ld_c, ld_cs);
           iov_seek(k, b, p, c_end);
-          const uint32_t n = (uint32_t)min<uint64_t>(m.len - p, 16);
+          const uint32_t n = (uint32_t)umin64(m.len - p, 16);
           if (n == 16 && p + 16 <= k.ce)
             v = load_blk_nt(k.in + (p - k.cs));
           else if (!iov_load2(b, k, p, n, c_end, v))  // a straddle, the last block
@@ -988,7 +548,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
           ld_c = k.c;
           ld_cs = k.cs;
           ld_ptr = k.in + (p - k.cs) + 16 * L;
-          ld_left = (int32_t)min<uint64_t>(k.ce - p, 1u << 30) - 16 * L;
+          ld_left = (int32_t)umin64(k.ce - p, 1u << 30) - 16 * L;
         }
       }
       return v;
@@ -1036,7 +596,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
         st_left -= 16 * L;
       } else if (j < nb) {
         const uint64_t p = (uint64_t)j * 16;
-        const uint32_t n = (uint32_t)min<uint64_t>(m.len - p, 16);
+        const uint32_t n = (uint32_t)umin64(m.len - p, 16);
         const uint64_t c_end = b.iovec_start[rec + 1];
         IovCur k;
         iov_at(k, b, st_c, st_cs);
@@ -1050,7 +610,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
         st_c = k.c;
         st_cs = k.cs;
         st_ptr = k.out + (p - k.cs) + 16 * L;
-        st_left = (int32_t)min<uint64_t>(k.ce - p, 1u << 30) - 16 * L;
+        st_left = (int32_t)umin64(k.ce - p, 1u << 30) - 16 * L;
       }
       if (j < nb) acc = xor4(h.g, OPEN ? x : y);
       return;
@@ -1058,7 +618,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     if (j < nfull) {
       store_blk_nt(dst + (uint64_t)j * 16, y);
     } else if (j < nb) {
-      const uint32_t n = (uint32_t)min<uint64_t>(m.len + m.xlen - (uint64_t)j * 16, 16);
+      const uint32_t n = (uint32_t)umin64(m.len + m.xlen - (uint64_t)j * 16, 16);
       if constexpr (XT) {
         y = crypt_partial_x(src, dst, m.len, xin, xout, (uint64_t)j * 16, ks, n, x);
       } else {
@@ -1091,61 +651,6 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   if (it < iters) step(it, x0);
   finish_record<OPEN, L>(acc, nb, m, quad_gather(ek0w), b, rec, active, live, dst,
                          key->hpow_ct);
-}
-
-// Byte table of H^16 from the key's nibble tables (power 4): entry (e, p) =
-// T[2p][e >> 4] ^ T[2p+1][e & 15] (key_setup.cc layout), at kLdsG8 + e*256 +
-// p*16.  Thread tid writes entries tid + i*kThreads; since kThreads is a
-// multiple of 256 its p and (e & 15) are fixed and e >> 4 steps by
-// kThreads/256, so all of its global loads are issued before the first LDS
-// write (one memory latency per key change instead of one per entry).
-template <int THREADS>
-__device__ __forceinline__ void build_g8(uint8_t *smem, const uint4 *__restrict__ t16, int tid) {
-  static_assert(THREADS % 256 == 0 && 4096 % THREADS == 0, "table build split");
-  constexpr int kPer = 4096 / THREADS;
-  const uint32_t p = (uint32_t)tid & 15u, lo = ((uint32_t)tid >> 4) & 15u;
-  const uint32_t hi = (uint32_t)tid >> 8;
-  const uint4 b = t16[(2 * p + 1) * 16 + lo];
-  uint4 a[kPer];
-#pragma unroll
-  for (int i = 0; i < kPer; i++) a[i] = t16[(2 * p) * 16 + hi + (uint32_t)i * (THREADS / 256)];
-#pragma unroll
-  for (int i = 0; i < kPer; i++)
-    reinterpret_cast<uint4 *>(smem + kLdsG8)[tid + i * THREADS] = xor4(a[i], b);
-}
-
-// Byte table of H^L (L < 16: the short-record kernels, whose GHASH stride is
-// L) computed in the kernel from the key's prepared H^L (hpow_ct[L]): the
-// 128 basis products (bit `bit` of byte p) x H^L by 128 threads with the
-// constant-time VALU product, then entry (e, p) = XOR of the basis elements
-// of p for the bits of e (e and p are table indices, public).
-template <int THREADS>
-__device__ __forceinline__ void build_gpow(uint8_t *smem, const uint32_t *hl, int tid) {
-  static_assert(THREADS >= 128 && 4096 % THREADS == 0, "table build split");
-  uint4 *basis = reinterpret_cast<uint4 *>(smem + kLdsBasis);
-  if (tid < 128) {
-    const uint32_t p = (uint32_t)tid >> 3, bit = (uint32_t)tid & 7u;
-    uint32_t w[4] = {0, 0, 0, 0};
-    w[p >> 2] = 1u << (8 * (p & 3) + bit);
-    basis[tid] = from_gf(gf_mul(to_gf(make_uint4(w[0], w[1], w[2], w[3])), gf_load(hl)));
-  }
-  __syncthreads();
-  const uint32_t p = (uint32_t)tid & 15u;
-  uint4 bv[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) bv[k] = basis[p * 8 + k];
-#pragma unroll
-  for (int i = 0; i < 4096 / THREADS; i++) {
-    const uint32_t e = ((uint32_t)tid >> 4) + (uint32_t)i * (THREADS / 16);
-    uint4 v = make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint32_t msk = 0u - ((e >> k) & 1u);
-      v = make_uint4(v.x ^ (bv[k].x & msk), v.y ^ (bv[k].y & msk), v.z ^ (bv[k].z & msk),
-                     v.w ^ (bv[k].w & msk));
-    }
-    reinterpret_cast<uint4 *>(smem + kLdsG8)[tid + i * THREADS] = v;
-  }
 }
 
 // The AES tables of the bulk kernels, replicated per bank: entry idx, slot t,
@@ -1193,7 +698,7 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
   if constexpr (L == 16)
     build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab16), tid);
   else
-    build_gpow<kThreads>(smem, keys[0].hpow_ct[L], tid);
+    build_gpow<kThreads, kLdsBasis>(smem, keys[0].hpow_ct[L], tid);
   __syncthreads();
   RoundKeys rk;
 #pragma unroll
@@ -1500,440 +1005,6 @@ bool one_record_batch(const BatchDesc &b) {
   return len <= 16u * kOneMaxBlocks;
 }
 
-// ---------------------------------------------------------------------------
-// Table-free engine (opt-in, BSSL_AMD_GCM_MODE=bs16): AES on
-// the VALU only, bitsliced 16 blocks per lane (bs16_aes.h), sharing the
-// T-table kernel's lane algebra, GHASH byte table and finish_record.
-typedef uint32_t v32u __attribute__((ext_vector_type(32)));
-
-// 0 or 0xffffffff: bit `k` of w (v_bfe_i32 / s_bfe_i32).
-__device__ __forceinline__ uint32_t bit_mask(uint32_t w, int k) {
-  return (uint32_t)(((int32_t)(w << (31 - k))) >> 31);
-}
-
-// 32x32 bit transpose (the swap-move network of bs_transpose32): the 16- and
-// 8-bit stages are byte permutations (one v_perm_b32 per output word), the
-// 4/2/1-bit stages one shift plus one v_bitop3 bit-select per output word.
-template <int S>
-__device__ __forceinline__ void tr_stage(uint32_t m[32]) {
-  constexpr uint32_t kLo = S == 4 ? 0x0f0f0f0fu : S == 2 ? 0x33333333u : 0x55555555u;
-#pragma unroll
-  for (int k = 0; k < 32; k++) {
-    if (k & S) continue;
-    const uint32_t a = m[k], b = m[k + S];
-    if constexpr (S == 16) {
-      m[k] = __builtin_amdgcn_perm(b, a, 0x05040100u);
-      m[k + S] = __builtin_amdgcn_perm(b, a, 0x07060302u);
-    } else if constexpr (S == 8) {
-      m[k] = __builtin_amdgcn_perm(b, a, 0x06020400u);
-      m[k + S] = __builtin_amdgcn_perm(b, a, 0x07030501u);
-    } else {
-      m[k] = (a & kLo) | ((b << S) & ~kLo);
-      m[k + S] = (b & ~kLo) | ((a >> S) & kLo);
-    }
-  }
-}
-
-__device__ __forceinline__ void transpose32_fast(uint32_t m[32]) {
-  tr_stage<16>(m);
-  tr_stage<8>(m);
-  tr_stage<4>(m);
-  tr_stage<2>(m);
-  tr_stage<1>(m);
-}
-
-// x * H^16 with the lane-rotated byte table (all 16 lookups in flight).
-__device__ __forceinline__ uint4 g8_mul(uint4 x, bool rs1, bool rs2, uint32_t rbs,
-                                        const uint32_t (&P)[4], const uint8_t *smem) {
-  Gh8 h;
-  g8_rotate(h, x, rs1, rs2, rbs);
-  const uint4 t0 = xor4_3(g8_load<0>(h, P, smem), g8_load<1>(h, P, smem), g8_load<2>(h, P, smem));
-  const uint4 t1 = xor4_3(g8_load<3>(h, P, smem), g8_load<4>(h, P, smem), g8_load<5>(h, P, smem));
-  const uint4 t2 = xor4_3(g8_load<6>(h, P, smem), g8_load<7>(h, P, smem), g8_load<8>(h, P, smem));
-  const uint4 t3 = xor4_3(g8_load<9>(h, P, smem), g8_load<10>(h, P, smem), g8_load<11>(h, P, smem));
-  const uint4 t4 = xor4_3(g8_load<12>(h, P, smem), g8_load<13>(h, P, smem), g8_load<14>(h, P, smem));
-  return xor4(xor4_3(t0, t1, t2), xor4_3(t3, t4, g8_load<15>(h, P, smem)));
-}
-
-// bs16 layout: register (r, h, b) holds bit b of state row r for column h in
-// its low 16 bits (block n in bit n) and for column h + 2 in its high 16 bits
-// (block n in bit 16 + n) -- 64 VGPRs of state, and every SubBytes /
-// MixColumns operation works on 32 bit-slots.  ShiftRows maps row r of column
-// c to column c - r: for the register pairs that is a renaming plus a swap of
-// the two halves (rot16) of 4 of the 8 (row, pair) groups per round.
-
-// Keystream words of pair h: word n (< 16) = column h of block n, word
-// 16 + n = column h + 2 of block n.
-__device__ __forceinline__ v32u bs16_words(const uint32_t (&p)[4][2][8], int h) {
-  uint32_t o[32];
-#pragma unroll
-  for (int r = 0; r < 4; r++)
-#pragma unroll
-    for (int b = 0; b < 8; b++) o[8 * r + b] = p[r][h][b];
-  transpose32_fast(o);
-  v32u v;
-#pragma unroll
-  for (int n = 0; n < 32; n++) v[n] = o[n];
-  return v;
-}
-
-// The (up to) 4 records of a wave with the bs16 engine.  Lane q owns blocks
-// j = 256*c + 16*n + q (n = 0..15) of chunk c -- the T-table role's lane
-// algebra, so GHASH (multiplier H^16, the LDS byte table) and finish_record
-// are shared.  Every record shape the T-table kernel takes: any length
-// (a chunk's slots past the record are computed and dropped), any alignment,
-// extra bytes (XT) and iovec records walked in place (IOV, the T-table
-// kernel's cursors at the same 256-byte lane stride).  J0, E_K(J0) (by the
-// bitsliced prologue) and the AD hash come from RecState.
-template <int NR, bool OPEN, bool XT, bool IOV>
-__device__ __forceinline__ void process_records_bs16(const uint32_t *__restrict__ rkp,
-                                                     const BatchDesc &b,
-                                                     const RecState *__restrict__ st,
-                                                     const UnitIn &in, const uint8_t *smem,
-                                                     const GcmKeyDev *key) {
-  // Register budget: the rounds need ~100 VGPRs, so little else may stay live
-  // across them -- the per-lane GHASH constants, J0 and the record metadata
-  // are re-derived (laundered through empty asm so they are not hoisted)
-  // after the rounds and at the end of the record.
-  constexpr int L = 16;
-  const uint64_t rec = in.rec;
-  const bool active = in.active;
-  const bool live = active && st[rec].live;
-  const RecordMeta m0 = in.m;
-  const uint32_t nb = live ? (uint32_t)((m0.len + m0.xlen + 15) / 16) : 0u;
-  const uint32_t nfull = live && !IOV ? (uint32_t)(m0.len / 16) : 0u;
-  uint4 acc = ((threadIdx.x & 15) == 15 && live) ? st[rec].ya : make_uint4(0, 0, 0, 0);
-  const int nchunks = wave_max((int)((nb + 255) / 256));
-  // iovec cursors (as process_records): chunk index + stream start; between
-  // chunk boundaries only the running pointers move.
-  uint64_t ld_c = 0, ld_cs = 0, st_c = 0, st_cs = 0;
-  const uint8_t *ld_ptr = nullptr;
-  uint8_t *st_ptr = nullptr;
-  int32_t ld_left = -1, st_left = -1;
-  if constexpr (IOV) {
-    if (live) ld_c = st_c = b.iovec_start[rec];
-  }
-#pragma unroll 1
-  for (int c = 0; c < nchunks; c++) {
-    uint32_t p[4][2][8];
-    {
-      // Round 0.  Pair 0 = columns 0 and 2 of J0 ^ rk0 (per-lane constants:
-      // 0 / 0xffff per half); pair 1 = column 1 (constant, low half) and the
-      // counter words of column 3 (high half), both out of one transpose:
-      // t[n] = column 1, t[16 + n] = word 3 of block n.
-      uint64_t rr = rec;
-      asm volatile("" : "+v"(rr));
-      const uint4 j0 = active ? st[rr].j0 : make_uint4(0, 0, 0, 0);
-      uint32_t rk0[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++) rk0[i] = (uint32_t)__builtin_amdgcn_readfirstlane(rkp[i]);
-      const uint32_t w0 = j0.x ^ rk0[0], w1 = j0.y ^ rk0[1], w2 = j0.z ^ rk0[2];
-#pragma unroll
-      for (int k = 0; k < 32; k++)
-        p[k / 8][0][k % 8] = (bit_mask(w0, k) & 0xffffu) | (bit_mask(w2, k) & 0xffff0000u);
-      const uint32_t jc = 256u * (uint32_t)c + (threadIdx.x & 15u);
-      const uint32_t cb = bswap32(j0.w) + 1u + jc;  // inc32: mod 2^32
-      uint32_t t[32];
-#pragma unroll
-      for (int n = 0; n < 16; n++) {
-        t[n] = w1;
-        t[16 + n] = bswap32(cb + 16u * (uint32_t)n) ^ rk0[3];
-      }
-      transpose32_fast(t);
-#pragma unroll
-      for (int k = 0; k < 32; k++) p[k / 8][1][k % 8] = t[k];
-    }
-    bs16_cipher<NR>(p, rkp);
-    uint32_t q = threadIdx.x & 15u;
-    asm volatile("" : "+v"(q));
-    const uint32_t jc = 256u * (uint32_t)c + q;
-    const bool rs1 = (q >> 2) & 1, rs2 = (q >> 3) & 1;
-    const uint32_t rbs = q & 3u;
-    uint32_t P[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int i = 0; i < 4; i++) v |= (((4u * k + i + q) & 15u) << 4) << (8 * i);
-      P[k] = v;
-    }
-    uint64_t rr = rec;
-    asm volatile("" : "+v"(rr));
-    RecordMeta m = m0;
-    asm volatile("" : "+v"(m.off), "+v"(m.len));
-    const uint8_t *src = b.in + m.off;
-    uint8_t *dst = b.out + m.off;
-    const uint8_t *xin = XT ? batch_extra_in(b, rr) : nullptr;
-    uint8_t *xout = XT ? batch_extra_out(b, rr) : nullptr;
-    v32u KA = bs16_words(p, 0), KB = bs16_words(p, 1);
-    const int nv = (int)min(16u, jc < nb ? (nb - jc + 15u) / 16u : 0u);
-    // Pass 1 (memory): out = in ^ keystream; the ciphertext (the output when
-    // sealing, the input when opening) replaces the keystream in KA/KB.
-#pragma unroll 1
-    for (int n = 0; n < 16; n++) {
-      const uint32_t j = jc + 16u * (uint32_t)n;
-      const uint4 ks = make_uint4(KA[n], KB[n], KA[16 + n], KB[16 + n]);
-      uint4 x = make_uint4(0, 0, 0, 0), y;
-      if constexpr (IOV) {
-        const uint64_t pb = (uint64_t)j * 16;
-        const uint32_t nbytes = j < nb ? (uint32_t)min<uint64_t>(m.len - pb, 16) : 0u;
-        const uint64_t c_end = b.iovec_start[rr + 1];
-        if (nbytes) {
-          if (ld_left >= 16 && nbytes == 16) {
-            x = load_blk_nt(ld_ptr);
-          } else {
-            IovCur k;
-            iov_at(k, b, ld_c, ld_cs);
-            iov_seek(k, b, pb, c_end);
-            if (nbytes == 16 && pb + 16 <= k.ce)
-              x = load_blk_nt(k.in + (pb - k.cs));
-            else if (!iov_load2(b, k, pb, nbytes, c_end, x))
-              x = iov_gather(b, k, pb, nbytes, c_end);
-            ld_c = k.c;
-            ld_cs = k.cs;
-            ld_ptr = k.in + (pb - k.cs);
-            ld_left = (int32_t)min<uint64_t>(k.ce - pb, 1u << 30);
-          }
-          ld_ptr += 16 * L;
-          ld_left -= 16 * L;
-          y = mask_block(xor4(x, ks), nbytes);
-          if (st_left >= 16 && nbytes == 16) {
-            store_blk_nt(st_ptr, y);
-          } else {
-            IovCur k;
-            iov_at(k, b, st_c, st_cs);
-            iov_seek(k, b, pb, c_end);
-            if (nbytes == 16 && pb + 16 <= k.ce)
-              store_blk_nt(k.out + (pb - k.cs), y);
-            else if (!iov_store2(b, k, pb, y, nbytes, c_end))
-              iov_scatter(b, k, pb, y, nbytes, c_end);
-            st_c = k.c;
-            st_cs = k.cs;
-            st_ptr = k.out + (pb - k.cs);
-            st_left = (int32_t)min<uint64_t>(k.ce - pb, 1u << 30);
-          }
-          st_ptr += 16 * L;
-          st_left -= 16 * L;
-        } else {
-          y = make_uint4(0, 0, 0, 0);
-        }
-      } else {
-        if (j < nfull) {
-          x = load_blk_nt(src + (uint64_t)j * 16);
-          y = xor4(x, ks);
-          store_blk_nt(dst + (uint64_t)j * 16, y);
-        } else if (j < nb) {
-          const uint32_t nbytes = (uint32_t)min<uint64_t>(m.len + m.xlen - (uint64_t)j * 16, 16);
-          if constexpr (XT) {
-            y = crypt_partial_x(src, dst, m.len, xin, xout, (uint64_t)j * 16, ks, nbytes, x);
-          } else {
-            x = load_partial(src + (uint64_t)j * 16, nbytes);
-            y = mask_block(xor4(x, ks), nbytes);
-            store_partial(dst + (uint64_t)j * 16, y, nbytes);
-          }
-        } else {
-          y = make_uint4(0, 0, 0, 0);
-        }
-      }
-      const uint4 cbk = OPEN ? x : y;
-      KA[n] = cbk.x;
-      KB[n] = cbk.y;
-      KA[16 + n] = cbk.z;
-      KB[16 + n] = cbk.w;
-    }
-    // Pass 2 (LDS): acc = acc * H^16 ^ C over the lane's valid blocks.
-#pragma unroll 1
-    for (int n = 0; n < 16; n++) {
-      const uint4 hm = g8_mul(acc, rs1, rs2, rbs, P, smem);
-      if (n < nv) acc = xor4(hm, make_uint4(KA[n], KB[n], KA[16 + n], KB[16 + n]));
-    }
-  }
-  uint64_t rr = rec;
-  asm volatile("" : "+v"(rr));
-  finish_record<OPEN, 16>(acc, nb, m0, st[rr].ek0, b, rr, active, live, b.out + m0.off,
-                          key->hpow_ct);
-}
-
-// Record inputs of a bs16 unit: the layout only (J0, E_K(J0) and the AD hash
-// are in RecState).
-template <bool XT>
-__device__ __forceinline__ void unit_meta(UnitIn &u, const BatchDesc &b, uint64_t i) {
-  u.active = i < b.num_records;
-  u.rec = u.active ? rec_at(b, i) : 0;
-  u.m = {0, 0, 0, 0, 0};
-  if (u.active) u.m = record_meta(b, u.rec);
-  if constexpr (!XT) u.m.xlen = 0;
-  u.live = u.active;
-}
-
-// Table-free prologue (bs16 mode): J0 and the AD hash as gcm_prologue
-// (constant-time VALU products), E_K(J0) by the bitsliced engine with each
-// lane's 16 block slots holding 16 consecutive records -- one bs16_cipher per
-// 16 records.  Records of several keys (keysets) take the per-lane-key cipher,
-// once per distinct key among the lane's 16 records.
-template <int NR>
-__global__ __launch_bounds__(256) void gcm_prologue_bs16(const GcmKeyDev *__restrict__ keys,
-                                                         BatchDesc b, RecState *__restrict__ st) {
-  const uint64_t r0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
-  uint4 j0[16];
-  uint32_t kidx[16];
-  bool lv[16];
-#pragma unroll
-  for (int n = 0; n < 16; n++) {
-    const uint64_t rec = r0 + n;
-    lv[n] = false;
-    kidx[n] = 0;
-    j0[n] = make_uint4(0, 0, 0, 0);
-    if (rec < b.num_records) {
-      const RecordMeta m = record_meta(b, rec);
-      lv[n] = record_live(b, rec, m);
-      kidx[n] = lv[n] && b.key_index ? b.key_index[rec] : 0u;
-      if (lv[n]) {
-        const GcmKeyDev *kp = keys + kidx[n];
-        j0[n] = record_j0(b, rec, kp->hpow_ct);
-        // Exclusive GHASH of the AD, sum A_k H^(m-1-k) (the lanes' element 0).
-        const Gf128 h1 = gf_load(kp->hpow_ct[1]);
-        Gf128 ya = {{0, 0, 0, 0}};
-        const uint64_t nad = (m.ad_len + 15) / 16;
-        for (uint64_t k = 0; k < nad; k++)
-          ya = k ? gf_xor(gf_mul(ya, h1), to_gf(ad_block(b, rec, m, k))) : to_gf(ad_block(b, rec, m, k));
-        RecState s;
-        s.live = 1;
-        s.pad[0] = s.pad[1] = s.pad[2] = 0;
-        s.j0 = j0[n];
-        s.ya = from_gf(ya);
-        s.ek0 = make_uint4(0, 0, 0, 0);
-        st[rec] = s;
-      } else {
-        RecState s;
-        s.live = 0;
-        s.pad[0] = s.pad[1] = s.pad[2] = 0;
-        s.j0 = s.ek0 = s.ya = make_uint4(0, 0, 0, 0);
-        st[rec] = s;
-      }
-    }
-  }
-  // E_K(J0) of the live slots, one cipher per distinct key of the lane.
-  uint32_t todo = 0;
-#pragma unroll
-  for (int n = 0; n < 16; n++) todo |= (uint32_t)lv[n] << n;
-  while (__ballot(todo != 0)) {
-    const uint32_t k = todo ? kidx[__builtin_ctz(todo)] : 0u;
-    uint32_t mine = 0;
-#pragma unroll
-    for (int n = 0; n < 16; n++) mine |= (uint32_t)((todo >> n) & 1u && kidx[n] == k) << n;
-    const uint32_t *rkp = &keys[k].rk_plain[0][0];
-    uint32_t p[4][2][8];
-    uint32_t t0[32], t1[32];
-#pragma unroll
-    for (int n = 0; n < 16; n++) {
-      t0[n] = j0[n].x ^ rkp[0];
-      t0[16 + n] = j0[n].z ^ rkp[2];
-      t1[n] = j0[n].y ^ rkp[1];
-      t1[16 + n] = j0[n].w ^ rkp[3];
-    }
-    transpose32_fast(t0);
-    transpose32_fast(t1);
-#pragma unroll
-    for (int q = 0; q < 32; q++) {
-      p[q / 8][0][q % 8] = t0[q];
-      p[q / 8][1][q % 8] = t1[q];
-    }
-    bs16_cipher<NR, false>(p, rkp);
-    const v32u KA = bs16_words(p, 0), KB = bs16_words(p, 1);
-#pragma unroll
-    for (int n = 0; n < 16; n++)
-      if ((mine >> n) & 1u) st[r0 + n].ek0 = make_uint4(KA[n], KB[n], KA[16 + n], KB[16 + n]);
-    todo &= ~mine;
-  }
-}
-
-// Table-free bulk kernels (BSSL_AMD_GCM_MODE=bs16): no AES table anywhere --
-// the LDS holds only the GHASH byte table of H^16.  One-key batches: 16 waves
-// per CU at 128 VGPRs, 4-record units from one grid-wide counter, every unit
-// on the bs16 engine whatever its records' shape.
-template <int NR, bool OPEN, bool XT, bool IOV>
-__global__ __launch_bounds__(1024) void gcm_bs16_kernel(const GcmKeyDev *__restrict__ keys,
-                                                        BatchDesc b,
-                                                        const RecState *__restrict__ st,
-                                                        uint32_t *__restrict__ units) {
-  constexpr int kThreads = 1024;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kG8Bytes];
-  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
-  build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab16), tid);
-  __syncthreads();
-  const uint32_t *rkp = &keys[0].rk_plain[0][0];
-  const uint64_t n = b.num_records;
-  for (;;) {
-    uint32_t u = 0;
-    if (lane == 0) u = atomicAdd(units, 1u);
-    const uint64_t first = (uint64_t)__builtin_amdgcn_readlane(u, 0) * kRecPerWave;
-    if (first >= n) break;
-    UnitIn in;
-    unit_meta<XT>(in, b, first + g);
-    process_records_bs16<NR, OPEN, XT, IOV>(rkp, b, st, in, smem, keys);
-  }
-}
-
-// Keyset batches in bs16 mode: gcm_keyset_kernel's tiles and passes, each
-// pass on the bs16 engine with the pass key's round keys.
-template <int NR, bool OPEN, bool XT>
-__global__ __launch_bounds__(1024) void gcm_keyset_bs16_kernel(const GcmKeyDev *__restrict__ keys,
-                                                               BatchDesc b,
-                                                               const RecState *__restrict__ st) {
-  constexpr int kThreads = 1024;
-  constexpr int kRecPerTile = 16 * kRecPerWave;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kG8Bytes + 64 * 16 + 16];
-  uint32_t *s_pass_key = reinterpret_cast<uint32_t *>(smem + kG8Bytes);
-  uint64_t *s_pass_mask = reinterpret_cast<uint64_t *>(smem + kG8Bytes + 64 * 4);
-  int *s_npass = reinterpret_cast<int *>(smem + kG8Bytes + 64 * 16);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  uint32_t loaded = 0xffffffffu;
-  const uint64_t n = b.num_records;
-  for (uint64_t base = (uint64_t)blockIdx.x * kRecPerTile; base < n;
-       base += (uint64_t)gridDim.x * kRecPerTile) {
-    __syncthreads();
-    if (wave == 0) {
-      const uint64_t i = base + lane;
-      uint32_t k = (lane < kRecPerTile && i < n) ? b.key_index[rec_at(b, i)] : 0xffffffffu;
-      if (k != 0xffffffffu && k >= b.num_keys) k = 0;  // (dead: RecState.live = 0)
-      uint64_t pending = __ballot(k != 0xffffffffu);
-      int np = 0;
-      while (pending) {
-        const uint32_t kk = __shfl(k, __builtin_ctzll(pending), 64);
-        const uint64_t mask = __ballot(k == kk) & pending;
-        if (lane == 0) {
-          s_pass_key[np] = kk;
-          s_pass_mask[np] = mask;
-        }
-        pending &= ~mask;
-        np++;
-      }
-      if (lane == 0) *s_npass = np;
-    }
-    __syncthreads();
-    const int npass = *s_npass;
-    for (int pi = 0; pi < npass; pi++) {
-      const uint32_t k = __builtin_amdgcn_readfirstlane(s_pass_key[pi]);
-      const uint64_t mask = s_pass_mask[pi];
-      if (k != loaded) {
-        __syncthreads();
-        build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[k].htab16), tid);
-        __syncthreads();
-        loaded = k;
-      }
-      const int t = wave * kRecPerWave + g;
-      const bool active = (mask >> t) & 1;
-      UnitIn in;
-      unit_meta<XT>(in, b, active ? base + t : n);
-      process_records_bs16<NR, OPEN, XT, false>(&keys[k].rk_plain[0][0], b, st, in, smem,
-                                                keys + k);
-    }
-  }
-}
-
-
-
 // Lanes per record of the one-key kernel: 4 (stride H^4, 16 records per
 // wave) for uniform batches of records up to 4 KiB -- config G (1350 bytes)
 // 760-766 GiB/s at 8 lanes, 889-893 at 4, same box (profiles/r04/s19/): a
@@ -1961,18 +1032,9 @@ bool runs_in_lines(const BatchDesc &b) {
            b.record_stride) & 63) == 0;
 }
 
-// Engine for a batch: 0 = the T-table kernels (default), 1 = the table-free
-// bs16 engine (BSSL_AMD_GCM_MODE=bs16) for every batch: one key or keysets,
-// any record shape, extra bytes, iovecs, single records.
-int gcm_mode(const BatchDesc &b) {
-  (void)b;
-  const char *e = getenv("BSSL_AMD_GCM_MODE");
-  return e && !strcmp(e, "bs16") ? 1 : 0;
-}
-
 template <int NR, bool OPEN>
 int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const KernelEvents *ev) {
-  if (one_record_batch(b) && gcm_mode(b) == 0) {
+  if (one_record_batch(b)) {
     if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
     if (b.record_len <= 16 * 256)
       hipLaunchKernelGGL((gcm_one_kernel<NR, OPEN, 256>), dim3(1), dim3(256), 0, s, keys, b);
@@ -1985,65 +1047,31 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
   }
   const int num_cus = device_cu_count();
   if (!num_cus) return 1;
-  const int mode = gcm_mode(b);
-  // The unit counter of the one-key kernels (64 bytes, zeroed) and, for the
-  // bs16 engine only, its per-record state (RecState, written by its
-  // prologue; the T-table kernel starts its records itself).
-  const uint64_t nst = mode == 1 ? b.num_records : 0;
-  RecState *st = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void **>(&st), (nst + 1) * sizeof(RecState), s) !=
-      hipSuccess)
+  // The unit counters of the one-key kernels (64 bytes each, zeroed).
+  uint32_t *units = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void **>(&units), 64, s) != hipSuccess) return 2;
+  if (hipMemsetAsync(units, 0, 64, s) != hipSuccess) {
+    hipFreeAsync(units, s);
     return 2;
-  uint32_t *units = reinterpret_cast<uint32_t *>(st + nst);
-  if (hipMemsetAsync(units, 0, sizeof(RecState), s) != hipSuccess) {
-    hipFreeAsync(st, s);
-    return 2;
-  }
-  if (mode == 1) {  // 16 records per thread
-    const uint64_t pblocks = (b.num_records + 16 * 256 - 1) / (16 * 256);
-    hipLaunchKernelGGL((gcm_prologue_bs16<NR>), dim3((unsigned)pblocks), dim3(256), 0, s, keys, b,
-                       st);
   }
   BatchDesc bo = b;  // with the processing order of a ragged batch
   uint32_t *order = nullptr;
   if (wants_length_order(b)) {
     if (hipMallocAsync(reinterpret_cast<void **>(&order), (b.num_records + 128) * sizeof(uint32_t),
                        s) != hipSuccess) {
-      hipFreeAsync(st, s);
+      hipFreeAsync(units, s);
       return 2;
     }
     const int orc = build_length_order(b.lengths, b.num_records, order, order + b.num_records, s);
     if (orc) {
       hipFreeAsync(order, s);
-      hipFreeAsync(st, s);
+      hipFreeAsync(units, s);
       return orc;
     }
     bo.order = order;
   }
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
-  const RecState *cst = st;
-  if (mode == 1) {
-    const uint64_t units_needed = (b.num_records + 4 * 16 - 1) / (4 * 16);
-    const unsigned grid = (unsigned)(units_needed < (uint64_t)num_cus ? units_needed
-                                                                       : (uint64_t)num_cus);
-    if (b.key_index) {
-      if (b.extra_len)
-        hipLaunchKernelGGL((gcm_keyset_bs16_kernel<NR, OPEN, true>), dim3(grid), dim3(1024), 0, s,
-                           keys, bo, cst);
-      else
-        hipLaunchKernelGGL((gcm_keyset_bs16_kernel<NR, OPEN, false>), dim3(grid), dim3(1024), 0, s,
-                           keys, bo, cst);
-    } else if (b.iovecs) {
-      hipLaunchKernelGGL((gcm_bs16_kernel<NR, OPEN, false, true>), dim3(grid), dim3(1024), 0, s,
-                         keys, bo, cst, units);
-    } else if (b.extra_len) {
-      hipLaunchKernelGGL((gcm_bs16_kernel<NR, OPEN, true, false>), dim3(grid), dim3(1024), 0, s,
-                         keys, bo, cst, units);
-    } else {
-      hipLaunchKernelGGL((gcm_bs16_kernel<NR, OPEN, false, false>), dim3(grid), dim3(1024), 0, s,
-                         keys, bo, cst, units);
-    }
-  } else {
+  {
     const uint64_t tiles = (b.num_records + kWaves * kRecPerWave - 1) / (kWaves * kRecPerWave);
     const unsigned grid = (unsigned)(tiles < (uint64_t)num_cus ? tiles : (uint64_t)num_cus);
     if (b.key_index) {
@@ -2097,16 +1125,38 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
   int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
   if (order) hipFreeAsync(order, s);
-  hipFreeAsync(st, s);
+  hipFreeAsync(units, s);
   return rc;
 }
 
 }  // namespace
 
+namespace {
+std::atomic<int> g_gcm_engine{-1};
+}  // namespace
+
+int gcm_engine() {
+  int e = g_gcm_engine.load(std::memory_order_relaxed);
+  if (e >= 0) return e;
+  const char *v = getenv("BSSL_AMD_GCM_MODE");
+  e = v && (!strcmp(v, "bs") || !strcmp(v, "bs16")) ? kGcmEngineBitsliced : kGcmEngineTable;
+  int expect = -1;
+  g_gcm_engine.compare_exchange_strong(expect, e, std::memory_order_relaxed);
+  return g_gcm_engine.load(std::memory_order_relaxed);
+}
+
+int set_gcm_engine(int engine) {
+  if (engine != kGcmEngineTable && engine != kGcmEngineBitsliced) return -1;
+  const int prev = gcm_engine();
+  g_gcm_engine.store(engine, std::memory_order_relaxed);
+  return prev;
+}
+
 int launch_gcm(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, void *stream,
                const KernelEvents *ev) {
   if (b.num_records == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (gcm_engine() == kGcmEngineBitsliced) return launch_gcm_bs(keys, b, open, nr, s, ev);
   switch (nr) {
     case 10: return open ? launch_nr<10, true>(keys, b, s, ev) : launch_nr<10, false>(keys, b, s, ev);
     case 12: return open ? launch_nr<12, true>(keys, b, s, ev) : launch_nr<12, false>(keys, b, s, ev);

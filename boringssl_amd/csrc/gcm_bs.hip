@@ -1,0 +1,798 @@
+// gcm_bs.hip -- the table-free AES-GCM engine (gfx950): AES bitsliced on the
+// VALU with no lookup table of any kind, GHASH by the conflict-free LDS byte
+// table of H^L, the record start and end in the bulk kernel.  DESIGN.md §4.2b.
+//
+// Replaces, like gcm.hip, aead_aes_gcm_sealv_impl / _openv_detached_impl
+// (crypto/fipsmodule/cipher/e_aes.cc.inc:779-867) ->
+// CRYPTO_gcm128_{init_ctx,aad,encrypt,decrypt,tag} (crypto/fipsmodule/aes/
+// gcm.cc.inc:298-604); its AES is the reference's own constant-time choice,
+// a bitsliced cipher (aes_nohw_sub_bytes, crypto/fipsmodule/aes/
+// aes_nohw.cc.inc:508; its batched CTR32, :1171-1214), here on 16 blocks per
+// lane with two state columns per register (bs16_aes.h).
+//
+// * Work split.  L lanes per record (64 / L records per wave: one "unit"),
+//   lane q encrypts the counter blocks j = 16*L*c + L*n + q of chunk c in its
+//   16 bit-slots n, so a wave instruction moves 16*L-byte runs per record,
+//   and folds its ciphertext blocks into a GHASH accumulator by Horner's rule
+//   at stride L (multiplier H^L, the LDS byte table; gcm_common.h).  Units are
+//   claimed from a grid-wide counter.
+// * Chunk.  Round 0 of the 16 counter blocks (J0 words XOR the round key, the
+//   counter word through one 32x32 bit transpose), rounds 1..NR with the
+//   key's precomputed AddRoundKey masks (GcmKeyDev::bsmask, scalar loads), two
+//   output transposes into 16 keystream blocks, then one pass over the slots
+//   in which the plaintext loads run ahead of the XOR/store and each slot's
+//   GHASH multiply (acc * H^L, whose input is known before the block arrives)
+//   is issued before waiting for the block.
+// * Record start.  J0 and the AD hash by the record's lanes (gcm_common.h).
+//   E_K(J0) by a bitsliced batch per 1,024 records (64 lanes x 16 slots): the
+//   wave that claims a group's producer unit computes the whole group's E_K(J0)
+//   into a per-launch scratch and raises the group's flag; the record end reads
+//   its value (normally long ready).  The producer unit of group g + 1 is the
+//   middle unit of group g, so a group's values are ready half a group ahead.
+// * Record end.  finish_record (gcm_common.h): the lanes' weights H^(L-p), the
+//   L-lane XOR, length block, tag, check and zero-fill.
+#include <hip/hip_runtime.h>
+
+#include "bs16_aes.h"
+#include "gcm_common.h"
+
+namespace bssl_amd {
+namespace {
+#include "gcm_bs_io.inc"
+}  // namespace
+}  // namespace bssl_amd
+
+namespace bssl_amd {
+namespace {
+
+constexpr int kBsThreads = 1024;          // 16 waves per CU at 128 VGPRs
+constexpr uint32_t kBsGroupRecs = 1024;   // records per E_K(J0) batch
+constexpr uint32_t kBsLdsBasis = kG8Bytes;  // build_gpow scratch (2 KiB)
+constexpr uint32_t kBsLdsState = kBsLdsBasis + 128 * 16;  // parked unit state (bs_unit)
+constexpr uint32_t kBsLdsBytes = kBsLdsState + 15 * 4 * kBsThreads;
+// Launch control words (zeroed by the launcher): unit counter, then one
+// ready flag per E_K(J0) group.
+constexpr int kCtlFlags = 16;
+
+typedef uint32_t v32u __attribute__((ext_vector_type(32)));
+
+// 0 or 0xffffffff: bit `k` of w.
+__device__ __forceinline__ uint32_t bit_mask(uint32_t w, int k) {
+  return (uint32_t)(((int32_t)(w << (31 - k))) >> 31);
+}
+
+// 32x32 bit transpose (bit n of m[k] <-> bit k of m[n]): the 16- and 8-bit
+// stages are byte permutations (one v_perm_b32 per output word), the 4/2/1-bit
+// stages one shift plus one bit-select per output word.
+template <int S>
+__device__ __forceinline__ void tr_stage(uint32_t m[32]) {
+  constexpr uint32_t kLo = S == 4 ? 0x0f0f0f0fu : S == 2 ? 0x33333333u : 0x55555555u;
+#pragma unroll
+  for (int k = 0; k < 32; k++) {
+    if (k & S) continue;
+    const uint32_t a = m[k], b = m[k + S];
+    if constexpr (S == 16) {
+      m[k] = __builtin_amdgcn_perm(b, a, 0x05040100u);
+      m[k + S] = __builtin_amdgcn_perm(b, a, 0x07060302u);
+    } else if constexpr (S == 8) {
+      m[k] = __builtin_amdgcn_perm(b, a, 0x06020400u);
+      m[k + S] = __builtin_amdgcn_perm(b, a, 0x07030501u);
+    } else {
+      m[k] = (a & kLo) | ((b << S) & ~kLo);
+      m[k + S] = (b & ~kLo) | ((a >> S) & kLo);
+    }
+  }
+}
+
+__device__ __forceinline__ void transpose32(uint32_t m[32]) {
+  tr_stage<16>(m);
+  tr_stage<8>(m);
+  tr_stage<4>(m);
+  tr_stage<2>(m);
+  tr_stage<1>(m);
+}
+
+// Keystream words of register pair h: word n (< 16) = column h of slot n,
+// word 16 + n = column h + 2 of slot n.
+__device__ __forceinline__ v32u bs16_words(const uint32_t (&p)[4][2][8], int h) {
+  uint32_t o[32];
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+#pragma unroll
+    for (int b = 0; b < 8; b++) o[8 * r + b] = p[r][h][b];
+  transpose32(o);
+  v32u v;
+#pragma unroll
+  for (int n = 0; n < 32; n++) v[n] = o[n];
+  return v;
+}
+
+// The 16 blocks w[n] ^ rk0 as bitsliced state (round 0 of 16 arbitrary
+// blocks: the E_K(J0) batches).
+__device__ __forceinline__ void bs16_load_blocks(uint32_t (&p)[4][2][8], const uint4 (&w)[16],
+                                                 const uint32_t rk0[4]) {
+  uint32_t t0[32], t1[32];
+#pragma unroll
+  for (int n = 0; n < 16; n++) {
+    t0[n] = w[n].x ^ rk0[0];
+    t0[16 + n] = w[n].z ^ rk0[2];
+    t1[n] = w[n].y ^ rk0[1];
+    t1[16 + n] = w[n].w ^ rk0[3];
+  }
+  transpose32(t0);
+  transpose32(t1);
+#pragma unroll
+  for (int k = 0; k < 32; k++) {
+    p[k / 8][0][k % 8] = t0[k];
+    p[k / 8][1][k % 8] = t1[k];
+  }
+}
+
+// acc * H^L with the lane-rotated byte table: 16 lookups in four groups of
+// four (sched barriers keep at most four lookups' 16 registers in flight
+// beside the 64 keystream words of the slot loop).
+__device__ __forceinline__ uint4 g8_mul(uint4 x, bool rs1, bool rs2, uint32_t rbs,
+                                        const uint32_t (&P)[4], const uint8_t *smem) {
+  Gh8 h;
+  g8_rotate(h, x, rs1, rs2, rbs);
+  uint4 a = xor4(xor4_3(g8_load<0>(h, P, smem), g8_load<1>(h, P, smem), g8_load<2>(h, P, smem)),
+                 g8_load<3>(h, P, smem));
+  __builtin_amdgcn_sched_barrier(0);
+  a = xor4(xor4_3(a, g8_load<4>(h, P, smem), g8_load<5>(h, P, smem)),
+           xor4_3(g8_load<6>(h, P, smem), g8_load<7>(h, P, smem), make_uint4(0, 0, 0, 0)));
+  __builtin_amdgcn_sched_barrier(0);
+  a = xor4(xor4_3(a, g8_load<8>(h, P, smem), g8_load<9>(h, P, smem)),
+           xor4(g8_load<10>(h, P, smem), g8_load<11>(h, P, smem)));
+  __builtin_amdgcn_sched_barrier(0);
+  a = xor4(xor4_3(a, g8_load<12>(h, P, smem), g8_load<13>(h, P, smem)),
+           xor4(g8_load<14>(h, P, smem), g8_load<15>(h, P, smem)));
+  return a;
+}
+
+// ---------------------------------------------------------------------------
+// E_K(J0) of records [i0, i0 + 1024) in processing order (one group): lane l
+// takes positions i0 + 16 l + s in its slots s.  KS: records carry their own
+// keys (keysets) -- one cipher per distinct key among a lane's slots, with
+// that key's masks per lane; one-key batches take one cipher with the key's
+// wave-uniform masks.  Results to ek0[i]; then the group's flag is raised
+// (release, agent scope: the consumers read with coherent loads).
+template <int NR, bool KS>
+__device__ __forceinline__ void produce_ek0(const GcmKeyDev *__restrict__ keys, const BatchDesc &b,
+                                         uint64_t i0, uint64_t end, uint4 *__restrict__ ek0,
+                                         uint32_t *flag) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t base = i0 + 16u * (uint64_t)lane;
+  uint4 j0[16];
+  uint32_t kidx[16];
+  uint32_t todo = 0;
+#pragma unroll
+  for (int s = 0; s < 16; s++) {
+    const uint64_t i = base + s;
+    j0[s] = make_uint4(0, 0, 0, 0);
+    kidx[s] = 0;
+    if (i < end) {
+      const uint64_t rec = rec_at(b, i);
+      const RecordMeta m = record_meta(b, rec);
+      if (record_live(b, rec, m)) {
+        kidx[s] = KS ? b.key_index[rec] : 0u;
+        if (b.nonce_len == 12) {
+          const uint4 nn = load_partial(b.nonces + rec * 12, 12);
+          j0[s] = make_uint4(nn.x, nn.y, nn.z, 0x01000000u);
+        } else {
+          j0[s] = record_j0(b, rec, keys[kidx[s]].hpow_ct);
+        }
+        todo |= 1u << s;
+      }
+    }
+  }
+  while (__ballot(todo != 0)) {
+    uint32_t mine = todo;
+    uint32_t p[4][2][8];
+    if constexpr (KS) {
+      const uint32_t k = todo ? kidx[__builtin_ctz(todo)] : 0u;
+      mine = 0;
+#pragma unroll
+      for (int s = 0; s < 16; s++) mine |= (uint32_t)(((todo >> s) & 1u) && kidx[s] == k) << s;
+      const uint32_t *rkp = &keys[k].rk_plain[0][0];
+      bs16_load_blocks(p, j0, rkp);
+      bs16_cipher<NR, false>(p, rkp);
+    } else {
+      uint32_t rk0[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) rk0[c] = keys[0].rk_plain[0][c];
+      bs16_load_blocks(p, j0, rk0);
+      bs16_cipher_tab<NR>(p, &keys[0].bsmask[0][0]);
+    }
+    const v32u KA = bs16_words(p, 0), KB = bs16_words(p, 1);
+#pragma unroll
+    for (int s = 0; s < 16; s++)
+      if ((mine >> s) & 1u) ek0[base + s] = make_uint4(KA[s], KB[s], KA[16 + s], KB[16 + s]);
+    todo &= ~mine;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  if (lane == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// E_K(J0) of processing position i, once its group's flag is up (coherent
+// loads: the values were written by another wave, maybe on another XCD, and
+// this CU's caches may hold the scratch lines of an earlier launch).
+__device__ __forceinline__ uint4 consume_ek0(const uint4 *ek0, uint32_t *flag, uint64_t i,
+                                             bool active) {
+  if ((threadIdx.x & 63) == 0)
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+      __builtin_amdgcn_s_sleep(4);
+  if (!active) return make_uint4(0, 0, 0, 0);
+  uint32_t *p = reinterpret_cast<uint32_t *>(const_cast<uint4 *>(ek0 + i));
+  return make_uint4(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                    __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                    __hip_atomic_load(p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                    __hip_atomic_load(p + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// ---------------------------------------------------------------------------
+// Per-lane unit state parked in LDS while the rounds hold the registers
+// (word k of thread t at kBsLdsState + (k * kBsThreads + t) * 4: consecutive
+// lanes on consecutive banks).  The rounds need ~105 VGPRs of the 128; these
+// values would otherwise stay live across them and spill.
+enum : int {
+  kSw0, kSw1, kSw2,  // J0 words 0..2 XOR round key 0 (round 0 of every counter block)
+  kScb,              // counter word of the lane's slot 0 of chunk 0: bswap(J0.w) + 1 + q
+  kSnb, kSnfull,     // the record's blocks and full blocks (this lane's record)
+  kSoff, kSoffHi,    // the record's offset in in / out
+  kSacc0, kSacc1, kSacc2, kSacc3,
+  kSflags,           // bit 0 active, bit 1 live
+  kSrec, kSrecHi,
+  kSwords
+};
+
+// The 64 / L records of one unit, L lanes each: the lane's record is at
+// processing position i (`active`: the group has a record in this unit).
+template <int NR, bool OPEN, bool XT, bool IOV, int L>
+__device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const BatchDesc &b,
+                                        uint64_t i, bool active, uint8_t *smem,
+                                        const uint4 *ek0, uint32_t *flag) {
+  static_assert(L == 16 || L == 8 || L == 4, "lanes per record");
+  static_assert(!(IOV && XT), "iovec records carry no extra bytes");
+  const int q = threadIdx.x & (L - 1);
+  // (Inline-asm LDS accesses: the compiler must neither forward the stored
+  // values in registers across the rounds nor turn them into flat accesses.)
+  const uint32_t la =
+      (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t *)smem) +
+      kBsLdsState + 4u * threadIdx.x;
+  auto put = [&](int k, uint32_t v) {
+    asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(la), "v"(v), "i"(k * 4 * kBsThreads));
+  };
+  auto get = [&](int k) -> uint32_t {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(v)
+                 : "v"(la), "i"(k * 4 * kBsThreads));
+    return v;
+  };
+  int nchunks;
+  // IOV: chunk cursors (as gcm.hip process_records: chunk index + stream
+  // start; between chunk boundaries only the running pointers move).
+  uint64_t ld_c = 0, ld_cs = 0, st_c = 0, st_cs = 0;
+  const uint8_t *ld_ptr = nullptr;
+  uint8_t *st_ptr = nullptr;
+  int32_t ld_left = -1, st_left = -1;
+  {
+    const uint64_t rec = active ? rec_at(b, i) : 0;
+    RecordMeta m = {0, 0, 0, 0, 0};
+    if (active) m = record_meta(b, rec);
+    if constexpr (!XT) m.xlen = 0;
+    const bool live = active && record_live(b, rec, m);
+    // J0 (gcm.cc.inc:316-338) and the AD hash (:347-398), in the record's lanes.
+    uint4 j0 = make_uint4(0, 0, 0, 0);
+    if (live) {
+      if (b.nonce_len == 12) {
+        const uint4 nn = load_partial(b.nonces + rec * 12, 12);
+        j0 = make_uint4(nn.x, nn.y, nn.z, 0x01000000u);
+      } else {
+        j0 = record_j0(b, rec, key->hpow_ct);
+      }
+    }
+    const bool many_ad = __ballot(live && m.ad_len > 16) != 0;
+    uint4 acc = record_ad_hash<L>(b, rec, m, live, many_ad, key->hpow_ct);
+    if (q != L - 1 || !live) acc = make_uint4(0, 0, 0, 0);
+    // (< 2^32: the GCM length limit holds for a live record)
+    const uint32_t nb = live ? (uint32_t)((m.len + m.xlen + 15) / 16) : 0u;
+    const uint32_t nfull = live && !IOV ? (uint32_t)(m.len / 16) : 0u;
+    nchunks = wave_max((int)((nb + 16 * L - 1) / (16 * L)));
+    put(kSw0, j0.x ^ key->rk_plain[0][0]);
+    put(kSw1, j0.y ^ key->rk_plain[0][1]);
+    put(kSw2, j0.z ^ key->rk_plain[0][2]);
+    put(kScb, bswap32(j0.w) + 1u + (uint32_t)q);
+    put(kSnb, nb);
+    put(kSnfull, nfull);
+    put(kSoff, (uint32_t)m.off);
+    put(kSoffHi, (uint32_t)(m.off >> 32));
+    put(kSacc0, acc.x);
+    put(kSacc1, acc.y);
+    put(kSacc2, acc.z);
+    put(kSacc3, acc.w);
+    put(kSflags, (active ? 1u : 0u) | (live ? 2u : 0u));
+    put(kSrec, (uint32_t)rec);
+    put(kSrecHi, (uint32_t)(rec >> 32));
+    if constexpr (IOV) {
+      if (live) ld_c = st_c = b.iovec_start[rec];
+    }
+  }
+  const uint32_t *__restrict__ mk = &key->bsmask[0][0];
+#pragma unroll 1
+  for (int c = 0; c < nchunks; c++) {
+    uint32_t p[4][2][8];
+    {
+      // Round 0.  Pair 0 = columns 0 and 2 of J0 ^ rk0 (the same in every
+      // slot: 0 / 0xffff per half); pair 1 = column 1 (low half, constant)
+      // and the counter words of column 3 (high half), out of one transpose:
+      // t[n] = column 1, t[16 + n] = word 3 of slot n.
+      const uint32_t w0 = get(kSw0), w1 = get(kSw1), w2 = get(kSw2);
+      const uint32_t rk3 = key->rk_plain[0][3];
+#pragma unroll
+      for (int k = 0; k < 32; k++)
+        p[k / 8][0][k % 8] = (bit_mask(w0, k) & 0xffffu) | (bit_mask(w2, k) & 0xffff0000u);
+      const uint32_t cb = get(kScb) + (uint32_t)(16 * L) * (uint32_t)c;  // inc32: mod 2^32
+      uint32_t t[32];
+#pragma unroll
+      for (int n = 0; n < 16; n++) {
+        t[n] = w1;
+        t[16 + n] = bswap32(cb + (uint32_t)L * (uint32_t)n) ^ rk3;
+      }
+      transpose32(t);
+#pragma unroll
+      for (int k = 0; k < 32; k++) p[k / 8][1][k % 8] = t[k];
+    }
+    bs16_cipher_tab<NR>(p, mk);
+    // Pass 1 (memory): out = in ^ keystream for the lane's full blocks, the
+    // plaintext loads running kAhead slots ahead (slot n of the lane is 16*L*n
+    // bytes past slot 0: immediate offsets); the hashed block (the ciphertext:
+    // the output when sealing, the input when opening) replaces the keystream
+    // in KA/KB.  Pass 2 (LDS): acc = acc * H^L ^ C over the lane's blocks.
+    // Both passes are unrolled, so every index is static and each slot's
+    // registers die with it.  A lane's other block (the record's partial last
+    // block and extra bytes, j in [nfull, nb): its last element, at most one
+    // per lane) parks its keystream in kt and is sealed and hashed last.
+    // (Scheduling barriers: the scheduler would otherwise interleave the two
+    // transposes and hoist the plaintext loads above them, which needs more
+    // than the 128 registers.)
+    uint32_t KA[32], KB[32];
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      const v32u ka = bs16_words(p, 0);
+#pragma unroll
+      for (int k = 0; k < 32; k++) {
+        KA[k] = ka[k];
+        asm volatile("" : "+v"(KA[k]));
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      const v32u kb = bs16_words(p, 1);
+#pragma unroll
+      for (int k = 0; k < 32; k++) {
+        KB[k] = kb[k];
+        asm volatile("" : "+v"(KB[k]));
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t jc = (uint32_t)(16 * L) * (uint32_t)c + (uint32_t)q;
+    const uint32_t nb = get(kSnb), nfull = get(kSnfull);
+    const uint64_t off = (uint64_t)get(kSoff) | ((uint64_t)get(kSoffHi) << 32);
+    const uint8_t *src = b.in + off;
+    uint8_t *dst = b.out + off;
+    const uint8_t *s0 = src + (uint64_t)jc * 16;
+    uint8_t *d0 = dst + (uint64_t)jc * 16;
+    // The output pass (not iovec records): one inline-asm statement
+    // (gcm_bs_io.inc) -- plaintext loads D slots ahead, each slot's GHASH
+    // multiply issued while its block is in flight, stores and the hash fold
+    // predicated on the lane's full blocks (a prefix of its slots: nv), fixed
+    // scratch registers.  (The compiler's schedule of the same work hoisted
+    // every load and spilled.)  A lane's other block in this chunk (the
+    // record's partial last block or extra bytes: slot tl) gets its keystream
+    // kept in kt and is sealed after the pass.
+    if constexpr (!IOV) {
+      const int gq = threadIdx.x & 15;
+      uint32_t P[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) v |= (((4u * k + e + gq) & 15u) << 4) << (8 * e);
+        P[k] = v;
+      }
+      const int nv = jc < nfull ? (int)min((nfull - jc + L - 1) / L, 16u) : 0;
+      const int tl = (nv < 16 && jc + (uint32_t)L * (uint32_t)nv < nb) ? nv : -1;
+      uint32_t accv[4] = {get(kSacc0), get(kSacc1), get(kSacc2), get(kSacc3)};
+      uint32_t kt[4] = {0, 0, 0, 0};
+      // (rs1 / rs2 of g8_rotate as lane masks: bits 2 and 3 of the lane's
+      // index in its 16-lane row)
+      constexpr uint64_t kM1 = 0xf0f0f0f0f0f0f0f0ull, kM2 = 0xff00ff00ff00ff00ull;
+      const uint64_t a0 = reinterpret_cast<uint64_t>(s0), a1 = reinterpret_cast<uint64_t>(d0);
+      const uint32_t rb = (uint32_t)gq & 3u;
+      const bool any_tail = __ballot(tl >= 0) != 0;
+#define BS_IO(SUFFIX) bs_chunk_io_##SUFFIX(KA, KB, accv, kt, a0, a1, kM1, kM2, rb, nv, tl, P)
+      if constexpr (L == 16) {
+        if (any_tail) { if constexpr (OPEN) BS_IO(open_tail_L16); else BS_IO(seal_tail_L16); }
+        else { if constexpr (OPEN) BS_IO(open_L16); else BS_IO(seal_L16); }
+      } else if constexpr (L == 8) {
+        if (any_tail) { if constexpr (OPEN) BS_IO(open_tail_L8); else BS_IO(seal_tail_L8); }
+        else { if constexpr (OPEN) BS_IO(open_L8); else BS_IO(seal_L8); }
+      } else {
+        if (any_tail) { if constexpr (OPEN) BS_IO(open_tail_L4); else BS_IO(seal_tail_L4); }
+        else { if constexpr (OPEN) BS_IO(open_L4); else BS_IO(seal_L4); }
+      }
+#undef BS_IO
+      if (tl >= 0) {
+        const uint32_t jt = jc + (uint32_t)L * (uint32_t)tl;
+        const uint64_t rec = (uint64_t)get(kSrec) | ((uint64_t)get(kSrecHi) << 32);
+        const RecordMeta m = record_meta(b, rec);
+        const uint32_t xlen = XT ? m.xlen : 0u;
+        const uint4 hm = g8_mul(make_uint4(accv[0], accv[1], accv[2], accv[3]), (gq >> 2) & 1,
+                                (gq >> 3) & 1, rb, P, smem);
+        const uint32_t nbytes = (uint32_t)umin64(m.len + xlen - (uint64_t)jt * 16, 16);
+        const uint4 ktv = make_uint4(kt[0], kt[1], kt[2], kt[3]);
+        uint4 x, y;
+        if constexpr (XT) {
+          y = crypt_partial_x(src, dst, m.len, batch_extra_in(b, rec), batch_extra_out(b, rec),
+                              (uint64_t)jt * 16, ktv, nbytes, x);
+        } else {
+          x = load_partial(src + (uint64_t)jt * 16, nbytes);
+          y = mask_block(xor4(x, ktv), nbytes);
+          store_partial(dst + (uint64_t)jt * 16, y, nbytes);
+        }
+        const uint4 c = OPEN ? x : y;
+        accv[0] = hm.x ^ c.x;
+        accv[1] = hm.y ^ c.y;
+        accv[2] = hm.z ^ c.z;
+        accv[3] = hm.w ^ c.w;
+      }
+      put(kSacc0, accv[0]);
+      put(kSacc1, accv[1]);
+      put(kSacc2, accv[2]);
+      put(kSacc3, accv[3]);
+      continue;
+    }
+    constexpr int kAhead = 4;
+    uint4 kt = make_uint4(0, 0, 0, 0);
+    uint32_t jt = 0xffffffffu;
+    int nv;  // the lane's full blocks of this chunk (hashed in pass 2)
+    // The loads are unconditional (a slot past the lane's full blocks reads
+    // the record's first block again, a valid address), so the plaintext
+    // registers are always defined and no control flow splits the pass; only
+    // the stores are predicated.
+    if constexpr (IOV) {
+      nv = 0;
+#pragma unroll
+      for (int n = 0; n < 16; n++) {
+        const uint32_t j = jc + (uint32_t)L * (uint32_t)n;
+        const uint4 ks = make_uint4(KA[n], KB[n], KA[16 + n], KB[16 + n]);
+        uint4 cv = make_uint4(0, 0, 0, 0);
+        if (j < nb) {
+          const uint64_t rec = (uint64_t)get(kSrec) | ((uint64_t)get(kSrecHi) << 32);
+          const uint64_t pb = (uint64_t)j * 16;
+          const uint64_t c_end = b.iovec_start[rec + 1];
+          const uint64_t rlen = b.lengths ? b.lengths[rec] : b.record_len;
+          const uint32_t nbytes = (uint32_t)umin64(rlen - pb, 16);
+          uint4 x;
+          if (ld_left >= 16 && nbytes == 16) {
+            x = load_blk_nt(ld_ptr);
+          } else {
+            IovCur k;
+            iov_at(k, b, ld_c, ld_cs);
+            iov_seek(k, b, pb, c_end);
+            if (nbytes == 16 && pb + 16 <= k.ce)
+              x = load_blk_nt(k.in + (pb - k.cs));
+            else if (!iov_load2(b, k, pb, nbytes, c_end, x))
+              x = iov_gather(b, k, pb, nbytes, c_end);
+            ld_c = k.c;
+            ld_cs = k.cs;
+            ld_ptr = k.in + (pb - k.cs);
+            ld_left = (int32_t)umin64(k.ce - pb, 1u << 30);
+          }
+          ld_ptr += 16 * L;
+          ld_left -= 16 * L;
+          const uint4 y = mask_block(xor4(x, ks), nbytes);
+          if (st_left >= 16 && nbytes == 16) {
+            store_blk_nt(st_ptr, y);
+          } else {
+            IovCur k;
+            iov_at(k, b, st_c, st_cs);
+            iov_seek(k, b, pb, c_end);
+            if (nbytes == 16 && pb + 16 <= k.ce)
+              store_blk_nt(k.out + (pb - k.cs), y);
+            else if (!iov_store2(b, k, pb, y, nbytes, c_end))
+              iov_scatter(b, k, pb, y, nbytes, c_end);
+            st_c = k.c;
+            st_cs = k.cs;
+            st_ptr = k.out + (pb - k.cs);
+            st_left = (int32_t)umin64(k.ce - pb, 1u << 30);
+          }
+          st_ptr += 16 * L;
+          st_left -= 16 * L;
+          cv = OPEN ? x : y;
+          nv = n + 1;
+        }
+        KA[n] = cv.x;
+        KB[n] = cv.y;
+        KA[16 + n] = cv.z;
+        KB[16 + n] = cv.w;
+      }
+    } else {
+      const uint8_t *s1 = jc < nfull ? s0 : src;  // (any valid address for the
+      const uint32_t lim = nfull > jc ? (nfull - jc + L - 1) / L : 0u;  // slots past nfull)
+      nv = (int)min(lim, 16u);
+      const int tl = jc < nb ? (int)((nb - 1 - jc) / L) : -1;  // the lane's last slot
+      uint4 xs[16];
+#pragma unroll
+      for (int n = 0; n < kAhead; n++) xs[n] = load_blk_nt(s1 + (n < nv ? 16 * L * n : 0));
+#pragma unroll
+      for (int n = 0; n < 16; n++) {
+        if (n + kAhead < 16)
+          xs[n + kAhead] = load_blk_nt(s1 + (n + kAhead < nv ? 16 * L * (n + kAhead) : 0));
+        const uint4 x = xs[n];
+        const uint4 y = make_uint4(x.x ^ KA[n], x.y ^ KB[n], x.z ^ KA[16 + n], x.w ^ KB[16 + n]);
+        if (n < nv) store_blk_nt(d0 + 16 * L * n, y);
+        // The partial / extra-byte block (slot tl when it is not full).
+        if (n == tl && n >= nv) {
+          kt = make_uint4(KA[n], KB[n], KA[16 + n], KB[16 + n]);
+          jt = jc + (uint32_t)L * (uint32_t)n;
+        }
+        const uint4 cv = OPEN ? x : y;
+        KA[n] = cv.x;
+        KB[n] = cv.y;
+        KA[16 + n] = cv.z;
+        KB[16 + n] = cv.w;
+      }
+    }
+    // (Pass 2 starts here: the pins keep the compiler from hoisting its
+    // lookups into pass 1, whose registers they would need.)
+#pragma unroll
+    for (int k = 0; k < 32; k++) asm volatile("" : "+v"(KA[k]), "+v"(KB[k]));
+    const int gq = threadIdx.x & 15;  // (GHASH lane constants, gcm_common.h Gh8)
+    const bool rs1 = (gq >> 2) & 1, rs2 = (gq >> 3) & 1;
+    const uint32_t rbs = (uint32_t)gq & 3u;
+    uint32_t P[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int e = 0; e < 4; e++) v |= (((4u * k + e + gq) & 15u) << 4) << (8 * e);
+      P[k] = v;
+    }
+    uint4 acc = make_uint4(get(kSacc0), get(kSacc1), get(kSacc2), get(kSacc3));
+#pragma unroll
+    for (int n = 0; n < 16; n++) {
+      const uint4 hm = g8_mul(acc, rs1, rs2, rbs, P, smem);
+      if (n < nv) acc = xor4(hm, make_uint4(KA[n], KB[n], KA[16 + n], KB[16 + n]));
+    }
+    if constexpr (!IOV) {
+      // The lane's partial / extra-byte block of this chunk, if any.
+      if (jt != 0xffffffffu) {
+        const uint64_t rec = (uint64_t)get(kSrec) | ((uint64_t)get(kSrecHi) << 32);
+        const RecordMeta m = record_meta(b, rec);
+        const uint32_t xlen = XT ? m.xlen : 0u;
+        const uint4 hm = g8_mul(acc, rs1, rs2, rbs, P, smem);
+        const uint32_t nbytes = (uint32_t)umin64(m.len + xlen - (uint64_t)jt * 16, 16);
+        uint4 x, y;
+        if constexpr (XT) {
+          y = crypt_partial_x(src, dst, m.len, batch_extra_in(b, rec), batch_extra_out(b, rec),
+                              (uint64_t)jt * 16, kt, nbytes, x);
+        } else {
+          x = load_partial(src + (uint64_t)jt * 16, nbytes);
+          y = mask_block(xor4(x, kt), nbytes);
+          store_partial(dst + (uint64_t)jt * 16, y, nbytes);
+        }
+        acc = xor4(hm, OPEN ? x : y);
+      }
+    }
+    put(kSacc0, acc.x);
+    put(kSacc1, acc.y);
+    put(kSacc2, acc.z);
+    put(kSacc3, acc.w);
+  }
+  // Record end.
+  const uint32_t fl = get(kSflags);
+  const bool act = fl & 1u, live = (fl >> 1) & 1u;
+  const uint64_t rec = (uint64_t)get(kSrec) | ((uint64_t)get(kSrecHi) << 32);
+  RecordMeta m = {0, 0, 0, 0, 0};
+  if (act) m = record_meta(b, rec);
+  if constexpr (!XT) m.xlen = 0;
+  const uint32_t nb = get(kSnb);
+  const uint4 acc = make_uint4(get(kSacc0), get(kSacc1), get(kSacc2), get(kSacc3));
+  const uint4 e0 = consume_ek0(ek0, flag, i, act);
+  finish_record<OPEN, L>(acc, nb, m, e0, b, rec, act, live, b.out + m.off, key->hpow_ct);
+}
+
+// One-key bulk kernel: one workgroup of 16 waves per CU; each wave takes the
+// next unit of 64 / L records from the grid-wide counter (ctl[0]).  Before
+// its unit, the claimant of a group's producer unit computes that group's
+// E_K(J0) (produce_ek0).
+template <int NR, bool OPEN, bool XT, bool IOV, int L>
+__global__ __launch_bounds__(kBsThreads) void gcm_bs_kernel(const GcmKeyDev *__restrict__ keys,
+                                                             BatchDesc b, uint32_t *__restrict__ ctl,
+                                                             uint4 *__restrict__ ek0) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kBsLdsBytes];
+  const int tid = threadIdx.x, lane = tid & 63;
+  if constexpr (L == 16)
+    build_g8<kBsThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab16), tid);
+  else
+    build_gpow<kBsThreads, kBsLdsBasis>(smem, keys[0].hpow_ct[L], tid);
+  __syncthreads();
+  constexpr uint32_t kRec = 64 / L;
+  constexpr uint32_t kGroupUnits = kBsGroupRecs / kRec;
+  const uint64_t n = b.num_records;
+  uint32_t *flags = ctl + kCtlFlags;
+  for (;;) {
+    uint32_t u = 0;
+    if (lane == 0) u = atomicAdd(ctl, 1u);
+    u = __builtin_amdgcn_readfirstlane(u);
+    const uint64_t first = (uint64_t)u * kRec;
+    if (first >= n) break;
+    // Producer units: 0 for group 0, the middle unit of group g for g + 1.
+    const uint32_t g = u / kGroupUnits;
+    uint32_t pg = 0xffffffffu;
+    if (u == 0) pg = 0;
+    if (u % kGroupUnits == kGroupUnits / 2 && (uint64_t)(g + 1) * kBsGroupRecs < n) pg = g + 1;
+    if (pg != 0xffffffffu)
+      produce_ek0<NR, false>(keys, b, (uint64_t)pg * kBsGroupRecs, n, ek0, flags + pg);
+    const uint64_t i = first + (uint64_t)(lane / L);
+    bs_unit<NR, OPEN, XT, IOV, L>(keys, b, i, i < n, smem, ek0, flags + g);
+  }
+}
+
+// Keyset batches (key_index per record): records in tiles of 16 units; a
+// tile whose records use several keys runs one pass per distinct key (the
+// LDS byte table is per key).  E_K(J0) groups as in the one-key kernel, per
+// record key (produce_ek0<KS = true>), claimed by the tile that holds the
+// group's producer position.
+template <int NR, bool OPEN, bool XT>
+__global__ __launch_bounds__(kBsThreads) void gcm_bs_keyset_kernel(
+    const GcmKeyDev *__restrict__ keys, BatchDesc b, uint32_t *__restrict__ ctl,
+    uint4 *__restrict__ ek0) {
+  constexpr int kRecPerTile = 16 * 4;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kBsLdsBytes + 64 * 16 + 16];
+  uint32_t *s_pass_key = reinterpret_cast<uint32_t *>(smem + kBsLdsBytes);
+  uint64_t *s_pass_mask = reinterpret_cast<uint64_t *>(smem + kBsLdsBytes + 64 * 4);
+  int *s_npass = reinterpret_cast<int *>(smem + kBsLdsBytes + 64 * 12);
+  uint64_t *s_base = reinterpret_cast<uint64_t *>(smem + kBsLdsBytes + 64 * 12 + 8);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g4 = lane >> 4;
+  uint32_t *flags = ctl + kCtlFlags;
+  uint32_t loaded = 0xffffffffu;
+  const uint64_t n = b.num_records;
+  for (;;) {
+    // Tiles from the grid-wide counter (ctl[0]); wave 0 plans the tile.
+    __syncthreads();
+    if (wave == 0) {
+      uint32_t t = 0;
+      if (lane == 0) t = atomicAdd(ctl, 1u);
+      t = __builtin_amdgcn_readfirstlane(t);
+      const uint64_t base = (uint64_t)t * kRecPerTile;
+      const uint64_t i = base + lane;
+      uint32_t k = (base < n && i < n) ? b.key_index[rec_at(b, i)] : 0xffffffffu;
+      if (k != 0xffffffffu && k >= b.num_keys) k = 0;  // (not live: zeroed output)
+      uint64_t pending = __ballot(k != 0xffffffffu);
+      int np = 0;
+      while (pending) {
+        const uint32_t kk = __shfl(k, __builtin_ctzll(pending), 64);
+        const uint64_t mask = __ballot(k == kk) & pending;
+        if (lane == 0) {
+          s_pass_key[np] = kk;
+          s_pass_mask[np] = mask;
+        }
+        pending &= ~mask;
+        np++;
+      }
+      if (lane == 0) {
+        *s_npass = base < n ? np : -1;
+        *s_base = base;
+      }
+      // Group producer: tile 0 for group 0, the middle tile of group g for g + 1.
+      if (base < n) {
+        constexpr uint32_t kGroupTiles = kBsGroupRecs / kRecPerTile;
+        const uint32_t g = t / kGroupTiles;
+        uint32_t pg = 0xffffffffu;
+        if (t == 0) pg = 0;
+        if (t % kGroupTiles == kGroupTiles / 2 && (uint64_t)(g + 1) * kBsGroupRecs < n) pg = g + 1;
+        if (pg != 0xffffffffu)
+          produce_ek0<NR, true>(keys, b, (uint64_t)pg * kBsGroupRecs, n, ek0, flags + pg);
+      }
+    }
+    __syncthreads();
+    const int npass = *s_npass;
+    if (npass < 0) break;
+    const uint64_t base = *s_base;
+    for (int pi = 0; pi < npass; pi++) {
+      const uint32_t k = __builtin_amdgcn_readfirstlane(s_pass_key[pi]);
+      const uint64_t mask = s_pass_mask[pi];
+      if (k != loaded) {
+        __syncthreads();
+        build_g8<kBsThreads>(smem, reinterpret_cast<const uint4 *>(keys[k].htab16), tid);
+        __syncthreads();
+        loaded = k;
+      }
+      const int t = wave * 4 + g4;
+      const bool act = (mask >> t) & 1;
+      bs_unit<NR, OPEN, XT, false, 16>(keys + k, b, base + t, act, smem, ek0,
+                                       flags + (uint32_t)(base / kBsGroupRecs));
+    }
+  }
+}
+
+}  // namespace
+
+// Table-free launcher (launch_gcm with the bitsliced engine selected).
+// Lanes per record: 16 (v1: every batch).
+int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, hipStream_t s,
+                  const KernelEvents *ev) {
+  const int num_cus = device_cu_count();
+  if (!num_cus) return 1;
+  const uint64_t n = b.num_records;
+  const uint64_t groups = (n + kBsGroupRecs - 1) / kBsGroupRecs;
+  const size_t ctl_bytes = ((kCtlFlags + groups) * 4 + 255) & ~size_t(255);
+  uint8_t *scratch = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void **>(&scratch), ctl_bytes + n * 16, s) != hipSuccess)
+    return 2;
+  uint32_t *ctl = reinterpret_cast<uint32_t *>(scratch);
+  uint4 *ek0 = reinterpret_cast<uint4 *>(scratch + ctl_bytes);
+  if (hipMemsetAsync(ctl, 0, ctl_bytes, s) != hipSuccess) {
+    hipFreeAsync(scratch, s);
+    return 2;
+  }
+  BatchDesc bo = b;  // with the processing order of a ragged batch
+  uint32_t *order = nullptr;
+  if (wants_length_order(b)) {
+    if (hipMallocAsync(reinterpret_cast<void **>(&order), (n + 128) * sizeof(uint32_t), s) !=
+        hipSuccess) {
+      hipFreeAsync(scratch, s);
+      return 2;
+    }
+    const int orc = build_length_order(b.lengths, n, order, order + n, s);
+    if (orc) {
+      hipFreeAsync(order, s);
+      hipFreeAsync(scratch, s);
+      return orc;
+    }
+    bo.order = order;
+  }
+  if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
+  const uint64_t units = (n + 3) / 4;
+  const unsigned grid = (unsigned)(units < (uint64_t)num_cus ? units : (uint64_t)num_cus);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBsThreads), 0, s, keys, bo, ctl, ek0);
+  };
+#define BSSL_BS_LAUNCH(NR_, OPEN_)                                                   \
+  do {                                                                               \
+    if (b.key_index) {                                                               \
+      if (b.extra_len) go(gcm_bs_keyset_kernel<NR_, OPEN_, true>);                   \
+      else go(gcm_bs_keyset_kernel<NR_, OPEN_, false>);                              \
+    } else if (b.iovecs) {                                                           \
+      go(gcm_bs_kernel<NR_, OPEN_, false, true, 16>);                                \
+    } else if (b.extra_len) {                                                        \
+      go(gcm_bs_kernel<NR_, OPEN_, true, false, 16>);                                \
+    } else {                                                                         \
+      go(gcm_bs_kernel<NR_, OPEN_, false, false, 16>);                               \
+    }                                                                                \
+  } while (0)
+  switch (nr * 2 + (open ? 1 : 0)) {
+#ifdef BSSL_BS_QUICK  // (development builds: AES-128 seal only)
+    case 20: go(gcm_bs_kernel<10, false, false, false, 16>); break;
+#else
+    case 20: BSSL_BS_LAUNCH(10, false); break;
+    case 21: BSSL_BS_LAUNCH(10, true); break;
+    case 24: BSSL_BS_LAUNCH(12, false); break;
+    case 25: BSSL_BS_LAUNCH(12, true); break;
+    case 28: BSSL_BS_LAUNCH(14, false); break;
+    case 29: BSSL_BS_LAUNCH(14, true); break;
+#endif
+    default: break;
+  }
+#undef BSSL_BS_LAUNCH
+  const int rc = (int)hipGetLastError();
+  if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
+  if (order) hipFreeAsync(order, s);
+  hipFreeAsync(scratch, s);
+  return rc;
+}
+
+}  // namespace bssl_amd

@@ -495,12 +495,12 @@ __device__ __forceinline__ void siv_record(const GcmKeyDev *__restrict__ keys, c
     if (j < nA) {
       if constexpr (IOV)
         blk = ivec_load16(b.aadvecs, b.aadvec_start[rec], b.aadvec_start[rec + 1], 16 * j,
-                          (uint32_t)min<uint64_t>(ad_len - 16 * j, 16));
+                          (uint32_t)umin64(ad_len - 16 * j, 16));
       else
         blk = load_block(ad + 16 * j, ad_len - 16 * j);
     } else if (j < nA + nP) {
       const uint64_t p = j - nA;
-      const uint32_t pn = (uint32_t)min<uint64_t>(len - 16 * p, 16);
+      const uint32_t pn = (uint32_t)umin64(len - 16 * p, 16);
       uint4 x;
       if constexpr (IOV)
         x = iov_walk_load(wl, b, rec, 16 * p, pn, 16 * kL);
@@ -570,7 +570,7 @@ __device__ __forceinline__ void siv_record(const GcmKeyDev *__restrict__ keys, c
       iov_walk_init(ws, b, rec);
     }
     for (uint64_t p = q; p < nP; p += kL) {
-      const uint32_t pn = (uint32_t)min<uint64_t>(len - 16 * p, 16);
+      const uint32_t pn = (uint32_t)umin64(len - 16 * p, 16);
       uint4 x;
       if constexpr (IOV)
         x = iov_walk_load(wl, b, rec, 16 * p, pn, 16 * kL);

@@ -2,10 +2,11 @@
 //
 // Device data layout (all resident in HBM, 16-byte aligned):
 //
-//   GcmKeyDev   one per AES-GCM key (8,976 bytes): the AES round keys (T-table
-//               and plain forms), the GHASH nibble table of H^16 and the powers
-//               H^1..H^16 as multipliers of the constant-time VALU product
-//               (gf128_ct.h).
+//   GcmKeyDev   one per AES-GCM key (12,816 bytes): the AES round keys
+//               (T-table and plain forms, and the bitsliced engine's per-round
+//               AddRoundKey masks), the GHASH nibble table of H^16 and the
+//               powers H^1..H^17 as multipliers of the constant-time VALU
+//               product (gf128_ct.h).
 //               Equivalent of the reference's GCM128_KEY
 //               (crypto/fipsmodule/aes/internal.h:325-334), re-laid-out for the
 //               LDS-table GHASH of gcm.hip.
@@ -43,8 +44,15 @@ struct alignas(16) GcmKeyDev {
   // (Rounds 1-2 also held H, H^2, H^4, H^8, H^32 for the record-end tree,
   // which is now the constant-time VALU product.)
   uint32_t htab16[32][16][4];
+  // AddRoundKey of the bitsliced engine (gcm_bs.hip, bs16_aes.h): bsmask[r][i]
+  // with i = 32*h + 8*row + bit is the mask XORed into state register (row, h,
+  // bit) in round r -- 0xffff in the low half when that bit of round-key
+  // column h is set, 0xffff0000 when that bit of column h + 2 is (the engine
+  // holds columns h and h + 2 in the two halves of a register).  Read by
+  // scalar loads, 64 per round, so no SALU work derives them in the rounds.
+  uint32_t bsmask[15][64];
 };
-static_assert(sizeof(GcmKeyDev) == 240 + 16 + 240 + 18 * 16 + 8192, "layout");
+static_assert(sizeof(GcmKeyDev) == 240 + 16 + 240 + 18 * 16 + 8192 + 15 * 256, "layout");
 
 struct alignas(16) ChaChaKeyDev {
   uint32_t k[8];
@@ -161,6 +169,15 @@ struct KernelEvents {
 // error code.  `ev` (optional) brackets the bulk kernel.
 int launch_gcm(const GcmKeyDev *keys, const BatchDesc &b, bool open,
                int nr, void *stream, const KernelEvents *ev);
+// AES-GCM engine of the bulk path: the bitsliced table-free engine
+// (gcm_bs.hip) or the LDS T-table engine (gcm.hip).  Process-wide; the
+// initial value comes from BSSL_AMD_GCM_MODE ("bs" / "bs16" or "table"),
+// read once; BSSL_AMD_set_aes_gcm_engine changes it.
+enum GcmEngine : int { kGcmEngineTable = 0, kGcmEngineBitsliced = 1 };
+int gcm_engine();
+int set_gcm_engine(int engine);  // returns the previous engine, or -1 (bad value)
+int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr,
+                  hipStream_t stream, const KernelEvents *ev);
 // Builds `order` (n entries) grouping records by length class, longest first;
 // `scratch` holds 128 uint32.  Returns 0 or a HIP error code.
 int build_length_order(const uint64_t *lengths, uint64_t n, uint32_t *order, uint32_t *scratch,

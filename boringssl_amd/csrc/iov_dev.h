@@ -19,6 +19,10 @@ namespace {
 // line in the TA, nothing on the VALU).
 typedef uint32_t u32_any __attribute__((aligned(1)));
 
+// Integer min of two 64-bit lengths.  (HIP's min<uint64_t> in device code
+// goes through double precision: two conversions and v_min_f64.)
+__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
 __device__ __forceinline__ uint4 load16_any(const uint8_t *p) {
   const u32_any *ip = reinterpret_cast<const u32_any *>(p);
   return make_uint4(ip[0], ip[1], ip[2], ip[3]);
@@ -168,7 +172,7 @@ __device__ __forceinline__ uint4 bytes_at(uint4 A, uint4 B, uint32_t a) {
 // when more chunks are involved.
 __device__ __forceinline__ bool iov_load2(const BatchDesc &b, const IovCur &k, uint64_t p,
                                           uint32_t n, uint64_t c_end, uint4 &v) {
-  const uint32_t n1 = (uint32_t)min<uint64_t>(n, k.ce - p);
+  const uint32_t n1 = (uint32_t)umin64(n, k.ce - p);
   uint4 v2 = make_uint4(0, 0, 0, 0);
   if (n1 < n) {
     if (k.c + 1 >= c_end) return false;
@@ -184,7 +188,7 @@ __device__ __forceinline__ bool iov_load2(const BatchDesc &b, const IovCur &k, u
 
 __device__ __forceinline__ bool iov_store2(const BatchDesc &b, const IovCur &k, uint64_t p,
                                            uint4 y, uint32_t n, uint64_t c_end) {
-  const uint32_t n1 = (uint32_t)min<uint64_t>(n, k.ce - p);
+  const uint32_t n1 = (uint32_t)umin64(n, k.ce - p);
   IovecDev nx = {nullptr, nullptr, 0};
   if (n1 < n) {
     if (k.c + 1 >= c_end) return false;

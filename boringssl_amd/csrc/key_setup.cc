@@ -184,6 +184,15 @@ bool gcm_key_setup(const uint8_t *key, size_t key_len, GcmKeyDev *out) {
       out->rk[r][c] = (r == 0 || r == nr) ? v : rotl32(v, 16);
       out->rk_plain[r][c] = v;
     }
+  // The bitsliced engine's AddRoundKey masks (GcmKeyDev::bsmask).
+  for (int r = 0; r <= nr; r++)
+    for (int h = 0; h < 2; h++)
+      for (int row = 0; row < 4; row++)
+        for (int bit = 0; bit < 8; bit++) {
+          const uint32_t lo = (out->rk_plain[r][h] >> (8 * row + bit)) & 1u;
+          const uint32_t hi = (out->rk_plain[r][h + 2] >> (8 * row + bit)) & 1u;
+          out->bsmask[r][32 * h + 8 * row + bit] = (lo * 0xffffu) | (hi * 0xffff0000u);
+        }
   uint8_t hb[16] = {0};
   encrypt_block(w, nr, hb, hb);  // H = E_K(0^128), gcm.cc.inc:270-272
   U128 p = load_u128(hb);

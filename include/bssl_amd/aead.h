@@ -245,11 +245,11 @@ BSSL_AMD_EXPORT int EVP_AEAD_CTX_open_batch_device(const EVP_AEAD_CTX *ctx,
  * nonce at nonces + i*nonce_len; tag at tags + i*tag_len (written by seal,
  * read by open).  status[i] (optional) as for BSSL_AMD_BATCH; a failed
  * record's chunks (and, for seal, tag) are zero-filled (clear_iovec,
- * aead.cc.inc:310-333).  The records are gathered into a device staging area,
- * run through the same kernels as BSSL_AMD_BATCH and scattered back; the call
- * synchronises `hip_stream` once (to size the staging area).  Chunks of one
- * batch must not partially overlap (aead.cc.inc:281-308; not checked on the
- * device). */
+ * aead.cc.inc:310-333).  The bulk kernels walk each record's chunks in place
+ * (no staging copy, no gather/scatter pass); the call only enqueues work on
+ * `hip_stream` (one small kernel for the per-record totals, then the bulk
+ * kernels) and never synchronises it.  Chunks of one batch must not partially
+ * overlap (aead.cc.inc:281-308; not checked on the device). */
 typedef struct bssl_amd_iov_batch_st {
   size_t num_records;
   const CRYPTO_IOVEC *iovecs;
@@ -310,6 +310,19 @@ BSSL_AMD_EXPORT void BSSL_AMD_set_kernel_timing(int enable);
 BSSL_AMD_EXPORT size_t BSSL_AMD_collect_kernel_times(double *out_ms, size_t max);
 BSSL_AMD_EXPORT double BSSL_AMD_last_kernel_ms(void);
 BSSL_AMD_EXPORT const char *BSSL_AMD_last_kernel_name(void);
+
+/* AES engine of the AES-GCM bulk path (process-wide; both produce the same
+ * bytes as the reference).  BSSL_AMD_AES_GCM_ENGINE_BITSLICED: AES bitsliced
+ * on the VALU with no lookup table (the reference's own constant-time
+ * approach, aes_nohw.cc.inc:508); BSSL_AMD_AES_GCM_ENGINE_TABLE: AES by
+ * bank-replicated T-tables in LDS.  The initial value comes from the
+ * environment variable BSSL_AMD_GCM_MODE ("bs" or "table"), read once.
+ * Returns the previous engine, or -1 (and changes nothing) for an unknown
+ * value.  Batches already enqueued keep the engine they were launched with. */
+#define BSSL_AMD_AES_GCM_ENGINE_TABLE 0
+#define BSSL_AMD_AES_GCM_ENGINE_BITSLICED 1
+BSSL_AMD_EXPORT int BSSL_AMD_set_aes_gcm_engine(int engine);
+BSSL_AMD_EXPORT int BSSL_AMD_aes_gcm_engine(void);
 
 #ifdef __cplusplus
 }

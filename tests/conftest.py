@@ -34,3 +34,13 @@ def pytest_collection_modifyitems(config, items):
 @pytest.fixture(scope="session")
 def golden_dir():
     return os.path.join(HERE, "golden")
+
+
+@pytest.fixture
+def aes_engine():
+    """Selects the AES-GCM engine for one test ("bs" or "table",
+    BSSL_AMD_set_aes_gcm_engine) and restores the previous one afterwards."""
+    import boringssl_amd as ba
+    prev = ba.aes_gcm_engine()
+    yield ba.set_aes_gcm_engine
+    ba.set_aes_gcm_engine(prev)

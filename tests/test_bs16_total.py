@@ -1,8 +1,8 @@
 """The table-free AES-GCM engine for every batch.
 
-With BSSL_AMD_GCM_MODE=bs16 every AES-GCM batch runs on the bitsliced engine
-(gcm.hip: gcm_prologue_bs16 -> gcm_bs16_kernel / gcm_keyset_bs16_kernel; no
-AES table in LDS or memory, north_star "no T-tables", reference
+With the bitsliced engine selected (BSSL_AMD_set_aes_gcm_engine) every AES-GCM
+batch runs on gcm_bs.hip (gcm_bs_kernel / gcm_bs_keyset_kernel; no AES table
+in LDS or memory, north_star "no T-tables", reference
 aes_nohw.cc.inc:508,866-878): one-key and keyset batches, any record length,
 alignment and AD, extra bytes (the TLS 1.3 inner type), iovec records and
 single records.  This module re-runs the GCM cases of the parity suite under
@@ -31,11 +31,11 @@ GCM = ["aes-128-gcm", "aes-256-gcm"]
 
 
 @pytest.fixture(autouse=True)
-def _bs16(monkeypatch):
+def _bs16(aes_engine):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     torch.cuda.set_device(0)
-    monkeypatch.setenv("BSSL_AMD_GCM_MODE", "bs16")
+    aes_engine("bs")
     yield
 
 

@@ -233,14 +233,14 @@ def test_batch_large_ragged_reordered(aead, multikey):
     assert st.all() and back == ins
 
 
-@pytest.mark.parametrize("mode", ["bs16"])
+@pytest.mark.parametrize("mode", ["bs"])
 @pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-192-gcm", "aes-256-gcm"])
 @pytest.mark.parametrize("rlen", [4096, 16384, 17408, 32768])
-def test_bitsliced_gcm_path(aead, rlen, mode, monkeypatch):
-    """The table-free engine (BSSL_AMD_GCM_MODE=bs16, gcm_bs16_kernel) on
+def test_bitsliced_gcm_path(aead, rlen, mode, aes_engine):
+    """The table-free engine (gcm_bs.hip, BSSL_AMD_set_aes_gcm_engine) on
     uniform, 16-byte-multiple records: full and partial 256-block chunks,
     seal and open (tags verified, one tampered record)."""
-    monkeypatch.setenv("BSSL_AMD_GCM_MODE", mode)
+    aes_engine(mode)
     rng = np.random.default_rng(rlen + len(mode))
     n = 50
     key = rng.integers(0, 256, size=AEAD_KEYLEN[aead], dtype=np.uint8).tobytes()
@@ -275,14 +275,14 @@ def test_bitsliced_gcm_path(aead, rlen, mode, monkeypatch):
     assert np.array_equal(np.delete(back.reshape(n, rlen), 7, 0), np.delete(pt.reshape(n, rlen), 7, 0))
 
 
-@pytest.mark.parametrize("mode", ["bs16"])
+@pytest.mark.parametrize("mode", ["bs"])
 @pytest.mark.parametrize("aead", ["aes-128-gcm", "aes-256-gcm"])
-def test_mix_kernel_ragged(aead, mode, monkeypatch):
-    """The table-free kernel (gcm_bs16_kernel) on a ragged one-key batch:
+def test_mix_kernel_ragged(aead, mode, aes_engine):
+    """The table-free kernel (gcm_bs_kernel) on a ragged one-key batch:
     16-byte-multiple records of 4-19 KiB mixed with records of any length,
     at two alignments -- every record must match the oracle, sealed and
     opened."""
-    monkeypatch.setenv("BSSL_AMD_GCM_MODE", mode)
+    aes_engine(mode)
     rng = random.Random(len(mode) * 7 + len(aead))
     key = bytes(rng.getrandbits(8) for _ in range(AEAD_KEYLEN[aead]))
     n = 600
