@@ -251,7 +251,7 @@ template <int NR, bool OPEN, bool XT, bool IOV, int L>
 __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const BatchDesc &b,
                                         uint64_t i, bool active, uint8_t *smem,
                                         const uint4 *ek0, uint32_t *flag) {
-  static_assert(L == 16 || L == 8 || L == 4, "lanes per record");
+  static_assert(L == 16 || L == 8 || L == 4 || L == 2, "lanes per record");
   static_assert(!(IOV && XT), "iovec records carry no extra bytes");
   const int q = threadIdx.x & (L - 1);
   // (Inline-asm LDS accesses: the compiler must neither forward the stored
@@ -411,16 +411,34 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
       const uint64_t a0 = reinterpret_cast<uint64_t>(s0), a1 = reinterpret_cast<uint64_t>(d0);
       const uint32_t rb = (uint32_t)gq & 3u;
       const bool any_tail = __ballot(tl >= 0) != 0;
+      const bool full = !any_tail && __ballot(nv < 16) == 0;
 #define BS_IO(SUFFIX) bs_chunk_io_##SUFFIX(KA, KB, accv, kt, a0, a1, kM1, kM2, rb, nv, tl, P)
+#if defined(BSSL_AMD_BS_ABLATE)  // diagnostic builds (wrong output): 1 no GHASH, 2 no I/O, 3 neither
+      if constexpr (BSSL_AMD_BS_ABLATE == 1) BS_IO(seal_L16_noghash);
+      else if constexpr (BSSL_AMD_BS_ABLATE == 2) BS_IO(seal_L16_nomem);
+      else if constexpr (BSSL_AMD_BS_ABLATE == 3) BS_IO(seal_L16_none);
+      else if constexpr (BSSL_AMD_BS_ABLATE == 4) {
+#pragma unroll
+        for (int k = 0; k < 32; k++) accv[k & 3] ^= KA[k] ^ KB[k];
+      }
+      if constexpr (false)
+#endif
       if constexpr (L == 16) {
-        if (any_tail) { if constexpr (OPEN) BS_IO(open_tail_L16); else BS_IO(seal_tail_L16); }
+        if (full) { if constexpr (OPEN) BS_IO(open_full_L16); else BS_IO(seal_full_L16); }
+        else if (any_tail) { if constexpr (OPEN) BS_IO(open_tail_L16); else BS_IO(seal_tail_L16); }
         else { if constexpr (OPEN) BS_IO(open_L16); else BS_IO(seal_L16); }
       } else if constexpr (L == 8) {
-        if (any_tail) { if constexpr (OPEN) BS_IO(open_tail_L8); else BS_IO(seal_tail_L8); }
+        if (full) { if constexpr (OPEN) BS_IO(open_full_L8); else BS_IO(seal_full_L8); }
+        else if (any_tail) { if constexpr (OPEN) BS_IO(open_tail_L8); else BS_IO(seal_tail_L8); }
         else { if constexpr (OPEN) BS_IO(open_L8); else BS_IO(seal_L8); }
-      } else {
-        if (any_tail) { if constexpr (OPEN) BS_IO(open_tail_L4); else BS_IO(seal_tail_L4); }
+      } else if constexpr (L == 4) {
+        if (full) { if constexpr (OPEN) BS_IO(open_full_L4); else BS_IO(seal_full_L4); }
+        else if (any_tail) { if constexpr (OPEN) BS_IO(open_tail_L4); else BS_IO(seal_tail_L4); }
         else { if constexpr (OPEN) BS_IO(open_L4); else BS_IO(seal_L4); }
+      } else {
+        if (full) { if constexpr (OPEN) BS_IO(open_full_L2); else BS_IO(seal_full_L2); }
+        else if (any_tail) { if constexpr (OPEN) BS_IO(open_tail_L2); else BS_IO(seal_tail_L2); }
+        else { if constexpr (OPEN) BS_IO(open_L2); else BS_IO(seal_L2); }
       }
 #undef BS_IO
       if (tl >= 0) {
@@ -621,21 +639,25 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_kernel(const GcmKeyDev *__r
   __syncthreads();
   constexpr uint32_t kRec = 64 / L;
   constexpr uint32_t kGroupUnits = kBsGroupRecs / kRec;
-  const uint64_t n = b.num_records;
+  // Processing positions of this launch (BatchDesc::split_lo/_hi: a length
+  // class of a ragged batch); E_K(J0) groups count from lo.
+  uint64_t lo = 0, n = b.num_records;
+  if (b.split_lo) lo = *b.split_lo;
+  if (b.split_hi) n = *b.split_hi;
   uint32_t *flags = ctl + kCtlFlags;
   for (;;) {
     uint32_t u = 0;
     if (lane == 0) u = atomicAdd(ctl, 1u);
     u = __builtin_amdgcn_readfirstlane(u);
-    const uint64_t first = (uint64_t)u * kRec;
+    const uint64_t first = lo + (uint64_t)u * kRec;
     if (first >= n) break;
     // Producer units: 0 for group 0, the middle unit of group g for g + 1.
     const uint32_t g = u / kGroupUnits;
     uint32_t pg = 0xffffffffu;
     if (u == 0) pg = 0;
-    if (u % kGroupUnits == kGroupUnits / 2 && (uint64_t)(g + 1) * kBsGroupRecs < n) pg = g + 1;
+    if (u % kGroupUnits == kGroupUnits / 2 && lo + (uint64_t)(g + 1) * kBsGroupRecs < n) pg = g + 1;
     if (pg != 0xffffffffu)
-      produce_ek0<NR, false>(keys, b, (uint64_t)pg * kBsGroupRecs, n, ek0, flags + pg);
+      produce_ek0<NR, false>(keys, b, lo + (uint64_t)pg * kBsGroupRecs, n, ek0, flags + pg);
     const uint64_t i = first + (uint64_t)(lane / L);
     bs_unit<NR, OPEN, XT, IOV, L>(keys, b, i, i < n, smem, ek0, flags + g);
   }
@@ -722,20 +744,29 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_keyset_kernel(
 }  // namespace
 
 // Table-free launcher (launch_gcm with the bitsliced engine selected).
-// Lanes per record: 16 (v1: every batch).
+// Lanes per record: 16 for records of 4 KiB or more, 2 for shorter ones
+// (a chunk covers 16 * L blocks of a record: a 1350-byte record of 85
+// blocks fills 3 chunks of 32 slots at L = 2, against one of 256 at L = 16;
+// the per-record start and end are spread over the record's L lanes, and at
+// L = 2 each lane has eight times the blocks).  A ragged batch in length
+// order is two launches, the records of 4 KiB or more at 16 lanes and the
+// shorter ones at 2 (the class cursor of the length sort, as gcm.hip).
 int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, hipStream_t s,
                   const KernelEvents *ev) {
   const int num_cus = device_cu_count();
   if (!num_cus) return 1;
   const uint64_t n = b.num_records;
   const uint64_t groups = (n + kBsGroupRecs - 1) / kBsGroupRecs;
-  const size_t ctl_bytes = ((kCtlFlags + groups) * 4 + 255) & ~size_t(255);
+  // Two control blocks (one per launch of a split batch): unit counter and
+  // E_K(J0) group flags, zeroed; then E_K(J0) of every processing position.
+  const size_t ctl_bytes = ((kCtlFlags + groups + 1) * 4 + 255) & ~size_t(255);
   uint8_t *scratch = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void **>(&scratch), ctl_bytes + n * 16, s) != hipSuccess)
+  if (hipMallocAsync(reinterpret_cast<void **>(&scratch), 2 * ctl_bytes + n * 16, s) != hipSuccess)
     return 2;
   uint32_t *ctl = reinterpret_cast<uint32_t *>(scratch);
-  uint4 *ek0 = reinterpret_cast<uint4 *>(scratch + ctl_bytes);
-  if (hipMemsetAsync(ctl, 0, ctl_bytes, s) != hipSuccess) {
+  uint32_t *ctl2 = reinterpret_cast<uint32_t *>(scratch + ctl_bytes);
+  uint4 *ek0 = reinterpret_cast<uint4 *>(scratch + 2 * ctl_bytes);
+  if (hipMemsetAsync(ctl, 0, 2 * ctl_bytes, s) != hipSuccess) {
     hipFreeAsync(scratch, s);
     return 2;
   }
@@ -756,27 +787,43 @@ int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, 
     bo.order = order;
   }
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
-  const uint64_t units = (n + 3) / 4;
-  const unsigned grid = (unsigned)(units < (uint64_t)num_cus ? units : (uint64_t)num_cus);
-  auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBsThreads), 0, s, keys, bo, ctl, ek0);
+  const unsigned grid = (unsigned)((n + 3) / 4 < (uint64_t)num_cus ? (n + 3) / 4 : (uint64_t)num_cus);
+  auto go = [&](auto kern, const BatchDesc &d, uint32_t *c) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBsThreads), 0, s, keys, d, c, ek0);
   };
+  // Length classes (one-key, not iovec): short uniform records take L = 2;
+  // a ragged batch in length order splits at 4 KiB.
+  const bool split = !b.key_index && !b.iovecs && order;
+  const bool short_uniform = !b.key_index && !b.iovecs && !b.lengths && b.record_len < 4096;
+  BatchDesc bl = bo, bs = bo;
+  if (split) bl.split_hi = bs.split_lo = order + n + kSplitWord;
+#define BSSL_BS_ONEKEY(NR_, OPEN_, XT_)                                              \
+  do {                                                                               \
+    if (split) {                                                                     \
+      go(gcm_bs_kernel<NR_, OPEN_, XT_, false, 16>, bl, ctl);                        \
+      go(gcm_bs_kernel<NR_, OPEN_, XT_, false, 2>, bs, ctl2);                        \
+    } else if (short_uniform) {                                                      \
+      go(gcm_bs_kernel<NR_, OPEN_, XT_, false, 2>, bo, ctl);                         \
+    } else {                                                                         \
+      go(gcm_bs_kernel<NR_, OPEN_, XT_, false, 16>, bo, ctl);                        \
+    }                                                                                \
+  } while (0)
 #define BSSL_BS_LAUNCH(NR_, OPEN_)                                                   \
   do {                                                                               \
     if (b.key_index) {                                                               \
-      if (b.extra_len) go(gcm_bs_keyset_kernel<NR_, OPEN_, true>);                   \
-      else go(gcm_bs_keyset_kernel<NR_, OPEN_, false>);                              \
+      if (b.extra_len) go(gcm_bs_keyset_kernel<NR_, OPEN_, true>, bo, ctl);          \
+      else go(gcm_bs_keyset_kernel<NR_, OPEN_, false>, bo, ctl);                     \
     } else if (b.iovecs) {                                                           \
-      go(gcm_bs_kernel<NR_, OPEN_, false, true, 16>);                                \
+      go(gcm_bs_kernel<NR_, OPEN_, false, true, 16>, bo, ctl);                       \
     } else if (b.extra_len) {                                                        \
-      go(gcm_bs_kernel<NR_, OPEN_, true, false, 16>);                                \
+      BSSL_BS_ONEKEY(NR_, OPEN_, true);                                              \
     } else {                                                                         \
-      go(gcm_bs_kernel<NR_, OPEN_, false, false, 16>);                               \
+      BSSL_BS_ONEKEY(NR_, OPEN_, false);                                             \
     }                                                                                \
   } while (0)
   switch (nr * 2 + (open ? 1 : 0)) {
 #ifdef BSSL_BS_QUICK  // (development builds: AES-128 seal only)
-    case 20: go(gcm_bs_kernel<10, false, false, false, 16>); break;
+    case 20: go(gcm_bs_kernel<10, false, false, false, 16>, bo, ctl); break;
 #else
     case 20: BSSL_BS_LAUNCH(10, false); break;
     case 21: BSSL_BS_LAUNCH(10, true); break;
@@ -788,6 +835,7 @@ int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, 
     default: break;
   }
 #undef BSSL_BS_LAUNCH
+#undef BSSL_BS_ONEKEY
   const int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
   if (order) hipFreeAsync(order, s);

@@ -226,12 +226,15 @@ __device__ __forceinline__ uint64_t rec_at(const BatchDesc &b, uint64_t i) {
 
 
 // XOR of a word over the L lanes of its group (L = 16: row_xor16; L = 8:
-// row_half_mirror then the quad permutations; L = 4: the quad permutations),
+// row_half_mirror then the quad permutations; L = 4: the quad permutations;
+// L = 2: the quad permutation 1032),
 // in every lane of the group.
 template <int L>
 __device__ __forceinline__ uint32_t row_xor(uint32_t v) {
-  static_assert(L == 16 || L == 8 || L == 4, "lanes per record");
+  static_assert(L == 16 || L == 8 || L == 4 || L == 2, "lanes per record");
   if constexpr (L == 16) return row_xor16(v);
+  if constexpr (L == 2)
+    return v ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false);  // quad 1032
   if constexpr (L == 8)
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false);  // half mirror
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false);    // quad 2301
