@@ -102,15 +102,70 @@ __device__ __forceinline__ void bs16_cipher(uint32_t (&p)[4][2][8],
   }
 }
 
-// Rounds 1..NR with the AddRoundKey masks taken from the key's precomputed
-// table (GcmKeyDev::bsmask: 64 words per round, mask of register (r, h, b)
-// at 32*h + 8*r + b).  `mk` is wave-uniform, so the masks arrive by scalar
-// loads (4 x s_load_dwordx16 per round) instead of ~5 SALU operations each.
-template <int NR>
-__device__ __forceinline__ void bs16_cipher_tab(uint32_t (&p)[4][2][8],
+// One round (SubBytes, ShiftRows, MixColumns unless LAST, AddRoundKey) with
+// the AddRoundKey masks of the key's precomputed table (GcmKeyDev::bsmask:
+// 64 words per round, mask of register (r, h, b) at 32*h + 8*r + b; `m` is
+// wave-uniform, so the masks arrive by scalar loads).  C1: the SubBytes
+// outputs of the pair-0 groups (r, 0) are supplied in c1 instead of computed
+// (round 1 of counter blocks, where those groups hold J0 words 0 and 2,
+// the same in every slot: counter-mode caching).
+template <bool LAST, bool C1>
+__device__ __forceinline__ void bs16_round_tab(uint32_t (&p)[4][2][8],
+                                               const uint32_t *__restrict__ m,
+                                               const uint32_t (*c1)[8]) {
+  uint32_t np[4][2][8];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    uint32_t a[4][8];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      if (C1 && ((h + r) & 1) == 0) {
+#pragma unroll
+        for (int b = 0; b < 8; b++) a[r][b] = c1[r][b];
+      } else {
+        sbox_planes(p[r][(h + r) & 1], a[r]);
+      }
+      if (((h + r) >> 1) & 1) {
+#pragma unroll
+        for (int b = 0; b < 8; b++) a[r][b] = swap16(a[r][b]);
+      }
+    }
+    if (!LAST) {
+      uint32_t km[4][8], o[4][8];
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int b = 0; b < 8; b++) km[r][b] = m[32 * h + 8 * r + b];
+      bs16_mix(a, o, km);
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int b = 0; b < 8; b++) np[r][h][b] = o[r][b];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int b = 0; b < 8; b++) np[r][h][b] = a[r][b] ^ m[32 * h + 8 * r + b];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+      for (int b = 0; b < 8; b++) p[r][h][b] = np[r][h][b];
+}
+
+// Rounds 1..NR with the key's AddRoundKey mask table (bs16_round_tab).
+// Rounds R0..NR with the key's AddRoundKey mask table: one loop whose body
+// branches to the last round's form inside (peeling the last round out, or
+// branching around whole rounds, measured spills in the loop: the register
+// allocator handles the loop-carried state better this way).
+template <int NR, int R0 = 1>
+__device__ __forceinline__ void bs16_rounds_tab(uint32_t (&p)[4][2][8],
                                                 const uint32_t *__restrict__ mk) {
 #pragma unroll 1
-  for (int rd = 1; rd <= NR; rd++) {
+  for (int rd = R0; rd <= NR; rd++) {
     const uint32_t *__restrict__ m = mk + 64 * rd;
     const bool last = rd == NR;
     uint32_t np[4][2][8];
@@ -150,6 +205,22 @@ __device__ __forceinline__ void bs16_cipher_tab(uint32_t (&p)[4][2][8],
 #pragma unroll
         for (int b = 0; b < 8; b++) p[r][h][b] = np[r][h][b];
   }
+}
+
+template <int NR>
+__device__ __forceinline__ void bs16_cipher_tab(uint32_t (&p)[4][2][8],
+                                                const uint32_t *__restrict__ mk) {
+  bs16_rounds_tab<NR, 1>(p, mk);
+}
+
+// The same for counter blocks whose pair-0 groups are the same in every slot
+// (columns 0 and 2 of J0 ^ rk0): their round-1 SubBytes outputs come in c1
+// (computed once per record), and p's pair 0 is not read.
+template <int NR>
+__device__ __forceinline__ void bs16_cipher_ctr(uint32_t (&p)[4][2][8], const uint32_t (&c1)[4][8],
+                                                const uint32_t *__restrict__ mk) {
+  bs16_round_tab<false, true>(p, mk + 64, c1);
+  bs16_rounds_tab<NR, 2>(p, mk);
 }
 
 }  // namespace bssl_amd

@@ -235,7 +235,8 @@ __device__ __forceinline__ uint4 consume_ek0(const uint4 *ek0, uint32_t *flag, u
 // lanes on consecutive banks).  The rounds need ~105 VGPRs of the 128; these
 // values would otherwise stay live across them and spill.
 enum : int {
-  kSw0, kSw1, kSw2,  // J0 words 0..2 XOR round key 0 (round 0 of every counter block)
+  kSc0, kSw1, kSc1,  // round-1 S-box outputs of the pair-0 groups (packed, bs_unit) and
+                     // J0 word 1 XOR round key 0
   kScb,              // counter word of the lane's slot 0 of chunk 0: bswap(J0.w) + 1 + q
   kSnb, kSnfull,     // the record's blocks and full blocks (this lane's record)
   kSoff, kSoffHi,    // the record's offset in in / out
@@ -299,9 +300,30 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
     const uint32_t nb = live ? (uint32_t)((m.len + m.xlen + 15) / 16) : 0u;
     const uint32_t nfull = live && !IOV ? (uint32_t)(m.len / 16) : 0u;
     nchunks = wave_max((int)((nb + 16 * L - 1) / (16 * L)));
-    put(kSw0, j0.x ^ key->rk_plain[0][0]);
+    // Counter-mode caching: the pair-0 groups (columns 0 and 2 of J0 ^ rk0)
+    // are the same in every slot of every chunk, so their round-1 SubBytes
+    // is done once here.  Each of the 32 output planes is 0 / 0xffff per
+    // half: packed as bits k (low half) and 16 + k (high half) of two words.
+    {
+      const uint32_t w0 = j0.x ^ key->rk_plain[0][0], w2 = j0.z ^ key->rk_plain[0][2];
+      uint32_t pk[2] = {0, 0};
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        uint32_t g[8], o[8];
+#pragma unroll
+        for (int bb = 0; bb < 8; bb++)
+          g[bb] = (bit_mask(w0, 8 * r + bb) & 0xffffu) | (bit_mask(w2, 8 * r + bb) & 0xffff0000u);
+        sbox_planes(g, o);
+#pragma unroll
+        for (int bb = 0; bb < 8; bb++) {
+          const int k = 8 * (r & 1) + bb;
+          pk[r >> 1] |= ((o[bb] & 1u) << k) | (((o[bb] >> 16) & 1u) << (16 + k));
+        }
+      }
+      put(kSc0, pk[0]);
+      put(kSc1, pk[1]);
+    }
     put(kSw1, j0.y ^ key->rk_plain[0][1]);
-    put(kSw2, j0.z ^ key->rk_plain[0][2]);
     put(kScb, bswap32(j0.w) + 1u + (uint32_t)q);
     put(kSnb, nb);
     put(kSnfull, nfull);
@@ -327,11 +349,8 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
       // slot: 0 / 0xffff per half); pair 1 = column 1 (low half, constant)
       // and the counter words of column 3 (high half), out of one transpose:
       // t[n] = column 1, t[16 + n] = word 3 of slot n.
-      const uint32_t w0 = get(kSw0), w1 = get(kSw1), w2 = get(kSw2);
+      const uint32_t w1 = get(kSw1);
       const uint32_t rk3 = key->rk_plain[0][3];
-#pragma unroll
-      for (int k = 0; k < 32; k++)
-        p[k / 8][0][k % 8] = (bit_mask(w0, k) & 0xffffu) | (bit_mask(w2, k) & 0xffff0000u);
       const uint32_t cb = get(kScb) + (uint32_t)(16 * L) * (uint32_t)c;  // inc32: mod 2^32
       uint32_t t[32];
 #pragma unroll
@@ -343,7 +362,24 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
 #pragma unroll
       for (int k = 0; k < 32; k++) p[k / 8][1][k % 8] = t[k];
     }
-    bs16_cipher_tab<NR>(p, mk);
+    {
+      // Round 1 of the pair-0 groups from the per-record cache: plane k of
+      // packed word W is W << (15 - k) with each 16-bit half shifted right
+      // arithmetically by 15 (v_pk_ashrrev_i16).
+      typedef short s16x2 __attribute__((ext_vector_type(2)));
+      const uint32_t pk[2] = {get(kSc0), get(kSc1)};
+      uint32_t c1[4][8];
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int bb = 0; bb < 8; bb++) {
+          const int k = 8 * (r & 1) + bb;
+          s16x2 v = __builtin_bit_cast(s16x2, pk[r >> 1] << (15 - k));
+          v = v >> (short)15;
+          c1[r][bb] = __builtin_bit_cast(uint32_t, v);
+        }
+      bs16_cipher_ctr<NR>(p, c1, mk);
+    }
     // Pass 1 (memory): out = in ^ keystream for the lane's full blocks, the
     // plaintext loads running kAhead slots ahead (slot n of the lane is 16*L*n
     // bytes past slot 0: immediate offsets); the hashed block (the ciphertext:
