@@ -73,6 +73,7 @@ EXPORTED_SYMBOLS = [
     "BSSL_AMD_set_device", "BSSL_AMD_device_count", "BSSL_AMD_synth_fill_device",
     "BSSL_AMD_set_kernel_timing", "BSSL_AMD_collect_kernel_times", "BSSL_AMD_last_kernel_ms",
     "BSSL_AMD_last_kernel_name", "BSSL_AMD_set_aes_gcm_engine", "BSSL_AMD_aes_gcm_engine",
+    "BSSL_AMD_gcm_key_tables",
     # include/bssl_amd/tls.h
     "BSSL_AMD_TLS_AEAD_new", "BSSL_AMD_TLS_AEAD_free", "BSSL_AMD_TLS_AEAD_prefix_len",
     "BSSL_AMD_TLS_AEAD_suffix_len", "BSSL_AMD_TLS_AEAD_sequence",
@@ -165,6 +166,7 @@ _SIGS = {
     "BSSL_AMD_last_kernel_name": (ctypes.c_char_p, []),
     "BSSL_AMD_set_aes_gcm_engine": (_I, [_I]),
     "BSSL_AMD_aes_gcm_engine": (_I, []),
+    "BSSL_AMD_gcm_key_tables": (_S, [_P, _S, _S, _I, _P]),
     "BSSL_AMD_TLS_AEAD_new": (_P, [_I, ctypes.c_uint16, _P, _P, _S, _P, _S, ctypes.c_uint64]),
     "BSSL_AMD_TLS_AEAD_free": (None, [_P]),
     "BSSL_AMD_TLS_AEAD_prefix_len": (_S, [_P]),
@@ -480,6 +482,20 @@ def collect_kernel_times(max_n=4096):
 
 
 AES_GCM_ENGINES = {"table": 0, "bs": 1}
+
+
+def gcm_key_tables(keys, key_len, on_device):
+    """The per-key AES-GCM device tables (GcmKeyDev bytes, one entry per key)
+    of the concatenated `keys`, from the host key setup (on_device False) or
+    the device key-setup kernel (True)."""
+    size = lib.BSSL_AMD_gcm_key_tables(None, 0, 0, 0, None)
+    n = len(keys) // key_len
+    out = ctypes.create_string_buffer(size * n)
+    kb = ctypes.create_string_buffer(bytes(keys), max(len(keys), 1))
+    if lib.BSSL_AMD_gcm_key_tables(kb, key_len, n, 1 if on_device else 0, out) != n:
+        raise RuntimeError("BSSL_AMD_gcm_key_tables failed")
+    raw = out.raw
+    return [raw[i * size:(i + 1) * size] for i in range(n)]
 
 
 def set_aes_gcm_engine(engine):

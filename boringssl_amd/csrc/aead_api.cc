@@ -134,11 +134,35 @@ CtxState *state_of(const EVP_AEAD_CTX *ctx) {
   return reinterpret_cast<CtxState *>(const_cast<uint8_t *>(ctx->state.opaque));
 }
 
-KeyMaterial *make_keys(const EVP_AEAD *aead, const uint8_t *keys, size_t num_keys) {
+// Key material of num_keys keys on the current device.  AES-GCM(-SIV) key
+// sets of kDeviceKeySetupMin keys or more are expanded by the device kernel
+// straight into device memory (gcm_key_setup_device); smaller ones -- the
+// single key of EVP_AEAD_CTX_init -- on the host and copied (a kernel launch
+// and synchronisation cost more than the host's few microseconds per key).
+// device_setup: -1 by that rule, 0 host, 1 device (BSSL_AMD_gcm_key_tables).
+KeyMaterial *make_keys(const EVP_AEAD *aead, const uint8_t *keys, size_t num_keys,
+                       int device_setup = -1) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   KeyMaterial *km = new (std::nothrow) KeyMaterial{aead, dev, num_keys, 0, nullptr, 0};
   if (!km) return nullptr;
+  const bool gcm = aead->kind == kAeadAesGcm || aead->kind == kAeadAesGcmSiv;
+  if (gcm && num_keys && (device_setup == 1 || (device_setup < 0 && num_keys >= kDeviceKeySetupMin))) {
+    const size_t bytes = num_keys * sizeof(GcmKeyDev);
+    if (hipMalloc(&km->dev, bytes) != hipSuccess) {
+      delete km;
+      return nullptr;
+    }
+    km->bytes = bytes;
+    if (gcm_key_setup_device(keys, aead->key_len, num_keys, reinterpret_cast<GcmKeyDev *>(km->dev),
+                             nullptr) != 0) {
+      hipFree(km->dev);
+      delete km;
+      return nullptr;
+    }
+    km->nr = (int)aead->key_len / 4 + 6;
+    return km;
+  }
   size_t bytes;
   std::vector<uint8_t> host;
   struct Wipe {  // the expanded keys in host memory are wiped on every path
@@ -251,7 +275,7 @@ int launch_desc(const KeyMaterial *km, const BatchDesc &d, bool open, void *stre
 // nonce / AD; BatchDesc::done, ::inl), or null.
 int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch, bool open,
               bool use_key_index, void *stream, const uint8_t *valid = nullptr,
-              const BatchDesc *one = nullptr) {
+              const BatchDesc *one = nullptr, bool *done_armed = nullptr) {
   BatchDesc d;
   memset(&d, 0, sizeof(d));
   d.in = batch->in;
@@ -279,7 +303,14 @@ int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch
   d.extra_out = nullptr;
   d.extra_len = d.extra_stride = d.extra_out_stride = d.tag_stride = 0;
   if (one) {
-    d.done = one->done;
+    // The completion word only when a one-record kernel will write it
+    // (*done_armed tells one_record whether to spin on it).
+    const AeadKind k = km->aead->kind;
+    const bool writes = k == kAeadAesGcm ? gcm_takes_one_record_kernel(d)
+                        : k == kAeadAesGcmSiv ? false
+                                              : chacha_takes_one_record_kernel(d);
+    d.done = writes ? one->done : nullptr;
+    if (done_armed) *done_armed = d.done != nullptr;
     d.done_seq = one->done_seq;
     d.inl = one->inl;
     memcpy(d.inl_nonce, one->inl_nonce, sizeof(d.inl_nonce));
@@ -362,10 +393,14 @@ Scratch *scratch(size_t bytes) {
       sc.dev = nullptr;
       return nullptr;
     }
-    // Mapped (and, by HIP's default, coherent) pinned memory; the kernels use
-    // its device address.  (Coherent / non-coherent / portable flag variants
-    // measured the same single-record latency, profiles/r04/s10/.)
-    if (hipHostMalloc(&sc.host, cap, hipHostMallocMapped) != hipSuccess) {
+    // Mapped pinned memory, explicitly fine-grained (hipHostMallocCoherent:
+    // with any flag but hipHostMallocDefault, HIP's coherence otherwise follows
+    // HIP_HOST_COHERENT, 0 by default).  The host spins on the completion word
+    // while the kernel runs, and the kernel re-reads lines the host rewrote in
+    // place since the previous call; both need the coherent mapping.  The
+    // kernels use its device address.  (Flag variants measured the same
+    // single-record latency, profiles/r04/s10/.)
+    if (hipHostMalloc(&sc.host, cap, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
       sc.host = nullptr;
       hipFree(sc.dev);
       sc.dev = nullptr;
@@ -395,13 +430,21 @@ size_t one_record_map_max() {
   return v;
 }
 
-// Waits for a single-record launch on stream s.  With `done` (mapped path)
-// the host spins on the completion word the one-record kernels write after
-// their last store -- it lands a few microseconds before the stream's
-// completion signal does -- and checks the stream every 256 polls, so a
-// launch that took another kernel (which does not write the word) or failed
-// still ends.  Otherwise (and for records that took the copies) it syncs the
-// stream.
+// Waits for a single-record launch on stream s.  With `done` (mapped path and
+// a one-record kernel launched: run_batch arms the word only then) the host
+// spins on the completion word the kernel writes after its last store -- it
+// lands a few microseconds before the stream's completion signal does -- and
+// checks the stream every 256 polls, so a failed launch still ends.
+// Otherwise (other kernels, records that took the copies) it blocks in
+// hipStreamSynchronize.
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#elif defined(__aarch64__)
+  asm volatile("yield");
+#endif
+}
+
 bool wait_record(hipStream_t s, const uint32_t *done, uint32_t seq) {
   if (!done) return hipStreamSynchronize(s) == hipSuccess;
   for (uint32_t i = 1;; i++) {
@@ -411,7 +454,7 @@ bool wait_record(hipStream_t s, const uint32_t *done, uint32_t seq) {
       if (e == hipSuccess) return true;
       if (e != hipErrorNotReady) return false;
     }
-    __builtin_ia32_pause();
+    cpu_relax();
   }
 }
 
@@ -482,10 +525,11 @@ int one_record(const EVP_AEAD_CTX *ctx, bool open, const uint8_t *in, uint8_t *o
     if (ad_len) memcpy(one.inl_ad, ad, ad_len);
     one.inl |= 2;
   }
-  if (!run_batch(st->km, tag_len, &b, open, false, s, nullptr, &one)) return 0;
+  bool armed = false;
+  if (!run_batch(st->km, tag_len, &b, open, false, s, nullptr, &one, &armed)) return 0;
   bool ok = mapped || hipMemcpyAsync(h + o_tag, d + o_tag, o_in - o_tag + len,
                                      hipMemcpyDeviceToHost, s) == hipSuccess;
-  ok = ok && wait_record(s, mapped ? hdone : nullptr, seq);
+  ok = ok && wait_record(s, armed ? hdone : nullptr, seq);
   if (!ok) {
     PUT_ERROR(ERR_R_INTERNAL_ERROR);
     return 0;
@@ -1296,6 +1340,26 @@ size_t BSSL_AMD_collect_kernel_times(double *out_ms, size_t max) {
 
 int BSSL_AMD_set_aes_gcm_engine(int engine) { return set_gcm_engine(engine); }
 int BSSL_AMD_aes_gcm_engine(void) { return gcm_engine(); }
+
+size_t BSSL_AMD_gcm_key_tables(const uint8_t *keys, size_t key_len, size_t n, int on_device,
+                               uint8_t *out) {
+  if (!out) return sizeof(GcmKeyDev);
+  if (key_len != 16 && key_len != 24 && key_len != 32) return 0;
+  GcmKeyDev *h = reinterpret_cast<GcmKeyDev *>(out);
+  if (!on_device) {
+    for (size_t i = 0; i < n; i++)
+      if (!gcm_key_setup(keys + i * key_len, key_len, &h[i])) return 0;
+    return n;
+  }
+  GcmKeyDev *d = nullptr;
+  if (hipMalloc(reinterpret_cast<void **>(&d), n * sizeof(GcmKeyDev)) != hipSuccess) return 0;
+  bool ok = gcm_key_setup_device(keys, key_len, n, d, nullptr) == 0 &&
+            hipMemcpy(out, d, n * sizeof(GcmKeyDev), hipMemcpyDeviceToHost) == hipSuccess;
+  hipMemset(d, 0, n * sizeof(GcmKeyDev));
+  hipDeviceSynchronize();
+  hipFree(d);
+  return ok ? n : 0;
+}
 
 double BSSL_AMD_last_kernel_ms(void) { return t_timing.last_ms; }
 const char *BSSL_AMD_last_kernel_name(void) { return t_timing.last_name; }

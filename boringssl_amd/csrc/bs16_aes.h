@@ -161,11 +161,19 @@ __device__ __forceinline__ void bs16_round_tab(uint32_t (&p)[4][2][8],
 // branches to the last round's form inside (peeling the last round out, or
 // branching around whole rounds, measured spills in the loop: the register
 // allocator handles the loop-carried state better this way).
-template <int NR, int R0 = 1>
+// `hook(rd)` runs at the start of round rd (between rounds, where only the
+// state is live: e.g. a prefetch of the chunk's record bytes).
+struct BsNoHook {
+  __device__ void operator()(int) const {}
+};
+
+template <int NR, int R0 = 1, class Hook = BsNoHook>
 __device__ __forceinline__ void bs16_rounds_tab(uint32_t (&p)[4][2][8],
-                                                const uint32_t *__restrict__ mk) {
+                                                const uint32_t *__restrict__ mk,
+                                                const Hook &hook = Hook()) {
 #pragma unroll 1
   for (int rd = R0; rd <= NR; rd++) {
+    hook(rd);
     const uint32_t *__restrict__ m = mk + 64 * rd;
     const bool last = rd == NR;
     uint32_t np[4][2][8];
@@ -216,11 +224,12 @@ __device__ __forceinline__ void bs16_cipher_tab(uint32_t (&p)[4][2][8],
 // The same for counter blocks whose pair-0 groups are the same in every slot
 // (columns 0 and 2 of J0 ^ rk0): their round-1 SubBytes outputs come in c1
 // (computed once per record), and p's pair 0 is not read.
-template <int NR>
+template <int NR, class Hook = BsNoHook>
 __device__ __forceinline__ void bs16_cipher_ctr(uint32_t (&p)[4][2][8], const uint32_t (&c1)[4][8],
-                                                const uint32_t *__restrict__ mk) {
+                                                const uint32_t *__restrict__ mk,
+                                                const Hook &hook = Hook()) {
   bs16_round_tab<false, true>(p, mk + 64, c1);
-  bs16_rounds_tab<NR, 2>(p, mk);
+  bs16_rounds_tab<NR, 2>(p, mk, hook);
 }
 
 }  // namespace bssl_amd

@@ -1462,6 +1462,8 @@ bool whole_lines(const BatchDesc &b) {
 
 }  // namespace
 
+bool chacha_takes_one_record_kernel(const BatchDesc &b) { return one_record_batch(b); }
+
 int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, bool xchacha,
                   void *stream, const KernelEvents *ev) {
   if (b.num_records == 0) return 0;

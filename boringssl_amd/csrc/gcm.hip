@@ -1152,6 +1152,10 @@ int set_gcm_engine(int engine) {
   return prev;
 }
 
+bool gcm_takes_one_record_kernel(const BatchDesc &b) {
+  return gcm_engine() != kGcmEngineBitsliced && one_record_batch(b);
+}
+
 int launch_gcm(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, void *stream,
                const KernelEvents *ev) {
   if (b.num_records == 0) return 0;

@@ -33,6 +33,11 @@
 //   L-lane XOR, length block, tag, check and zero-fill.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#ifdef BSSL_AMD_BS_PROF
+#include <cstdio>
+#endif
+
 #include "bs16_aes.h"
 #include "gcm_common.h"
 
@@ -49,12 +54,51 @@ constexpr int kBsThreads = 1024;          // 16 waves per CU at 128 VGPRs
 constexpr uint32_t kBsGroupRecs = 1024;   // records per E_K(J0) batch
 constexpr uint32_t kBsLdsBasis = kG8Bytes;  // build_gpow scratch (2 KiB)
 constexpr uint32_t kBsLdsState = kBsLdsBasis + 128 * 16;  // parked unit state (bs_unit)
-constexpr uint32_t kBsLdsBytes = kBsLdsState + 15 * 4 * kBsThreads;
-// Launch control words (zeroed by the launcher): unit counter, then one
-// ready flag per E_K(J0) group.
-constexpr int kCtlFlags = 16;
+// L2 prefetch of a chunk's record bytes at the start of round NR - BS_PF
+// (0: none); the loads land in a scratch line of LDS.
+#ifndef BS_PF
+#define BS_PF 0
+#endif
+constexpr uint32_t kBsLdsSink = kBsLdsState + 16 * 4 * kBsThreads;  // 256 B
+#define BS_PF_LD(n) "global_load_lds_dword %1, off offset:%" #n "\n\t"
+#define BS_PF_ASM                                                                                  \
+  "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t" BS_PF_LD(3) BS_PF_LD(4) BS_PF_LD(5)         \
+      BS_PF_LD(6) BS_PF_LD(7) BS_PF_LD(8) BS_PF_LD(9) BS_PF_LD(10) BS_PF_LD(11) BS_PF_LD(12)       \
+          BS_PF_LD(13) BS_PF_LD(14) BS_PF_LD(15) BS_PF_LD(16) BS_PF_LD(17) BS_PF_LD(18)            \
+              "s_mov_b32 m0, %0"
+#ifdef BSSL_AMD_BS_PROF
+// Diagnostic builds: per-wave phase clocks (s_memtime cycles), summed per
+// launch into g_bs_prof and printed by the launcher.
+constexpr int kBsProfN = 16;
+constexpr uint32_t kBsLdsProf = kBsLdsSink + 256;
+constexpr uint32_t kBsLdsBytes = kBsLdsProf + 8 * kBsProfN * (kBsThreads / 64);
+__device__ unsigned long long g_bs_prof[kBsProfN];
+struct BsClock {
+  uint64_t t = __builtin_amdgcn_s_memtime();
+  __device__ void lap(uint8_t *smem, int k) {
+    const uint64_t n = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) == 0)
+      reinterpret_cast<uint64_t *>(smem + kBsLdsProf)[(threadIdx.x >> 6) * kBsProfN + k] += n - t;
+    t = n;
+  }
+};
+#define BS_LAP(k) clk.lap(smem, k)
+#else
+constexpr uint32_t kBsLdsBytes = kBsLdsSink + 256;
+#define BS_LAP(k) ((void)0)
+#endif
+// Launch control words (zeroed by the launcher): the unit counter.
+// E_K(J0) of processing position i: four data-tagged 8-byte granules {E word
+// k, epoch} at ek0[2i], ek0[2i + 1] (two per 16-byte write-through (sc1)
+// store), read by sc1 loads until all four carry this launch's epoch (a
+// per-launch number): no flag, no ordering, no reliance on a 16-byte store
+// landing whole, and a line left in an XCD's L2 by an earlier launch cannot
+// pass for this one's (MI355X_MICROARCH.md, inter-workgroup visibility:
+// granule hand-off).  (A flag per group written after the values
+// raced on the GPU: a tag mismatch in the ragged parity test.)
 
 typedef uint32_t v32u __attribute__((ext_vector_type(32)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // 0 or 0xffffffff: bit `k` of w.
 __device__ __forceinline__ uint32_t bit_mask(uint32_t w, int k) {
@@ -154,12 +198,11 @@ __device__ __forceinline__ uint4 g8_mul(uint4 x, bool rs1, bool rs2, uint32_t rb
 // takes positions i0 + 16 l + s in its slots s.  KS: records carry their own
 // keys (keysets) -- one cipher per distinct key among a lane's slots, with
 // that key's masks per lane; one-key batches take one cipher with the key's
-// wave-uniform masks.  Results to ek0[i]; then the group's flag is raised
-// (release, agent scope: the consumers read with coherent loads).
+// wave-uniform masks.  Results to the granules of ek0 (above).
 template <int NR, bool KS>
 __device__ __forceinline__ void produce_ek0(const GcmKeyDev *__restrict__ keys, const BatchDesc &b,
                                          uint64_t i0, uint64_t end, uint4 *__restrict__ ek0,
-                                         uint32_t *flag) {
+                                         uint32_t epoch) {
   const int lane = threadIdx.x & 63;
   const uint64_t base = i0 + 16u * (uint64_t)lane;
   uint4 j0[16];
@@ -206,27 +249,52 @@ __device__ __forceinline__ void produce_ek0(const GcmKeyDev *__restrict__ keys, 
     const v32u KA = bs16_words(p, 0), KB = bs16_words(p, 1);
 #pragma unroll
     for (int s = 0; s < 16; s++)
-      if ((mine >> s) & 1u) ek0[base + s] = make_uint4(KA[s], KB[s], KA[16 + s], KB[16 + s]);
+      if ((mine >> s) & 1u) {
+        const u32x4 g0 = {KA[s], epoch, KB[s], epoch}, g1 = {KA[16 + s], epoch, KB[16 + s], epoch};
+        // (s_nop 1: a store of more than 8 bytes reads its data registers a
+        // cycle late, and the compiler's hazard check does not see inside
+        // inline asm -- without it the next VALU write of those registers
+        // went into the granule.)
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\tglobal_store_dwordx4 %0, %2, off offset:16 sc1\n\t"
+                     "s_nop 1"
+                     ::"v"(ek0 + 2 * (base + s)), "v"(g0), "v"(g1)
+                     : "memory");
+      }
     todo &= ~mine;
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  if (lane == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// E_K(J0) of processing position i, once its group's flag is up (coherent
-// loads: the values were written by another wave, maybe on another XCD, and
-// this CU's caches may hold the scratch lines of an earlier launch).
-__device__ __forceinline__ uint4 consume_ek0(const uint4 *ek0, uint32_t *flag, uint64_t i,
-                                             bool active) {
-  if ((threadIdx.x & 63) == 0)
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-      __builtin_amdgcn_s_sleep(4);
-  if (!active) return make_uint4(0, 0, 0, 0);
-  uint32_t *p = reinterpret_cast<uint32_t *>(const_cast<uint4 *>(ek0 + i));
-  return make_uint4(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                    __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                    __hip_atomic_load(p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                    __hip_atomic_load(p + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+// E_K(J0) of processing position i (active lanes): sc1 loads of its two
+// granules until both carry `epoch` (the wave loops until every active lane
+// has its value).  `polls`: the retries.
+__device__ __forceinline__ uint4 load_ek0(const uint4 *ek0, uint64_t i, bool active, uint32_t epoch,
+                                          uint32_t &polls) {
+  u32x4 g0 = {0, 0, 0, 0}, g1 = {0, 0, 0, 0};
+  polls = 0;
+  for (;;) {
+    bool ok = true;
+    if (active) {
+      asm volatile("global_load_dwordx4 %0, %2, off sc1\n\tglobal_load_dwordx4 %1, %2, off offset:16 sc1\n\t"
+                   "s_waitcnt vmcnt(0)"
+                   : "=&v"(g0), "=&v"(g1)
+                   : "v"(ek0 + 2 * i)
+                   : "memory");
+      ok = g0.y == epoch && g0.w == epoch && g1.y == epoch && g1.w == epoch;
+    }
+    if (__ballot(!ok) == 0) break;
+    __builtin_amdgcn_s_sleep(4);
+    polls++;
+  }
+  return make_uint4(g0.x, g0.z, g1.x, g1.z);
+}
+
+// The lane's index in its wave from a volatile asm statement: an opaque value
+// the compiler recomputes at each use instead of keeping it (and everything
+// derived from it) live across the rounds.
+__device__ __forceinline__ uint32_t bs_lane() {
+  uint32_t v;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
+  return v;
 }
 
 // ---------------------------------------------------------------------------
@@ -247,29 +315,63 @@ enum : int {
 };
 
 // The 64 / L records of one unit, L lanes each: the lane's record is at
-// processing position i (`active`: the group has a record in this unit).
+// processing position first + r for r = lane / L (wave-uniform `first`; bit r
+// of the wave-uniform `amask`: the unit has a record there).  The lane's own
+// position and flag are recomputed from the lane index where needed.
 template <int NR, bool OPEN, bool XT, bool IOV, int L>
 __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const BatchDesc &b,
-                                        uint64_t i, bool active, uint8_t *smem,
-                                        const uint4 *ek0, uint32_t *flag) {
+                                        uint64_t first, uint64_t amask, uint8_t *smem,
+                                        const uint4 *ek0, uint32_t epoch) {
   static_assert(L == 16 || L == 8 || L == 4 || L == 2, "lanes per record");
   static_assert(!(IOV && XT), "iovec records carry no extra bytes");
-  const int q = threadIdx.x & (L - 1);
-  // (Inline-asm LDS accesses: the compiler must neither forward the stored
-  // values in registers across the rounds nor turn them into flat accesses.)
-  const uint32_t la =
+#ifdef BSSL_AMD_BS_PROF
+  BsClock clk;
+#endif
+  // Lane-derived values are recomputed where they are used from an opaque
+  // lane index (v_mbcnt in a volatile asm statement): kept live across the
+  // rounds they spilled to scratch, and every chunk paid the scratch round
+  // trips.  The unit state goes through inline-asm LDS accesses (the compiler
+  // must neither forward the stored values in registers across the rounds nor
+  // turn them into flat accesses).  Word k of thread t is at kBsLdsState +
+  // (k / 4) * 16 * kBsThreads + 16 * t + 4 * (k % 4): quads of consecutive
+  // words per lane, read by one ds_read_b128 (16-byte lane stride: no bank
+  // conflicts).
+#if BS_PF > 0
+  const uint32_t lsink =
       (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t *)smem) +
-      kBsLdsState + 4u * threadIdx.x;
-  auto put = [&](int k, uint32_t v) {
-    asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(la), "v"(v), "i"(k * 4 * kBsThreads));
+      kBsLdsSink;
+#endif
+  const uint32_t lbase =
+      (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t *)smem) +
+      kBsLdsState + 16u * 64u * (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  auto addr = [&]() -> uint32_t {
+    uint32_t a;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\t"
+                 "v_lshl_add_u32 %0, %0, 4, %1"
+                 : "=&v"(a)
+                 : "s"(lbase));
+    return a;
   };
   auto get = [&](int k) -> uint32_t {
     uint32_t v;
     asm volatile("ds_read_b32 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
                  : "=v"(v)
-                 : "v"(la), "i"(k * 4 * kBsThreads));
+                 : "v"(addr()), "i"((k >> 2) * 16 * kBsThreads + 4 * (k & 3)));
     return v;
   };
+  auto put4 = [&](int k, uint4 v) {  // words k..k+3 (k % 4 == 0)
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    asm volatile("ds_write_b128 %0, %1 offset:%2\n\ts_nop 1" ::"v"(addr()), "v"(w),
+                 "i"((k >> 2) * 16 * kBsThreads));
+  };
+  auto get4 = [&](int k) -> uint4 {  // words k..k+3 (k % 4 == 0)
+    u32x4 w;
+    asm volatile("ds_read_b128 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(w)
+                 : "v"(addr()), "i"((k >> 2) * 16 * kBsThreads));
+    return make_uint4(w.x, w.y, w.z, w.w);
+  };
+  const int q = (int)(bs_lane() & (L - 1));
   int nchunks;
   // IOV: chunk cursors (as gcm.hip process_records: chunk index + stream
   // start; between chunk boundaries only the running pointers move).
@@ -278,6 +380,9 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
   uint8_t *st_ptr = nullptr;
   int32_t ld_left = -1, st_left = -1;
   {
+    const uint32_t r = bs_lane() / L;
+    const uint64_t i = first + r;
+    const bool active = (amask >> r) & 1u;
     const uint64_t rec = active ? rec_at(b, i) : 0;
     RecordMeta m = {0, 0, 0, 0, 0};
     if (active) m = record_meta(b, rec);
@@ -299,7 +404,7 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
     // (< 2^32: the GCM length limit holds for a live record)
     const uint32_t nb = live ? (uint32_t)((m.len + m.xlen + 15) / 16) : 0u;
     const uint32_t nfull = live && !IOV ? (uint32_t)(m.len / 16) : 0u;
-    nchunks = wave_max((int)((nb + 16 * L - 1) / (16 * L)));
+    nchunks = __builtin_amdgcn_readfirstlane(wave_max((int)((nb + 16 * L - 1) / (16 * L))));
     // Counter-mode caching: the pair-0 groups (columns 0 and 2 of J0 ^ rk0)
     // are the same in every slot of every chunk, so their round-1 SubBytes
     // is done once here.  Each of the 32 output planes is 0 / 0xffff per
@@ -320,38 +425,31 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
           pk[r >> 1] |= ((o[bb] & 1u) << k) | (((o[bb] >> 16) & 1u) << (16 + k));
         }
       }
-      put(kSc0, pk[0]);
-      put(kSc1, pk[1]);
+      put4(kSc0, make_uint4(pk[0], j0.y ^ key->rk_plain[0][1], pk[1],
+                            bswap32(j0.w) + 1u + (uint32_t)q));
     }
-    put(kSw1, j0.y ^ key->rk_plain[0][1]);
-    put(kScb, bswap32(j0.w) + 1u + (uint32_t)q);
-    put(kSnb, nb);
-    put(kSnfull, nfull);
-    put(kSoff, (uint32_t)m.off);
-    put(kSoffHi, (uint32_t)(m.off >> 32));
-    put(kSacc0, acc.x);
-    put(kSacc1, acc.y);
-    put(kSacc2, acc.z);
-    put(kSacc3, acc.w);
-    put(kSflags, (active ? 1u : 0u) | (live ? 2u : 0u));
-    put(kSrec, (uint32_t)rec);
-    put(kSrecHi, (uint32_t)(rec >> 32));
+    put4(kSnb, make_uint4(nb, nfull, (uint32_t)m.off, (uint32_t)(m.off >> 32)));
+    put4(kSacc0, acc);
+    put4(kSflags, make_uint4((active ? 1u : 0u) | (live ? 2u : 0u), (uint32_t)rec,
+                             (uint32_t)(rec >> 32), 0u));
     if constexpr (IOV) {
       if (live) ld_c = st_c = b.iovec_start[rec];
     }
   }
   const uint32_t *__restrict__ mk = &key->bsmask[0][0];
+  BS_LAP(0);
 #pragma unroll 1
   for (int c = 0; c < nchunks; c++) {
     uint32_t p[4][2][8];
+    const uint4 st = get4(kSc0);  // round-1 cache words, w1, counter base
     {
       // Round 0.  Pair 0 = columns 0 and 2 of J0 ^ rk0 (the same in every
       // slot: 0 / 0xffff per half); pair 1 = column 1 (low half, constant)
       // and the counter words of column 3 (high half), out of one transpose:
       // t[n] = column 1, t[16 + n] = word 3 of slot n.
-      const uint32_t w1 = get(kSw1);
+      const uint32_t w1 = st.y;
       const uint32_t rk3 = key->rk_plain[0][3];
-      const uint32_t cb = get(kScb) + (uint32_t)(16 * L) * (uint32_t)c;  // inc32: mod 2^32
+      const uint32_t cb = st.w + (uint32_t)(16 * L) * (uint32_t)c;  // inc32: mod 2^32
       uint32_t t[32];
 #pragma unroll
       for (int n = 0; n < 16; n++) {
@@ -367,7 +465,7 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
       // packed word W is W << (15 - k) with each 16-bit half shifted right
       // arithmetically by 15 (v_pk_ashrrev_i16).
       typedef short s16x2 __attribute__((ext_vector_type(2)));
-      const uint32_t pk[2] = {get(kSc0), get(kSc1)};
+      const uint32_t pk[2] = {st.x, st.z};
       uint32_t c1[4][8];
 #pragma unroll
       for (int r = 0; r < 4; r++)
@@ -378,8 +476,34 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
           v = v >> (short)15;
           c1[r][bb] = __builtin_bit_cast(uint32_t, v);
         }
+#if BS_PF > 0
+      // Prefetch of the chunk's record bytes into L2 a few rounds before the
+      // output pass reads them (LDS-DMA dword loads into a shared scratch line
+      // of LDS: no VGPR destination, nothing waits for them; the output pass's
+      // counted waits only get stricter): full chunks only, so every address is
+      // inside the lane's record.
+      auto pf = [&](int rd) {
+        if (rd != NR - BS_PF) return;
+        const uint4 rs = get4(kSnb);
+        const uint32_t jc = (uint32_t)(16 * L) * (uint32_t)c + (bs_lane() & (L - 1));
+        if (jc + (uint32_t)(16 * L) * 15u < rs.y) {
+          const uint8_t *s0 = b.in + ((uint64_t)rs.z | ((uint64_t)rs.w << 32)) + (uint64_t)jc * 16;
+          uint32_t keep;
+          asm volatile(BS_PF_ASM
+                       : "=&s"(keep)
+                       : "v"(s0), "s"(lsink), "i"(0), "i"(16 * L), "i"(32 * L), "i"(48 * L),
+                         "i"(64 * L), "i"(80 * L), "i"(96 * L), "i"(112 * L), "i"(128 * L),
+                         "i"(144 * L), "i"(160 * L), "i"(176 * L), "i"(192 * L), "i"(208 * L),
+                         "i"(224 * L), "i"(240 * L)
+                       : "memory");
+        }
+      };
+      bs16_cipher_ctr<NR>(p, c1, mk, pf);
+#else
       bs16_cipher_ctr<NR>(p, c1, mk);
+#endif
     }
+    BS_LAP(1);
     // Pass 1 (memory): out = in ^ keystream for the lane's full blocks, the
     // plaintext loads running kAhead slots ahead (slot n of the lane is 16*L*n
     // bytes past slot 0: immediate offsets); the hashed block (the ciphertext:
@@ -412,9 +536,11 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    const uint32_t jc = (uint32_t)(16 * L) * (uint32_t)c + (uint32_t)q;
-    const uint32_t nb = get(kSnb), nfull = get(kSnfull);
-    const uint64_t off = (uint64_t)get(kSoff) | ((uint64_t)get(kSoffHi) << 32);
+    BS_LAP(2);
+    const uint32_t jc = (uint32_t)(16 * L) * (uint32_t)c + (bs_lane() & (L - 1));
+    const uint4 rs = get4(kSnb);
+    const uint32_t nb = rs.x, nfull = rs.y;
+    const uint64_t off = (uint64_t)rs.z | ((uint64_t)rs.w << 32);
     const uint8_t *src = b.in + off;
     uint8_t *dst = b.out + off;
     const uint8_t *s0 = src + (uint64_t)jc * 16;
@@ -428,7 +554,7 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
     // record's partial last block or extra bytes: slot tl) gets its keystream
     // kept in kt and is sealed after the pass.
     if constexpr (!IOV) {
-      const int gq = threadIdx.x & 15;
+      const int gq = (int)(bs_lane() & 15);
       uint32_t P[4];
 #pragma unroll
       for (int k = 0; k < 4; k++) {
@@ -439,7 +565,8 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
       }
       const int nv = jc < nfull ? (int)min((nfull - jc + L - 1) / L, 16u) : 0;
       const int tl = (nv < 16 && jc + (uint32_t)L * (uint32_t)nv < nb) ? nv : -1;
-      uint32_t accv[4] = {get(kSacc0), get(kSacc1), get(kSacc2), get(kSacc3)};
+      const uint4 av = get4(kSacc0);
+      uint32_t accv[4] = {av.x, av.y, av.z, av.w};
       uint32_t kt[4] = {0, 0, 0, 0};
       // (rs1 / rs2 of g8_rotate as lane masks: bits 2 and 3 of the lane's
       // index in its 16-lane row)
@@ -477,6 +604,7 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
         else { if constexpr (OPEN) BS_IO(open_L2); else BS_IO(seal_L2); }
       }
 #undef BS_IO
+      BS_LAP(3);
       if (tl >= 0) {
         const uint32_t jt = jc + (uint32_t)L * (uint32_t)tl;
         const uint64_t rec = (uint64_t)get(kSrec) | ((uint64_t)get(kSrecHi) << 32);
@@ -501,10 +629,8 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
         accv[2] = hm.z ^ c.z;
         accv[3] = hm.w ^ c.w;
       }
-      put(kSacc0, accv[0]);
-      put(kSacc1, accv[1]);
-      put(kSacc2, accv[2]);
-      put(kSacc3, accv[3]);
+      put4(kSacc0, make_uint4(accv[0], accv[1], accv[2], accv[3]));
+      BS_LAP(4);
       continue;
     }
     constexpr int kAhead = 4;
@@ -603,7 +729,7 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
     // lookups into pass 1, whose registers they would need.)
 #pragma unroll
     for (int k = 0; k < 32; k++) asm volatile("" : "+v"(KA[k]), "+v"(KB[k]));
-    const int gq = threadIdx.x & 15;  // (GHASH lane constants, gcm_common.h Gh8)
+    const int gq = (int)(bs_lane() & 15);  // (GHASH lane constants, gcm_common.h Gh8)
     const bool rs1 = (gq >> 2) & 1, rs2 = (gq >> 3) & 1;
     const uint32_t rbs = (uint32_t)gq & 3u;
     uint32_t P[4];
@@ -614,7 +740,7 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
       for (int e = 0; e < 4; e++) v |= (((4u * k + e + gq) & 15u) << 4) << (8 * e);
       P[k] = v;
     }
-    uint4 acc = make_uint4(get(kSacc0), get(kSacc1), get(kSacc2), get(kSacc3));
+    uint4 acc = get4(kSacc0);
 #pragma unroll
     for (int n = 0; n < 16; n++) {
       const uint4 hm = g8_mul(acc, rs1, rs2, rbs, P, smem);
@@ -640,22 +766,37 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
         acc = xor4(hm, OPEN ? x : y);
       }
     }
-    put(kSacc0, acc.x);
-    put(kSacc1, acc.y);
-    put(kSacc2, acc.z);
-    put(kSacc3, acc.w);
+    put4(kSacc0, acc);
   }
   // Record end.
-  const uint32_t fl = get(kSflags);
+  const uint4 rq = get4(kSflags);
+  const uint32_t fl = rq.x;
   const bool act = fl & 1u, live = (fl >> 1) & 1u;
-  const uint64_t rec = (uint64_t)get(kSrec) | ((uint64_t)get(kSrecHi) << 32);
+  const uint64_t rec = (uint64_t)rq.y | ((uint64_t)rq.z << 32);
   RecordMeta m = {0, 0, 0, 0, 0};
   if (act) m = record_meta(b, rec);
   if constexpr (!XT) m.xlen = 0;
   const uint32_t nb = get(kSnb);
-  const uint4 acc = make_uint4(get(kSacc0), get(kSacc1), get(kSacc2), get(kSacc3));
-  const uint4 e0 = consume_ek0(ek0, flag, i, act);
+  const uint4 acc = get4(kSacc0);
+  BS_LAP(5);
+  uint32_t polls;
+  // (Live records only: the producer skips the others, whose output
+  // finish_record zero-fills.)
+  const uint4 e0 = load_ek0(ek0, first + bs_lane() / L, act && live, epoch, polls);
+  BS_LAP(8);
+#ifdef BSSL_AMD_BS_PROF
+  if ((threadIdx.x & 63) == 0) {
+    uint64_t *w = reinterpret_cast<uint64_t *>(smem + kBsLdsProf) + (threadIdx.x >> 6) * kBsProfN;
+    w[10] += polls;
+    w[11] += 1;
+    if (polls) w[15] += 1;
+  }
+#else
+  (void)polls;
+#endif
+  BS_LAP(9);
   finish_record<OPEN, L>(acc, nb, m, e0, b, rec, act, live, b.out + m.off, key->hpow_ct);
+  BS_LAP(6);
 }
 
 // One-key bulk kernel: one workgroup of 16 waves per CU; each wave takes the
@@ -665,9 +806,14 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
 template <int NR, bool OPEN, bool XT, bool IOV, int L>
 __global__ __launch_bounds__(kBsThreads) void gcm_bs_kernel(const GcmKeyDev *__restrict__ keys,
                                                              BatchDesc b, uint32_t *__restrict__ ctl,
-                                                             uint4 *__restrict__ ek0) {
+                                                             uint4 *__restrict__ ek0,
+                                                             uint32_t epoch) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[kBsLdsBytes];
   const int tid = threadIdx.x, lane = tid & 63;
+#ifdef BSSL_AMD_BS_PROF
+  if (lane < kBsProfN) reinterpret_cast<uint64_t *>(smem + kBsLdsProf)[(tid >> 6) * kBsProfN + lane] = 0;
+  uint64_t t_prod = 0;
+#endif
   if constexpr (L == 16)
     build_g8<kBsThreads>(smem, reinterpret_cast<const uint4 *>(keys[0].htab16), tid);
   else
@@ -680,23 +826,39 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_kernel(const GcmKeyDev *__r
   uint64_t lo = 0, n = b.num_records;
   if (b.split_lo) lo = *b.split_lo;
   if (b.split_hi) n = *b.split_hi;
-  uint32_t *flags = ctl + kCtlFlags;
   for (;;) {
     uint32_t u = 0;
     if (lane == 0) u = atomicAdd(ctl, 1u);
     u = __builtin_amdgcn_readfirstlane(u);
     const uint64_t first = lo + (uint64_t)u * kRec;
     if (first >= n) break;
-    // Producer units: 0 for group 0, the middle unit of group g for g + 1.
+    // Producer units: unit 0 for groups 0 and 1, the middle unit of group g
+    // for g + 2 (one group ahead, a tenth of the units waited ~90 us for
+    // their group's values at the record end).
     const uint32_t g = u / kGroupUnits;
-    uint32_t pg = 0xffffffffu;
-    if (u == 0) pg = 0;
-    if (u % kGroupUnits == kGroupUnits / 2 && lo + (uint64_t)(g + 1) * kBsGroupRecs < n) pg = g + 1;
-    if (pg != 0xffffffffu)
-      produce_ek0<NR, false>(keys, b, lo + (uint64_t)pg * kBsGroupRecs, n, ek0, flags + pg);
-    const uint64_t i = first + (uint64_t)(lane / L);
-    bs_unit<NR, OPEN, XT, IOV, L>(keys, b, i, i < n, smem, ek0, flags + g);
+    uint32_t pg0 = 1, pg1 = 0;  // groups [pg0, pg1)
+    if (u == 0) pg0 = 0, pg1 = 2;
+    if (u % kGroupUnits == kGroupUnits / 2) pg0 = g + 2, pg1 = g + 3;
+    for (uint32_t pg = pg0; pg < pg1 && lo + (uint64_t)pg * kBsGroupRecs < n; pg++) {
+#ifdef BSSL_AMD_BS_PROF
+      const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
+      produce_ek0<NR, false>(keys, b, lo + (uint64_t)pg * kBsGroupRecs, n, ek0, epoch);
+#ifdef BSSL_AMD_BS_PROF
+      t_prod += __builtin_amdgcn_s_memtime() - t0;
+#endif
+    }
+    const uint64_t amask = n - first >= kRec ? (kRec == 64 ? ~0ull : (1ull << kRec) - 1)
+                                             : (1ull << (n - first)) - 1;
+    bs_unit<NR, OPEN, XT, IOV, L>(keys, b, first, amask, smem, ek0, epoch);
   }
+#ifdef BSSL_AMD_BS_PROF
+  if (lane == 0) {
+    uint64_t *w = reinterpret_cast<uint64_t *>(smem + kBsLdsProf) + (tid >> 6) * kBsProfN;
+    w[7] = t_prod;
+    for (int k = 0; k < kBsProfN; k++) atomicAdd(&g_bs_prof[k], (unsigned long long)w[k]);
+  }
+#endif
 }
 
 // Keyset batches (key_index per record): records in tiles of 16 units; a
@@ -707,15 +869,14 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_kernel(const GcmKeyDev *__r
 template <int NR, bool OPEN, bool XT>
 __global__ __launch_bounds__(kBsThreads) void gcm_bs_keyset_kernel(
     const GcmKeyDev *__restrict__ keys, BatchDesc b, uint32_t *__restrict__ ctl,
-    uint4 *__restrict__ ek0) {
+    uint4 *__restrict__ ek0, uint32_t epoch) {
   constexpr int kRecPerTile = 16 * 4;
   __shared__ __attribute__((aligned(16))) uint8_t smem[kBsLdsBytes + 64 * 16 + 16];
   uint32_t *s_pass_key = reinterpret_cast<uint32_t *>(smem + kBsLdsBytes);
   uint64_t *s_pass_mask = reinterpret_cast<uint64_t *>(smem + kBsLdsBytes + 64 * 4);
   int *s_npass = reinterpret_cast<int *>(smem + kBsLdsBytes + 64 * 12);
   uint64_t *s_base = reinterpret_cast<uint64_t *>(smem + kBsLdsBytes + 64 * 12 + 8);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g4 = lane >> 4;
-  uint32_t *flags = ctl + kCtlFlags;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint32_t loaded = 0xffffffffu;
   const uint64_t n = b.num_records;
   for (;;) {
@@ -745,15 +906,16 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_keyset_kernel(
         *s_npass = base < n ? np : -1;
         *s_base = base;
       }
-      // Group producer: tile 0 for group 0, the middle tile of group g for g + 1.
+      // Group producers: tile 0 for groups 0 and 1, the middle tile of
+      // group g for g + 2 (as the one-key kernel).
       if (base < n) {
         constexpr uint32_t kGroupTiles = kBsGroupRecs / kRecPerTile;
         const uint32_t g = t / kGroupTiles;
-        uint32_t pg = 0xffffffffu;
-        if (t == 0) pg = 0;
-        if (t % kGroupTiles == kGroupTiles / 2 && (uint64_t)(g + 1) * kBsGroupRecs < n) pg = g + 1;
-        if (pg != 0xffffffffu)
-          produce_ek0<NR, true>(keys, b, (uint64_t)pg * kBsGroupRecs, n, ek0, flags + pg);
+        uint32_t pg0 = 1, pg1 = 0;
+        if (t == 0) pg0 = 0, pg1 = 2;
+        if (t % kGroupTiles == kGroupTiles / 2) pg0 = g + 2, pg1 = g + 3;
+        for (uint32_t pg = pg0; pg < pg1 && (uint64_t)pg * kBsGroupRecs < n; pg++)
+          produce_ek0<NR, true>(keys, b, (uint64_t)pg * kBsGroupRecs, n, ek0, epoch);
       }
     }
     __syncthreads();
@@ -769,10 +931,8 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_keyset_kernel(
         __syncthreads();
         loaded = k;
       }
-      const int t = wave * 4 + g4;
-      const bool act = (mask >> t) & 1;
-      bs_unit<NR, OPEN, XT, false, 16>(keys + k, b, base + t, act, smem, ek0,
-                                       flags + (uint32_t)(base / kBsGroupRecs));
+      bs_unit<NR, OPEN, XT, false, 16>(keys + k, b, base + 4 * wave, (mask >> (4 * wave)) & 15u,
+                                       smem, ek0, epoch);
     }
   }
 }
@@ -792,12 +952,15 @@ int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, 
   const int num_cus = device_cu_count();
   if (!num_cus) return 1;
   const uint64_t n = b.num_records;
-  const uint64_t groups = (n + kBsGroupRecs - 1) / kBsGroupRecs;
-  // Two control blocks (one per launch of a split batch): unit counter and
-  // E_K(J0) group flags, zeroed; then E_K(J0) of every processing position.
-  const size_t ctl_bytes = ((kCtlFlags + groups + 1) * 4 + 255) & ~size_t(255);
+  // Two control blocks (one per launch of a split batch): the unit counters,
+  // zeroed; then the E_K(J0) granules of every processing position (not
+  // cleared: they carry the launch's epoch, never 0).
+  static std::atomic<uint32_t> s_epoch{0};
+  uint32_t epoch = s_epoch.fetch_add(1, std::memory_order_relaxed) + 1;
+  if (!epoch) epoch = s_epoch.fetch_add(1, std::memory_order_relaxed) + 1;
+  const size_t ctl_bytes = 256;
   uint8_t *scratch = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void **>(&scratch), 2 * ctl_bytes + n * 16, s) != hipSuccess)
+  if (hipMallocAsync(reinterpret_cast<void **>(&scratch), 2 * ctl_bytes + n * 32, s) != hipSuccess)
     return 2;
   uint32_t *ctl = reinterpret_cast<uint32_t *>(scratch);
   uint32_t *ctl2 = reinterpret_cast<uint32_t *>(scratch + ctl_bytes);
@@ -825,7 +988,7 @@ int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, 
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
   const unsigned grid = (unsigned)((n + 3) / 4 < (uint64_t)num_cus ? (n + 3) / 4 : (uint64_t)num_cus);
   auto go = [&](auto kern, const BatchDesc &d, uint32_t *c) {
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBsThreads), 0, s, keys, d, c, ek0);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBsThreads), 0, s, keys, d, c, ek0, epoch);
   };
   // Length classes (one-key, not iovec): short uniform records take L = 2;
   // a ragged batch in length order splits at 4 KiB.
@@ -874,6 +1037,21 @@ int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, 
 #undef BSSL_BS_ONEKEY
   const int rc = (int)hipGetLastError();
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->stop), s);
+#ifdef BSSL_AMD_BS_PROF
+  {
+    unsigned long long h[kBsProfN];
+    hipStreamSynchronize(s);
+    hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bs_prof), sizeof(h));
+    const unsigned long long z[kBsProfN] = {};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_bs_prof), z, sizeof(z));
+    fprintf(stderr,
+            "bs_prof n=%llu start %llu rounds %llu transp %llu out %llu tail %llu endmeta %llu "
+            "finish %llu produce %llu flagwait %llu ek0load %llu polls %llu units %llu "
+            "late_rt %llu late_units %llu vis_rt %llu polled_units %llu\n",
+            (unsigned long long)n, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9],
+            h[10], h[11], h[12], h[13], h[14], h[15]);
+  }
+#endif
   if (order) hipFreeAsync(order, s);
   hipFreeAsync(scratch, s);
   return rc;

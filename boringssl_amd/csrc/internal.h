@@ -198,6 +198,10 @@ int launch_gcm_siv(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr,
 // xchacha: XChaCha20-Poly1305 (24-byte nonces, per-record HChaCha20 subkey).
 int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, bool xchacha,
                   void *stream, const KernelEvents *ev);
+// Whether launch_gcm / launch_chacha would run this batch on a one-record
+// kernel, the only kernels that write the completion word BatchDesc::done.
+bool gcm_takes_one_record_kernel(const BatchDesc &b);
+bool chacha_takes_one_record_kernel(const BatchDesc &b);
 // tls12 / tls13 nonce checks over a batch of seal calls (tls_scan.hip):
 // writes valid[i] (device) and advances the context's nonce state in place
 // (min_next_nonce, mask); synchronises `stream`.  and_into: valid[i] &= the
@@ -268,9 +272,14 @@ inline int device_cu_count() {
 // Wipes key material that goes out of scope (reference: OPENSSL_cleanse).
 void secure_zero(void *p, size_t n);
 
-// Host-side key setup (key_setup.cc).
+// Key setup (key_setup.cc, key_sched.h): one key on the host, or n keys by
+// the device kernel into device memory (synchronous on `s`; 0 or an error).
 bool gcm_key_setup(const uint8_t *key, size_t key_len, GcmKeyDev *out);
+int gcm_key_setup_device(const uint8_t *keys, size_t key_len, size_t n, GcmKeyDev *out,
+                         hipStream_t s);
 void chacha_key_setup(const uint8_t *key, ChaChaKeyDev *out);
+// Key counts from which make_keys builds AES-GCM tables on the device.
+constexpr size_t kDeviceKeySetupMin = 64;
 
 }  // namespace bssl_amd
 
