@@ -52,6 +52,10 @@ namespace {
 
 constexpr int kBsThreads = 1024;          // 16 waves per CU at 128 VGPRs
 constexpr uint32_t kBsGroupRecs = 1024;   // records per E_K(J0) batch
+#ifndef BS_AHEAD
+#define BS_AHEAD 4
+#endif
+constexpr uint32_t kBsAhead = BS_AHEAD;    // E_K(J0) groups produced ahead (bs_kernel)
 constexpr uint32_t kBsLdsBasis = kG8Bytes;  // build_gpow scratch (2 KiB)
 constexpr uint32_t kBsLdsState = kBsLdsBasis + 128 * 16;  // parked unit state (bs_unit)
 // L2 prefetch of a chunk's record bytes at the start of round NR - BS_PF
@@ -789,7 +793,13 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
     uint64_t *w = reinterpret_cast<uint64_t *>(smem + kBsLdsProf) + (threadIdx.x >> 6) * kBsProfN;
     w[10] += polls;
     w[11] += 1;
-    if (polls) w[15] += 1;
+    if (polls) {
+      w[15] += 1;
+      // where the waiting units are: position in the batch (first 16 groups,
+      // last 16 groups, the rest) -- diagnostic buckets in slots 12..14
+      const uint64_t gi = first / kBsGroupRecs, ng = (b.num_records + kBsGroupRecs - 1) / kBsGroupRecs;
+      w[gi < 16 ? 12 : gi + 16 >= ng ? 13 : 14] += 1;
+    }
   }
 #else
   (void)polls;
@@ -832,14 +842,15 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_kernel(const GcmKeyDev *__r
     u = __builtin_amdgcn_readfirstlane(u);
     const uint64_t first = lo + (uint64_t)u * kRec;
     if (first >= n) break;
-    // Producer units: unit 0 for groups 0 and 1, the middle unit of group g
-    // for g + 2 (one group ahead, a tenth of the units waited ~90 us for
-    // their group's values at the record end).
+    // Producer units: unit u < kBsAhead for group u (in parallel at the
+    // start), the middle unit of group g for g + kBsAhead (with the producer
+    // half a group ahead, a tenth of the units waited ~90 us for their
+    // group's values at the record end).
     const uint32_t g = u / kGroupUnits;
-    uint32_t pg0 = 1, pg1 = 0;  // groups [pg0, pg1)
-    if (u == 0) pg0 = 0, pg1 = 2;
-    if (u % kGroupUnits == kGroupUnits / 2) pg0 = g + 2, pg1 = g + 3;
-    for (uint32_t pg = pg0; pg < pg1 && lo + (uint64_t)pg * kBsGroupRecs < n; pg++) {
+    uint32_t pg = 0xffffffffu;
+    if (u < kBsAhead && u < kGroupUnits / 2) pg = u;
+    if (u % kGroupUnits == kGroupUnits / 2) pg = g + kBsAhead;
+    if (pg != 0xffffffffu && lo + (uint64_t)pg * kBsGroupRecs < n) {
 #ifdef BSSL_AMD_BS_PROF
       const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -906,15 +917,15 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_keyset_kernel(
         *s_npass = base < n ? np : -1;
         *s_base = base;
       }
-      // Group producers: tile 0 for groups 0 and 1, the middle tile of
-      // group g for g + 2 (as the one-key kernel).
+      // Group producers: tile t < kBsAhead for group t, the middle tile of
+      // group g for g + kBsAhead (as the one-key kernel).
       if (base < n) {
         constexpr uint32_t kGroupTiles = kBsGroupRecs / kRecPerTile;
         const uint32_t g = t / kGroupTiles;
-        uint32_t pg0 = 1, pg1 = 0;
-        if (t == 0) pg0 = 0, pg1 = 2;
-        if (t % kGroupTiles == kGroupTiles / 2) pg0 = g + 2, pg1 = g + 3;
-        for (uint32_t pg = pg0; pg < pg1 && (uint64_t)pg * kBsGroupRecs < n; pg++)
+        uint32_t pg = 0xffffffffu;
+        if (t < kBsAhead && t < kGroupTiles / 2) pg = t;
+        if (t % kGroupTiles == kGroupTiles / 2) pg = g + kBsAhead;
+        if (pg != 0xffffffffu && (uint64_t)pg * kBsGroupRecs < n)
           produce_ek0<NR, true>(keys, b, (uint64_t)pg * kBsGroupRecs, n, ek0, epoch);
       }
     }
@@ -1047,7 +1058,7 @@ int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, 
     fprintf(stderr,
             "bs_prof n=%llu start %llu rounds %llu transp %llu out %llu tail %llu endmeta %llu "
             "finish %llu produce %llu flagwait %llu ek0load %llu polls %llu units %llu "
-            "late_rt %llu late_units %llu vis_rt %llu polled_units %llu\n",
+            "polled_first16 %llu polled_last16 %llu polled_mid %llu polled_units %llu\n",
             (unsigned long long)n, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9],
             h[10], h[11], h[12], h[13], h[14], h[15]);
   }
