@@ -403,6 +403,15 @@ def load_profile(config, kernel_prefix):
                 cb = {x: round(v[x], 3) for x in ("lds_busy", "valu_busy") if x in v}
                 if cb:
                     cb["source"] = f"profiles/traffic.json[{config}] (rocprofv3 PMC)"
+                # HBM bytes: FETCH_SIZE / WRITE_SIZE scaled by the calibration
+                # copy of the kernel's record access pattern when the profile
+                # has one (tools/micro/calib_copy), else the guide's x2 rule.
+                if v.get("hbm_bytes_calibrated"):
+                    if cb:
+                        cb["traffic_rule"] = f"calibrated ({v.get('calib_pattern', '?')})"
+                    return v["hbm_bytes_calibrated"], cb or None
+                if cb:
+                    cb["traffic_rule"] = "FETCH_SIZE x2 (guide)"
                 return v.get("hbm_bytes_per_launch"), cb or None
     except Exception:
         return None, None

@@ -77,6 +77,10 @@ constexpr int kBsProfN = 16;
 constexpr uint32_t kBsLdsProf = kBsLdsSink + 256;
 constexpr uint32_t kBsLdsBytes = kBsLdsProf + 8 * kBsProfN * (kBsThreads / 64);
 __device__ unsigned long long g_bs_prof[kBsProfN];
+// Per group (first 4096 of a launch): realtime of production start / end, of
+// the first consumer's arrival at its record end, and of the claim of the
+// group's first unit.
+__device__ unsigned long long g_bs_grp[4096][4];
 struct BsClock {
   uint64_t t = __builtin_amdgcn_s_memtime();
   __device__ void lap(uint8_t *smem, int k) {
@@ -209,6 +213,11 @@ __device__ __forceinline__ void produce_ek0(const GcmKeyDev *__restrict__ keys, 
                                          uint32_t epoch) {
   const int lane = threadIdx.x & 63;
   const uint64_t base = i0 + 16u * (uint64_t)lane;
+  // Top priority while producing: a group's consumers wait for it, and at
+  // the kernel's start ~20 productions run beside every wave's first record
+  // start (at priority 0 they took 300-470 us there and the first consumers
+  // arrived at ~230 us: ~7 % of the groups late by 160 us on average).
+  __builtin_amdgcn_s_setprio(3);
   uint4 j0[16];
   uint32_t kidx[16];
   uint32_t todo = 0;
@@ -266,6 +275,7 @@ __device__ __forceinline__ void produce_ek0(const GcmKeyDev *__restrict__ keys, 
       }
     todo &= ~mine;
   }
+  __builtin_amdgcn_s_setprio(0);
 }
 
 // E_K(J0) of processing position i (active lanes): sc1 loads of its two
@@ -783,6 +793,10 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
   const uint32_t nb = get(kSnb);
   const uint4 acc = get4(kSacc0);
   BS_LAP(5);
+#ifdef BSSL_AMD_BS_PROF
+  if ((threadIdx.x & 63) == 0 && first / kBsGroupRecs < 4096)
+    atomicMin(&g_bs_grp[first / kBsGroupRecs][2], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
   uint32_t polls;
   // (Live records only: the producer skips the others, whose output
   // finish_record zero-fills.)
@@ -853,14 +867,22 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_kernel(const GcmKeyDev *__r
     if (pg != 0xffffffffu && lo + (uint64_t)pg * kBsGroupRecs < n) {
 #ifdef BSSL_AMD_BS_PROF
       const uint64_t t0 = __builtin_amdgcn_s_memtime();
+      const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
 #endif
       produce_ek0<NR, false>(keys, b, lo + (uint64_t)pg * kBsGroupRecs, n, ek0, epoch);
 #ifdef BSSL_AMD_BS_PROF
       t_prod += __builtin_amdgcn_s_memtime() - t0;
+      if (lane == 0 && pg < 4096) {
+        g_bs_grp[pg][0] = r0;
+        g_bs_grp[pg][1] = __builtin_amdgcn_s_memrealtime();
+      }
 #endif
     }
     const uint64_t amask = n - first >= kRec ? (kRec == 64 ? ~0ull : (1ull << kRec) - 1)
                                              : (1ull << (n - first)) - 1;
+#ifdef BSSL_AMD_BS_PROF
+    if (lane == 0 && u % kGroupUnits == 0 && g < 4096) g_bs_grp[g][3] = __builtin_amdgcn_s_memrealtime();
+#endif
     bs_unit<NR, OPEN, XT, IOV, L>(keys, b, first, amask, smem, ek0, epoch);
   }
 #ifdef BSSL_AMD_BS_PROF
@@ -1055,6 +1077,33 @@ int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, 
     hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bs_prof), sizeof(h));
     const unsigned long long z[kBsProfN] = {};
     hipMemcpyToSymbol(HIP_SYMBOL(g_bs_prof), z, sizeof(z));
+    static unsigned long long gr[4096][4];
+    hipMemcpyFromSymbol(gr, HIP_SYMBOL(g_bs_grp), sizeof(gr));
+    const uint64_t ng = (n + kBsGroupRecs - 1) / kBsGroupRecs < 4096 ? (n + kBsGroupRecs - 1) / kBsGroupRecs : 4096;
+    uint64_t late = 0, late_sum = 0, prod_sum = 0, lead_sum = 0, maxlate = 0, nprod = 0;
+    for (uint64_t g = 0; g < ng; g++) {
+      if (!gr[g][1] || gr[g][2] == ~0ull) continue;
+      nprod++;
+      prod_sum += gr[g][1] - gr[g][0];
+      lead_sum += gr[g][3] > gr[g][0] ? gr[g][3] - gr[g][0] : 0;
+      if (gr[g][2] < gr[g][1]) {
+        late++;
+        late_sum += gr[g][1] - gr[g][2];
+        if (gr[g][1] - gr[g][2] > maxlate) maxlate = gr[g][1] - gr[g][2];
+      }
+    }
+    fprintf(stderr, "bs_grp groups %llu late %llu late_avg_us %.1f late_max_us %.1f prod_avg_us %.1f "
+            "claim_after_prod_start_avg_us %.1f\n", (unsigned long long)nprod, (unsigned long long)late,
+            late ? late_sum / 100.0 / late : 0.0, maxlate / 100.0, nprod ? prod_sum / 100.0 / nprod : 0.0,
+            nprod ? lead_sum / 100.0 / nprod : 0.0);
+    for (uint64_t g = 0; g < ng && g < 48; g++)
+      if (gr[g][1] && gr[g][2] != ~0ull && gr[g][2] < gr[g][1])
+        fprintf(stderr, "bs_grp late g=%llu prod %.1f..%.1f us, first arrival %.1f, first claim %.1f\n",
+                (unsigned long long)g, (gr[g][0] - gr[0][3]) / 100.0, (gr[g][1] - gr[0][3]) / 100.0,
+                (gr[g][2] - gr[0][3]) / 100.0, (gr[g][3] - gr[0][3]) / 100.0);
+    static unsigned long long init[4096][4];
+    for (auto &row : init) row[0] = row[1] = row[3] = 0, row[2] = ~0ull;
+    hipMemcpyToSymbol(HIP_SYMBOL(g_bs_grp), init, sizeof(init));
     fprintf(stderr,
             "bs_prof n=%llu start %llu rounds %llu transp %llu out %llu tail %llu endmeta %llu "
             "finish %llu produce %llu flagwait %llu ek0load %llu polls %llu units %llu "

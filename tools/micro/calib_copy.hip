@@ -12,6 +12,9 @@
 //                  per record)
 //   copy_gcm     : gcm.hip's pattern: 16 lanes per record, lane q moves
 //                  16-byte block 16*it+q (256 contiguous bytes per record)
+//   copy_gcm8    : the same at 8 lanes per record (128-byte runs: the
+//                  T-table kernel's L = 8 of configs 2 and 4)
+//   (copy_quad is the L = 4 pattern: 64-byte runs, config G)
 // Known bytes per launch: read = write = records * 1350 (+ tags written).
 // Build: hipcc --offload-arch=gfx950 -O3 -o calib_copy calib_copy.hip
 #include <hip/hip_runtime.h>
@@ -73,14 +76,15 @@ __global__ __launch_bounds__(256) void copy_rec4(const uint8_t *s, uint8_t *d, u
   if (q == 0) reinterpret_cast<uint4 *>(tags)[rec] = make_uint4(rec, 1, 2, 3);
 }
 
+template <int LN>  // lanes per record
 __global__ __launch_bounds__(256) void copy_gcm(const uint8_t *s, uint8_t *d, uint8_t *tags) {
-  const uint64_t rec = (blockIdx.x * 256ull + threadIdx.x) / 16;
-  const int q = threadIdx.x & 15;
+  const uint64_t rec = (blockIdx.x * 256ull + threadIdx.x) / LN;
+  const int q = threadIdx.x & (LN - 1);
   if (rec >= kRecs) return;
   const uint8_t *sp = s + rec * kStride;
   uint8_t *dp = d + rec * kStride;
   constexpr uint32_t kFull = kLen / 16;  // 84 full 16-byte blocks
-  for (uint32_t j = q; j <= kFull; j += 16) {
+  for (uint32_t j = q; j <= kFull; j += LN) {
     if (j < kFull) reinterpret_cast<uint4 *>(dp)[j] = reinterpret_cast<const uint4 *>(sp)[j];
     else copy_tail(sp + 16 * j, dp + 16 * j, kLen - 16 * kFull);
   }
@@ -99,15 +103,16 @@ int main(int argc, char **argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const char *names[4] = {"copy_stream", "copy_chacha", "copy_quad", "copy_gcm"};
-  for (int v = 0; v < 4; v++) {
+  const char *names[5] = {"copy_stream", "copy_chacha", "copy_quad", "copy_gcm", "copy_gcm8"};
+  for (int v = 0; v < 5; v++) {
     float best = 1e30f;
     for (int r = 0; r < reps; r++) {
       CK(hipEventRecord(e0));
       if (v == 0) copy_stream<<<8192, 256>>>((const uint4 *)s, (uint4 *)d, bytes / 16);
       if (v == 1) copy_rec4<0><<<kRecs * 4 / 256, 256>>>(s, d, t);
       if (v == 2) copy_rec4<1><<<kRecs * 4 / 256, 256>>>(s, d, t);
-      if (v == 3) copy_gcm<<<kRecs * 16 / 256, 256>>>(s, d, t);
+      if (v == 3) copy_gcm<16><<<kRecs * 16 / 256, 256>>>(s, d, t);
+      if (v == 4) copy_gcm<8><<<kRecs * 8 / 256, 256>>>(s, d, t);
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;

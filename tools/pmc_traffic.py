@@ -26,7 +26,22 @@ CALIB_KNOWN = {  # bytes per launch moved by each tools/micro/calib_copy kernel
     "copy_chacha": (1 << 20) * 1350,
     "copy_quad": (1 << 20) * 1350,
     "copy_gcm": (1 << 20) * 1350,
+    "copy_gcm8": (1 << 20) * 1350,
 }
+
+
+def calib_pattern(full_name):
+    """The calib_copy pattern of a bulk kernel instantiation's record reads:
+    lanes per record L -> runs of 16 L bytes (gcm_kernel's last template
+    argument; the keyset kernel and gcm_bs_kernel<..., 16> 16 lanes; ChaCha its
+    own 64-byte-block pattern)."""
+    if "chacha" in full_name:
+        return "copy_chacha"
+    m = re.search(r"gcm(?:_bs)?_kernel<([^>]*)>", full_name)
+    lanes = int(m.group(1).split(",")[-1]) if m else 16
+    if "keyset" in full_name:
+        lanes = 16
+    return {4: "copy_quad", 8: "copy_gcm8", 16: "copy_gcm"}.get(lanes, "copy_gcm")
 CALIB_TAGS = (1 << 20) * 16  # the record kernels also write one 16-byte tag per record
 
 
@@ -58,7 +73,7 @@ def combine(entries):
         return entries[0]
     e = {"instantiations": len(entries)}
     for k in ("fetch_bytes_corrected", "write_bytes", "hbm_bytes_per_launch",
-              "grbm_gui_active_per_xcd"):
+              "fetch_bytes_calibrated", "hbm_bytes_calibrated", "grbm_gui_active_per_xcd"):
         if all(k in x for x in entries):
             e[k] = sum(x[k] for x in entries)
     cyc = [x.get("grbm_gui_active_per_xcd", 0) for x in entries]
@@ -68,7 +83,7 @@ def combine(entries):
     return e
 
 
-def summarise(c):
+def summarise(c, full_name="", calib=None):
     avg = {n: sum(v) / len(v) for n, v in c.items()}
     e = {"counters_avg_per_dispatch": avg}
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
@@ -76,6 +91,15 @@ def summarise(c):
         write = avg["WRITE_SIZE"] * 1024
         e.update({"fetch_bytes_corrected": fetch, "write_bytes": write,
                   "hbm_bytes_per_launch": fetch + write})
+        # Calibrated: the counted bytes scaled by known / counted of the copy
+        # kernel with the same record access pattern (tools/micro/calib_copy).
+        pat = calib_pattern(full_name)
+        cal = (calib or {}).get(pat, {})
+        if cal.get("fetch_counted_over_known") and cal.get("write_counted_over_known"):
+            fc = avg["FETCH_SIZE"] * 1024 / cal["fetch_counted_over_known"]
+            wc = write / cal["write_counted_over_known"]
+            e.update({"calib_pattern": pat, "fetch_bytes_calibrated": fc,
+                      "hbm_bytes_calibrated": fc + wc})
     if "GRBM_GUI_ACTIVE" in avg:
         cyc = avg["GRBM_GUI_ACTIVE"] / 8  # kernel cycles (GRBM sums the 8 XCDs)
         e["grbm_gui_active_per_xcd"] = cyc
@@ -99,26 +123,13 @@ def main():
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "traffic.json")
     res = {}
     if os.path.exists(dst):  # merge: configs not profiled in `src` keep their entries
-        res = {k: v for k, v in json.load(open(dst)).items() if k != "calibration"}
-    per_cfg = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(list)))
-    for sub in sorted(os.listdir(src)):
-        m = re.match(r"pmc_(config\w+?)_(fetch|write|sq)$", sub)
-        if not m:
-            continue
-        for k, c in load(os.path.join(src, sub)).items():
-            for n, v in c.items():
-                per_cfg[m.group(1)][k][n].extend(v)
-    for cfg, kernels in per_cfg.items():
-        fam = collections.defaultdict(list)
-        for (family, _), c in sorted(kernels.items()):
-            fam[family].append(summarise(c))
-        res[cfg] = {k: combine(v) for k, v in fam.items()}
-        res[cfg]["source"] = src
+        res = json.load(open(dst))
     calib = collections.defaultdict(dict)
     for sub, key in (("calib_fetch", "FETCH_SIZE"), ("calib_write", "WRITE_SIZE")):
         for (k, _), c in load(os.path.join(src, sub)).items():
             base = k.split("<")[0]
-            name = {"copy_rec4<0>": "copy_chacha", "copy_rec4<1>": "copy_quad"}.get(k, base)
+            name = {"copy_rec4<0>": "copy_chacha", "copy_rec4<1>": "copy_quad",
+                    "copy_gcm<16>": "copy_gcm", "copy_gcm<8>": "copy_gcm8"}.get(k, base)
             if name not in CALIB_KNOWN or key not in c:
                 continue
             counted = sum(c[key]) / len(c[key]) * 1024
@@ -131,6 +142,22 @@ def main():
                 calib[name]["write_counted_over_known"] = counted / known_w
     if calib:
         res["calibration"] = dict(calib)
+        res["calibration_source"] = src
+    calib_now = res.get("calibration", {})
+    per_cfg = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(list)))
+    for sub in sorted(os.listdir(src)):
+        m = re.match(r"pmc_(config\w+?)_(fetch|write|sq)$", sub)
+        if not m:
+            continue
+        for k, c in load(os.path.join(src, sub)).items():
+            for n, v in c.items():
+                per_cfg[m.group(1)][k][n].extend(v)
+    for cfg, kernels in per_cfg.items():
+        fam = collections.defaultdict(list)
+        for (family, full), c in sorted(kernels.items()):
+            fam[family].append(summarise(c, full, calib_now))
+        res[cfg] = {k: combine(v) for k, v in fam.items()}
+        res[cfg]["source"] = src
     json.dump(res, open(dst, "w"), indent=1, sort_keys=True)
     for cfg, ks in res.items():
         if not isinstance(ks, dict):

@@ -23,6 +23,13 @@ step() {
   [ $rc -eq 0 ] || exit $rc
 }
 has() { case " $PASSES " in *" $1 "*) return 0 ;; esac; return 1; }
+# FETCH_SIZE / WRITE_SIZE calibration on known byte counts, one copy kernel
+# per record access pattern (tools/micro/calib_copy, built in-tree here).
+if has calib; then
+  step calib_run 60 tools/micro/calib_copy 3
+  step calib_fetch 60 rocprofv3 --pmc FETCH_SIZE -d $O/calib_fetch -o run --output-format csv -- tools/micro/calib_copy 2
+  step calib_write 60 rocprofv3 --pmc WRITE_SIZE -d $O/calib_write -o run --output-format csv -- tools/micro/calib_copy 2
+fi
 for cfg in $CONFIGS; do
   case $cfg in config3|config3x) K=chacha_poly_kernel ;; configS) K=gcm_siv_kernel ;; config5) K=gcm_keyset_kernel ;; *) K=gcm_kernel ;; esac
   if has stats; then
