@@ -616,7 +616,12 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
       return;
     }
     if (j < nfull) {
-      store_blk_nt(dst + (uint64_t)j * 16, y);
+      // (L = 4: temporal stores, +2 % on config G's 64-byte runs, same box;
+      // non-temporal ones for the longer runs of L = 8 / 16, profiles/r05/r5s19)
+      if constexpr (L == 4)
+        store_blk(dst + (uint64_t)j * 16, y);
+      else
+        store_blk_nt(dst + (uint64_t)j * 16, y);
     } else if (j < nb) {
       const uint32_t n = (uint32_t)umin64(m.len + m.xlen - (uint64_t)j * 16, 16);
       if constexpr (XT) {

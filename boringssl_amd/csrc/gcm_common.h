@@ -211,12 +211,27 @@ __device__ __forceinline__ uint4 load_blk_nt(const uint8_t *p) {
                     __builtin_nontemporal_load(ip + 2), __builtin_nontemporal_load(ip + 3));
 }
 
+__device__ __forceinline__ void store_blk(uint8_t *p, uint4 y) {
+  u32_any *o = reinterpret_cast<u32_any *>(p);
+  o[0] = y.x;
+  o[1] = y.y;
+  o[2] = y.z;
+  o[3] = y.w;
+}
+
 __device__ __forceinline__ void store_blk_nt(uint8_t *p, uint4 y) {
   u32_any *o = reinterpret_cast<u32_any *>(p);
+#ifdef BSSL_PLAIN_STORES  // (A/B builds: temporal stores)
+  o[0] = y.x;
+  o[1] = y.y;
+  o[2] = y.z;
+  o[3] = y.w;
+#else
   __builtin_nontemporal_store(y.x, o);
   __builtin_nontemporal_store(y.y, o + 1);
   __builtin_nontemporal_store(y.z, o + 2);
   __builtin_nontemporal_store(y.w, o + 3);
+#endif
 }
 
 // Record at processing position i (sched.hip's length order, if any).

@@ -182,12 +182,25 @@ int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr,
 // `scratch` holds 128 uint32.  Returns 0 or a HIP error code.
 int build_length_order(const uint64_t *lengths, uint64_t n, uint32_t *order, uint32_t *scratch,
                        void *stream);
-// After build_length_order: processing positions [0, scratch[kSplitWord]) hold
-// the records of 4096 bytes or more, the rest the shorter ones (the class
-// cursor that ends at the first class below 4096 bytes, sched.hip).
-constexpr int kSplitWord = 64 + 47;
+// The length classes of build_length_order (sched.hip uses these): class
+// c = kSchedClasses - 1 - len / kSchedClassBytes (the longest records, of
+// (kSchedClasses - 1) * kSchedClassBytes bytes or more, in class 0); scratch
+// holds the class histogram, then the class cursors, which end the scatter at
+// the end of their class.
+constexpr int kSchedClasses = 64;
+constexpr uint64_t kSchedClassBytes = 256;
+// The scratch word that then holds the number of records of min_len bytes or
+// more (a multiple of kSchedClassBytes): the cursor of the last class whose
+// records are that long.
+constexpr int split_word_for(uint64_t min_len) {
+  return kSchedClasses + (kSchedClasses - 1 - (int)(min_len / kSchedClassBytes));
+}
+// Processing positions [0, scratch[kSplitWord]) hold the records of 4096
+// bytes or more, the rest the shorter ones ...
+constexpr int kSplitWord = split_word_for(4096);
 // ... and [0, scratch[kSplitWord2k]) the records of 2048 bytes or more.
-constexpr int kSplitWord2k = 64 + 55;
+constexpr int kSplitWord2k = split_word_for(2048);
+static_assert(kSplitWord == 64 + 47 && kSplitWord2k == 64 + 55, "length classes of sched.hip");
 // Whether a batch is worth reordering (ragged and large enough).
 inline bool wants_length_order(const BatchDesc &b) {
   return b.lengths && b.num_records >= 4096 && b.num_records < (uint64_t(1) << 32);

@@ -14,12 +14,12 @@
 namespace bssl_amd {
 namespace {
 
-constexpr int kClasses = 64;
+constexpr int kClasses = kSchedClasses;  // (internal.h: the split words derive from these)
 constexpr int kThreads = 256;
 constexpr int kPerThread = 16;  // records per thread in the scatter pass
 
 __device__ __forceinline__ int length_class(uint64_t len) {
-  const uint64_t c = len >> 8;
+  const uint64_t c = len / kSchedClassBytes;
   return c >= kClasses - 1 ? 0 : kClasses - 1 - (int)c;  // longest first
 }
 

@@ -25,7 +25,9 @@
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); return 1; } } while (0)
 
-constexpr uint64_t kRecs = 1 << 20, kLen = 1350, kStride = 1360;
+struct Geo {
+  uint64_t recs, len, stride;
+};
 
 // Tail of a record: dword copies of the last (len % 16) bytes' 16-byte chunk.
 __device__ __forceinline__ void copy_tail(const uint8_t *s, uint8_t *d, uint32_t n) {
@@ -41,13 +43,14 @@ __global__ __launch_bounds__(256) void copy_stream(const uint4 *s, uint4 *d, uin
 }
 
 template <int MODE>  // 0 chacha, 1 quad
-__global__ __launch_bounds__(256) void copy_rec4(const uint8_t *s, uint8_t *d, uint8_t *tags) {
+__global__ __launch_bounds__(256) void copy_rec4(const uint8_t *s, uint8_t *d, uint8_t *tags, Geo g) {
   const uint64_t rec = (blockIdx.x * 256ull + threadIdx.x) / 4;
   const int q = threadIdx.x & 3;
-  if (rec >= kRecs) return;
-  const uint8_t *sp = s + rec * kStride;
-  uint8_t *dp = d + rec * kStride;
-  constexpr uint32_t kFull = kLen / 64;  // 21 full blocks
+  if (rec >= g.recs) return;
+  const uint64_t kLen = g.len;
+  const uint8_t *sp = s + rec * g.stride;
+  uint8_t *dp = d + rec * g.stride;
+  const uint32_t kFull = (uint32_t)(kLen / 64);
   for (uint32_t it = 0; it * 4 < kFull + 1; it++) {
     const uint32_t blk = it * 4 + q;
     if (MODE == 0) {
@@ -57,8 +60,8 @@ __global__ __launch_bounds__(256) void copy_rec4(const uint8_t *s, uint8_t *d, u
         for (int k = 0; k < 4; k++) v[k] = a[k];
         uint4 *b = reinterpret_cast<uint4 *>(dp + 64 * blk);
         for (int k = 0; k < 4; k++) b[k] = v[k];
-      } else if (blk == kFull) {
-        copy_tail(sp + 64 * blk, dp + 64 * blk, kLen - 64 * kFull);
+      } else if (blk == kFull && kLen > 64ull * kFull) {
+        copy_tail(sp + 64 * blk, dp + 64 * blk, (uint32_t)(kLen - 64 * kFull));
       }
     } else {
       uint4 v[4];
@@ -69,7 +72,8 @@ __global__ __launch_bounds__(256) void copy_rec4(const uint8_t *s, uint8_t *d, u
       for (int k = 0; k < 4; k++) {
         const uint32_t bk = it * 4 + k;
         if (bk < kFull) reinterpret_cast<uint4 *>(dp + 64 * bk)[q] = v[k];
-        else if (bk == kFull && q == 0) copy_tail(sp + 64 * bk, dp + 64 * bk, kLen - 64 * kFull);
+        else if (bk == kFull && q == 0 && kLen > 64ull * kFull)
+          copy_tail(sp + 64 * bk, dp + 64 * bk, (uint32_t)(kLen - 64 * kFull));
       }
     }
   }
@@ -77,23 +81,28 @@ __global__ __launch_bounds__(256) void copy_rec4(const uint8_t *s, uint8_t *d, u
 }
 
 template <int LN>  // lanes per record
-__global__ __launch_bounds__(256) void copy_gcm(const uint8_t *s, uint8_t *d, uint8_t *tags) {
+__global__ __launch_bounds__(256) void copy_gcm(const uint8_t *s, uint8_t *d, uint8_t *tags, Geo g) {
   const uint64_t rec = (blockIdx.x * 256ull + threadIdx.x) / LN;
   const int q = threadIdx.x & (LN - 1);
-  if (rec >= kRecs) return;
-  const uint8_t *sp = s + rec * kStride;
-  uint8_t *dp = d + rec * kStride;
-  constexpr uint32_t kFull = kLen / 16;  // 84 full 16-byte blocks
+  if (rec >= g.recs) return;
+  const uint64_t kLen = g.len;
+  const uint8_t *sp = s + rec * g.stride;
+  uint8_t *dp = d + rec * g.stride;
+  const uint32_t kFull = (uint32_t)(kLen / 16);
   for (uint32_t j = q; j <= kFull; j += LN) {
     if (j < kFull) reinterpret_cast<uint4 *>(dp)[j] = reinterpret_cast<const uint4 *>(sp)[j];
-    else copy_tail(sp + 16 * j, dp + 16 * j, kLen - 16 * kFull);
+    else if (kLen > 16ull * kFull) copy_tail(sp + 16 * j, dp + 16 * j, (uint32_t)(kLen - 16 * kFull));
   }
   if (q == 0) reinterpret_cast<uint4 *>(tags)[rec] = make_uint4(rec, 1, 2, 3);
 }
 
 int main(int argc, char **argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 5;
-  const uint64_t bytes = kRecs * kStride;
+  Geo g{argc > 4 ? strtoull(argv[4], nullptr, 10) : (1ull << 20),
+        argc > 2 ? strtoull(argv[2], nullptr, 10) : 1350,
+        argc > 3 ? strtoull(argv[3], nullptr, 10) : 1360};
+  const uint64_t kRecs = g.recs, kLen = g.len;
+  const uint64_t bytes = g.recs * g.stride;
   uint8_t *s, *d, *t;
   CK(hipMalloc(&s, bytes));
   CK(hipMalloc(&d, bytes));
@@ -109,10 +118,10 @@ int main(int argc, char **argv) {
     for (int r = 0; r < reps; r++) {
       CK(hipEventRecord(e0));
       if (v == 0) copy_stream<<<8192, 256>>>((const uint4 *)s, (uint4 *)d, bytes / 16);
-      if (v == 1) copy_rec4<0><<<kRecs * 4 / 256, 256>>>(s, d, t);
-      if (v == 2) copy_rec4<1><<<kRecs * 4 / 256, 256>>>(s, d, t);
-      if (v == 3) copy_gcm<16><<<kRecs * 16 / 256, 256>>>(s, d, t);
-      if (v == 4) copy_gcm<8><<<kRecs * 8 / 256, 256>>>(s, d, t);
+      if (v == 1) copy_rec4<0><<<(unsigned)((kRecs * 4 + 255) / 256), 256>>>(s, d, t, g);
+      if (v == 2) copy_rec4<1><<<(unsigned)((kRecs * 4 + 255) / 256), 256>>>(s, d, t, g);
+      if (v == 3) copy_gcm<16><<<(unsigned)((kRecs * 16 + 255) / 256), 256>>>(s, d, t, g);
+      if (v == 4) copy_gcm<8><<<(unsigned)((kRecs * 8 + 255) / 256), 256>>>(s, d, t, g);
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;

@@ -21,13 +21,19 @@ import os
 import re
 import sys
 
-CALIB_KNOWN = {  # bytes per launch moved by each tools/micro/calib_copy kernel
-    "copy_stream": (1 << 20) * 1360,
-    "copy_chacha": (1 << 20) * 1350,
-    "copy_quad": (1 << 20) * 1350,
-    "copy_gcm": (1 << 20) * 1350,
-    "copy_gcm8": (1 << 20) * 1350,
-}
+CALIB_PATTERNS = ("copy_stream", "copy_chacha", "copy_quad", "copy_gcm", "copy_gcm8")
+# Record geometry of each config's bench layout (length x stride): the
+# counters' ratio to the bytes moved depends on it, so every config reads the
+# calibration copy of its own geometry (calib_{fetch,write}_LENxSTRIDExRECS).
+CONFIG_GEO = {"config2": "16384x16384", "config5": "16384x16384", "configG": "1350x1408",
+              "config3": "1350x1408", "config3x": "1350x1408"}
+
+
+def geo_known(geo, pattern):
+    n_len, n_stride, n_recs = (int(x) for x in geo.split("x"))
+    if pattern == "copy_stream":
+        return n_recs * n_stride, n_recs * n_stride
+    return n_recs * n_len, n_recs * (n_len + CALIB_TAGS_PER_REC)
 
 
 def calib_pattern(full_name):
@@ -42,7 +48,7 @@ def calib_pattern(full_name):
     if "keyset" in full_name:
         lanes = 16
     return {4: "copy_quad", 8: "copy_gcm8", 16: "copy_gcm"}.get(lanes, "copy_gcm")
-CALIB_TAGS = (1 << 20) * 16  # the record kernels also write one 16-byte tag per record
+CALIB_TAGS_PER_REC = 16  # the copy kernels also write one 16-byte tag per record
 
 
 def short_name(name):
@@ -124,24 +130,27 @@ def main():
     res = {}
     if os.path.exists(dst):  # merge: configs not profiled in `src` keep their entries
         res = json.load(open(dst))
-    calib = collections.defaultdict(dict)
-    for sub, key in (("calib_fetch", "FETCH_SIZE"), ("calib_write", "WRITE_SIZE")):
+    calib = collections.defaultdict(lambda: collections.defaultdict(dict))
+    for sub in sorted(os.listdir(src)):
+        m = re.match(r"calib_(fetch|write)_(\d+x\d+x\d+)$", sub)
+        if not m:
+            continue
+        key = "FETCH_SIZE" if m.group(1) == "fetch" else "WRITE_SIZE"
+        geo = m.group(2)
         for (k, _), c in load(os.path.join(src, sub)).items():
-            base = k.split("<")[0]
             name = {"copy_rec4<0>": "copy_chacha", "copy_rec4<1>": "copy_quad",
-                    "copy_gcm<16>": "copy_gcm", "copy_gcm<8>": "copy_gcm8"}.get(k, base)
-            if name not in CALIB_KNOWN or key not in c:
+                    "copy_gcm<16>": "copy_gcm", "copy_gcm<8>": "copy_gcm8"}.get(k, k.split("<")[0])
+            if name not in CALIB_PATTERNS or key not in c:
                 continue
             counted = sum(c[key]) / len(c[key]) * 1024
-            known = CALIB_KNOWN[name]
+            known_r, known_w = geo_known(geo, name)
             if key == "FETCH_SIZE":
-                calib[name]["fetch_counted_over_known"] = counted / known
-                calib[name]["fetch_x2_over_known"] = 2 * counted / known
+                calib[geo][name]["fetch_counted_over_known"] = counted / known_r
+                calib[geo][name]["fetch_x2_over_known"] = 2 * counted / known_r
             else:
-                known_w = known + (CALIB_TAGS if name != "copy_stream" else 0)
-                calib[name]["write_counted_over_known"] = counted / known_w
+                calib[geo][name]["write_counted_over_known"] = counted / known_w
     if calib:
-        res["calibration"] = dict(calib)
+        res["calibration"] = {g: dict(v) for g, v in calib.items()}
         res["calibration_source"] = src
     calib_now = res.get("calibration", {})
     per_cfg = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(list)))
@@ -155,7 +164,11 @@ def main():
     for cfg, kernels in per_cfg.items():
         fam = collections.defaultdict(list)
         for (family, full), c in sorted(kernels.items()):
-            fam[family].append(summarise(c, full, calib_now))
+            geo = CONFIG_GEO.get(cfg)
+            if cfg == "config4":  # mixed lengths: the long records at L = 8, the short at 4
+                geo = "1350x1408" if calib_pattern(full) == "copy_quad" else "16384x16384"
+            cal = next((v for g, v in calib_now.items() if geo and g.startswith(geo + "x")), None)
+            fam[family].append(summarise(c, full, cal))
         res[cfg] = {k: combine(v) for k, v in fam.items()}
         res[cfg]["source"] = src
     json.dump(res, open(dst, "w"), indent=1, sort_keys=True)

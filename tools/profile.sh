@@ -25,10 +25,15 @@ step() {
 has() { case " $PASSES " in *" $1 "*) return 0 ;; esac; return 1; }
 # FETCH_SIZE / WRITE_SIZE calibration on known byte counts, one copy kernel
 # per record access pattern (tools/micro/calib_copy, built in-tree here).
+# Geometries: 1350-byte records at the bench's 1408-byte stride (configs G, 3,
+# the short records of 4) and 16 KiB records (configs 2, 5, the long ones of 4).
 if has calib; then
-  step calib_run 60 tools/micro/calib_copy 3
-  step calib_fetch 60 rocprofv3 --pmc FETCH_SIZE -d $O/calib_fetch -o run --output-format csv -- tools/micro/calib_copy 2
-  step calib_write 60 rocprofv3 --pmc WRITE_SIZE -d $O/calib_write -o run --output-format csv -- tools/micro/calib_copy 2
+  for geo in "1350 1408 1048576" "16384 16384 262144"; do
+    tag=$(echo $geo | tr ' ' 'x')
+    step calib_run_$tag 60 tools/micro/calib_copy 3 $geo
+    step calib_fetch_$tag 60 rocprofv3 --pmc FETCH_SIZE -d $O/calib_fetch_$tag -o run --output-format csv -- tools/micro/calib_copy 2 $geo
+    step calib_write_$tag 60 rocprofv3 --pmc WRITE_SIZE -d $O/calib_write_$tag -o run --output-format csv -- tools/micro/calib_copy 2 $geo
+  done
 fi
 for cfg in $CONFIGS; do
   case $cfg in config3|config3x) K=chacha_poly_kernel ;; configS) K=gcm_siv_kernel ;; config5) K=gcm_keyset_kernel ;; *) K=gcm_kernel ;; esac
