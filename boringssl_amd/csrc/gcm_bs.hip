@@ -973,13 +973,27 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_keyset_kernel(
 }  // namespace
 
 // Table-free launcher (launch_gcm with the bitsliced engine selected).
-// Lanes per record: 16 for records of 4 KiB or more, 2 for shorter ones
+// Lanes per record: 16 for records of 4 KiB or more (8 in a ragged batch), 2 for shorter ones
 // (a chunk covers 16 * L blocks of a record: a 1350-byte record of 85
 // blocks fills 3 chunks of 32 slots at L = 2, against one of 256 at L = 16;
 // the per-record start and end are spread over the record's L lanes, and at
 // L = 2 each lane has eight times the blocks).  A ragged batch in length
 // order is two launches, the records of 4 KiB or more at 16 lanes and the
 // shorter ones at 2 (the class cursor of the length sort, as gcm.hip).
+#ifndef BS_LONG_L
+#define BS_LONG_L 16
+#endif
+#ifndef BS_SHORT_L
+#define BS_SHORT_L 2
+#endif
+// Lanes per record: 16 for uniform batches of records of 4 KiB or more, 8 for
+// the long class of a ragged batch (4 KiB to 16 KiB and beyond: fewer empty
+// slots in a record's last chunk; config 4 644 -> 677 GiB/s, while config 2
+// lost 3 % at 8, same box, gpurun_out r5s21), 2 below 4 KiB (config G at 4:
+// 544 against 676).
+constexpr int kBsLongL = BS_LONG_L, kBsShortL = BS_SHORT_L;  // (A/B builds: -DBS_LONG_L=8 ...)
+constexpr int kBsRaggedL = 8;
+
 int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, hipStream_t s,
                   const KernelEvents *ev) {
   const int num_cus = device_cu_count();
@@ -1032,12 +1046,12 @@ int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, 
 #define BSSL_BS_ONEKEY(NR_, OPEN_, XT_)                                              \
   do {                                                                               \
     if (split) {                                                                     \
-      go(gcm_bs_kernel<NR_, OPEN_, XT_, false, 16>, bl, ctl);                        \
-      go(gcm_bs_kernel<NR_, OPEN_, XT_, false, 2>, bs, ctl2);                        \
+      go(gcm_bs_kernel<NR_, OPEN_, XT_, false, kBsRaggedL>, bl, ctl);                \
+      go(gcm_bs_kernel<NR_, OPEN_, XT_, false, kBsShortL>, bs, ctl2);                \
     } else if (short_uniform) {                                                      \
-      go(gcm_bs_kernel<NR_, OPEN_, XT_, false, 2>, bo, ctl);                         \
+      go(gcm_bs_kernel<NR_, OPEN_, XT_, false, kBsShortL>, bo, ctl);                 \
     } else {                                                                         \
-      go(gcm_bs_kernel<NR_, OPEN_, XT_, false, 16>, bo, ctl);                        \
+      go(gcm_bs_kernel<NR_, OPEN_, XT_, false, kBsLongL>, bo, ctl);                  \
     }                                                                                \
   } while (0)
 #define BSSL_BS_LAUNCH(NR_, OPEN_)                                                   \

@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round 5, session 21: lanes per record of the table-free engine -- 16 vs 8
+# for records of 4 KiB or more (configs 2, 5, 4), 2 vs 4 below (configs G, 4);
+# every line digest-checked against the reference library.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+O=gpurun_out/${RUN:-r5s21}
+mkdir -p $O
+export TMPDIR=/tmp
+step() {
+  local name=$1 t=$2; shift 2
+  echo "[$(date +%T)] $name" | tee -a $O/steps.log
+  timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc $(grep -o '"value": [0-9.]*' $O/$name.log | head -1) $(grep -o '"parity": "[a-z_]*' $O/$name.log | head -1)" | tee -a $O/steps.log
+  [ $rc -eq 0 ] || { tail -5 $O/$name.log; exit $rc; }
+}
+export BSSL_AMD_GCM_MODE=bs
+L=boringssl_amd/csrc/build
+B="python bench.py --steps 10 --warmup 2 --no-cpu-baseline --config"
+for cfg in config2 config5 config4; do
+  step base_$cfg 200 $B $cfg
+  step long8_$cfg 200 env BSSL_AMD_LIB=$L/ab_long8/libbssl_amd.so $B $cfg
+done
+for cfg in configG config4; do
+  step base2_$cfg 200 $B $cfg
+  step short4_$cfg 200 env BSSL_AMD_LIB=$L/ab_short4/libbssl_amd.so $B $cfg
+done
