@@ -55,6 +55,9 @@ constexpr uint32_t kBsGroupRecs = 1024;   // records per E_K(J0) batch
 #ifndef BS_AHEAD
 #define BS_AHEAD 4
 #endif
+#ifndef BS_EDGE_PRIO
+#define BS_EDGE_PRIO 0  // (A/B builds: s_setprio of the record start and end)
+#endif
 constexpr uint32_t kBsAhead = BS_AHEAD;    // E_K(J0) groups produced ahead (bs_kernel)
 constexpr uint32_t kBsLdsBasis = kG8Bytes;  // build_gpow scratch (2 KiB)
 constexpr uint32_t kBsLdsState = kBsLdsBasis + 128 * 16;  // parked unit state (bs_unit)
@@ -393,6 +396,9 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
   const uint8_t *ld_ptr = nullptr;
   uint8_t *st_ptr = nullptr;
   int32_t ld_left = -1, st_left = -1;
+#if BS_EDGE_PRIO
+  __builtin_amdgcn_s_setprio(BS_EDGE_PRIO);  // (A/B: the record start's loads and products)
+#endif
   {
     const uint32_t r = bs_lane() / L;
     const uint64_t i = first + r;
@@ -451,6 +457,9 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
     }
   }
   const uint32_t *__restrict__ mk = &key->bsmask[0][0];
+#if BS_EDGE_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
   BS_LAP(0);
 #pragma unroll 1
   for (int c = 0; c < nchunks; c++) {
@@ -783,6 +792,9 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
     put4(kSacc0, acc);
   }
   // Record end.
+#if BS_EDGE_PRIO
+  __builtin_amdgcn_s_setprio(BS_EDGE_PRIO);
+#endif
   const uint4 rq = get4(kSflags);
   const uint32_t fl = rq.x;
   const bool act = fl & 1u, live = (fl >> 1) & 1u;
@@ -821,6 +833,9 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
   BS_LAP(9);
   finish_record<OPEN, L>(acc, nb, m, e0, b, rec, act, live, b.out + m.off, key->hpow_ct);
   BS_LAP(6);
+#if BS_EDGE_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
 }
 
 // One-key bulk kernel: one workgroup of 16 waves per CU; each wave takes the
