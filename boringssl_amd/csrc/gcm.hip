@@ -1037,6 +1037,18 @@ bool runs_in_lines(const BatchDesc &b) {
            b.record_stride) & 63) == 0;
 }
 
+// Lanes per record of the iovec length classes of 4 KiB or more and below
+// 2 KiB (the class between takes 8).  Round 5 (profiles/r05/r5s25): 8 lanes
+// for the long class 817 against 911-932 GiB/s (16 KiB records in three
+// chunks), 8 for the short class 474 against 505 (1350 B).
+#ifndef GCM_IOV_LONG_L
+#define GCM_IOV_LONG_L 16
+#endif
+#ifndef GCM_IOV_SHORT_L
+#define GCM_IOV_SHORT_L 4
+#endif
+constexpr int kIovLongL = GCM_IOV_LONG_L, kIovShortL = GCM_IOV_SHORT_L;
+
 template <int NR, bool OPEN>
 int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const KernelEvents *ev) {
   if (one_record_batch(b)) {
@@ -1095,11 +1107,11 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
       BatchDesc bl = bo, bm = bo, bs = bo;
       bl.split_hi = bm.split_lo = order + b.num_records + kSplitWord;
       bm.split_hi = bs.split_lo = order + b.num_records + kSplitWord2k;
-      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, true, 16>), dim3(grid),
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, true, kIovLongL>), dim3(grid),
                          dim3(kWaves * 64), 0, s, keys, bl, units);
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, true, 8>), dim3(grid),
                          dim3(kWaves * 64), 0, s, keys, bm, units + 4);
-      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, true, 4>), dim3(grid),
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, true, kIovShortL>), dim3(grid),
                          dim3(kWaves * 64), 0, s, keys, bs, units + 8);
     } else if (b.iovecs) {
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, true, 16>), dim3(grid),
