@@ -437,6 +437,11 @@ __device__ __forceinline__ uint4 aes_block_rep(uint4 in, const RoundKeys &rk, co
 // 4) -- in the tiled path all 16 waves must finish their units together, and
 // with fixed priorities the SIMD arbiter's age order makes the youngest wave
 // of each SIMD ~1.9x slower than the oldest.
+#ifndef GCM_IOV_HANDOFF
+#define GCM_IOV_HANDOFF 1
+#endif
+constexpr bool kIovHandoff = GCM_IOV_HANDOFF != 0;
+
 template <int NR, bool OPEN, bool XT, int L = 16, bool RP = false, bool IOV = false>
 __device__ __forceinline__ void process_records(const RoundKeys &rk, const BatchDesc &b,
                                                 const UnitIn &in, const uint8_t *smem,
@@ -514,6 +519,17 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   const uint8_t *ld_ptr = nullptr;
   uint8_t *st_ptr = nullptr;
   int32_t ld_left = -1, st_left = -1;
+  // Store anchor handed over by the load cursor (kIovHandoff): when a load
+  // walks the chunk table to a whole block inside one chunk, the output
+  // address of that block (the output chunks have the input chunks' lengths)
+  // and the bytes left in its chunk, tagged with the block index.  The store
+  // of that block (one iteration later) then re-anchors its run without a
+  // walk of its own: the walk's chunk-table loads, issued after the previous
+  // stores and the next block's load, wait for all of them (vmcnt counts
+  // loads and stores in issue order).
+  uint8_t *ho_ptr = nullptr;
+  int32_t ho_left = -1;
+  uint32_t ho_j = 0xffffffffu;
   if constexpr (IOV) {
     if (live) {
       ld_c = st_c = b.iovec_start[rec];
@@ -541,9 +557,14 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
           iov_at(k, b, ld_c, ld_cs);
           iov_seek(k, b, p, c_end);
           const uint32_t n = (uint32_t)umin64(m.len - p, 16);
-          if (n == 16 && p + 16 <= k.ce)
+          if (n == 16 && p + 16 <= k.ce) {
             v = load_blk_nt(k.in + (p - k.cs));
-          else if (!iov_load2(b, k, p, n, c_end, v))  // a straddle, the last block
+            if constexpr (kIovHandoff) {
+              ho_ptr = k.out + (p - k.cs);
+              ho_left = (int32_t)umin64(k.ce - p, 1u << 30);
+              ho_j = (uint32_t)j;
+            }
+          } else if (!iov_load2(b, k, p, n, c_end, v))  // a straddle, the last block
             v = iov_gather(b, k, p, n, c_end);        // (three or more chunks)
           ld_c = k.c;
           ld_cs = k.cs;
@@ -594,6 +615,10 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
         store_blk_nt(st_ptr, y);
         st_ptr += 16 * L;
         st_left -= 16 * L;
+      } else if (kIovHandoff && ho_j == j) {  // (j < nb: a whole block was loaded)
+        store_blk_nt(ho_ptr, y);
+        st_ptr = ho_ptr + 16 * L;
+        st_left = ho_left - 16 * L;
       } else if (j < nb) {
         const uint64_t p = (uint64_t)j * 16;
         const uint32_t n = (uint32_t)umin64(m.len - p, 16);
