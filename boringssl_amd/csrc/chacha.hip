@@ -50,6 +50,10 @@ constexpr int kLanes = 2;
 #define CHACHA_PRAGMA_(x) _Pragma(#x)
 #define CHACHA_PRAGMA(x) CHACHA_PRAGMA_(x)
 constexpr uint32_t kM26 = 0x3ffffff;
+#ifndef CHACHA_IOV_HANDOFF
+#define CHACHA_IOV_HANDOFF 1
+#endif
+constexpr bool kIovHandoff = CHACHA_IOV_HANDOFF != 0;
 
 __device__ __forceinline__ uint32_t rotl(uint32_t v, int n) {
   return __builtin_amdgcn_alignbit(v, v, 32 - n);
@@ -574,6 +578,14 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
   const uint8_t *ld_ptr = nullptr;
   uint8_t *st_ptr = nullptr;
   int64_t ld_left = -1, st_left = -1;
+  // Store anchor handed over by the load cursor (as gcm.hip's kIovHandoff):
+  // when prefetch walks the chunk table to a whole block inside one chunk, the
+  // block's output address and the bytes left in its chunk, tagged with the
+  // data block index; the block's store re-anchors its run from it without a
+  // walk of its own (whose loads would wait for every older load and store).
+  uint8_t *ho_ptr = nullptr;
+  int64_t ho_left = -1;
+  uint32_t ho_d = 0xffffffffu;
   bool pre_ok = false;  // pre[] holds the lane's whole current block
   if constexpr (IOV) {
     if (live) ld_c = st_c = b.iovec_start[rec];
@@ -603,6 +615,11 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
             gp = k.in + (p - k.cs);
             ld_ptr = gp + 64 * L;
             ld_left = (int64_t)(k.ce - p) - 64 * L;
+            if constexpr (kIovHandoff) {
+              ho_ptr = k.out + (p - k.cs);
+              ho_left = (int64_t)(k.ce - p);
+              ho_d = (uint32_t)d;
+            }
           } else {
             ld_left = -1;
           }
@@ -660,6 +677,13 @@ __device__ __forceinline__ void chacha_group(const ChaChaKeyDev *__restrict__ ke
                         make_uint4(y[4 * i], y[4 * i + 1], y[4 * i + 2], y[4 * i + 3]));
           st_ptr += 64 * L;
           st_left -= 64 * L;
+        } else if (kIovHandoff && ho_d == (uint32_t)d) {
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            store16_any(ho_ptr + 16 * i,
+                        make_uint4(y[4 * i], y[4 * i + 1], y[4 * i + 2], y[4 * i + 3]));
+          st_ptr = ho_ptr + 64 * L;
+          st_left = ho_left - 64 * L;
         } else {
           IovCur k;
           iov_at(k, b, st_c, st_cs);
