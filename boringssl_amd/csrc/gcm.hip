@@ -441,6 +441,10 @@ __device__ __forceinline__ uint4 aes_block_rep(uint4 in, const RoundKeys &rk, co
 #define GCM_IOV_HANDOFF 1
 #endif
 constexpr bool kIovHandoff = GCM_IOV_HANDOFF != 0;
+#ifndef GCM_IOV_KEEP_END
+#define GCM_IOV_KEEP_END 0
+#endif
+constexpr bool kIovKeepEnd = GCM_IOV_KEEP_END != 0;
 
 template <int NR, bool OPEN, bool XT, int L = 16, bool RP = false, bool IOV = false>
 __device__ __forceinline__ void process_records(const RoundKeys &rk, const BatchDesc &b,
@@ -530,6 +534,10 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   uint8_t *ho_ptr = nullptr;
   int32_t ho_left = -1;
   uint32_t ho_j = 0xffffffffu;
+  // End of the load cursor's chunk once walked (kIovKeepEnd; 0: not yet): a
+  // load past it starts the walk at the next chunk, one dependent chunk-table
+  // load instead of two.
+  uint64_t ld_ce = 0;
   if constexpr (IOV) {
     if (live) {
       ld_c = st_c = b.iovec_start[rec];
@@ -554,7 +562,10 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
         if (live && p < m.len) {  // (a dead record never walks the batch's chunks)
           const uint64_t c_end = b.iovec_start[rec + 1];
           IovCur k;
-          iov_at(k, b, ld_c, ld_cs);
+          if (kIovKeepEnd && ld_ce && p >= ld_ce && ld_c + 1 < c_end)
+            iov_at(k, b, ld_c + 1, ld_ce);
+          else
+            iov_at(k, b, ld_c, ld_cs);
           iov_seek(k, b, p, c_end);
           const uint32_t n = (uint32_t)umin64(m.len - p, 16);
           if (n == 16 && p + 16 <= k.ce) {
@@ -568,6 +579,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
             v = iov_gather(b, k, p, n, c_end);        // (three or more chunks)
           ld_c = k.c;
           ld_cs = k.cs;
+          if constexpr (kIovKeepEnd) ld_ce = k.ce;
           ld_ptr = k.in + (p - k.cs) + 16 * L;
           ld_left = (int32_t)umin64(k.ce - p, 1u << 30) - 16 * L;
         }
