@@ -73,7 +73,8 @@ EXPORTED_SYMBOLS = [
     "BSSL_AMD_set_device", "BSSL_AMD_device_count", "BSSL_AMD_synth_fill_device",
     "BSSL_AMD_set_kernel_timing", "BSSL_AMD_collect_kernel_times", "BSSL_AMD_last_kernel_ms",
     "BSSL_AMD_last_kernel_name", "BSSL_AMD_set_aes_gcm_engine", "BSSL_AMD_aes_gcm_engine",
-    "BSSL_AMD_gcm_key_tables",
+    # include/bssl_amd/test_hooks.h (test support, not part of the EVP surface)
+    "BSSL_AMD_gcm_key_tables", "BSSL_AMD_test_set_bs_ek0_producers",
     # include/bssl_amd/tls.h
     "BSSL_AMD_TLS_AEAD_new", "BSSL_AMD_TLS_AEAD_free", "BSSL_AMD_TLS_AEAD_prefix_len",
     "BSSL_AMD_TLS_AEAD_suffix_len", "BSSL_AMD_TLS_AEAD_sequence",
@@ -167,6 +168,7 @@ _SIGS = {
     "BSSL_AMD_set_aes_gcm_engine": (_I, [_I]),
     "BSSL_AMD_aes_gcm_engine": (_I, []),
     "BSSL_AMD_gcm_key_tables": (_S, [_P, _S, _S, _I, _P]),
+    "BSSL_AMD_test_set_bs_ek0_producers": (_I, [_I]),
     "BSSL_AMD_TLS_AEAD_new": (_P, [_I, ctypes.c_uint16, _P, _P, _S, _P, _S, ctypes.c_uint64]),
     "BSSL_AMD_TLS_AEAD_free": (None, [_P]),
     "BSSL_AMD_TLS_AEAD_prefix_len": (_S, [_P]),
@@ -501,10 +503,20 @@ def gcm_key_tables(keys, key_len, on_device):
 def set_aes_gcm_engine(engine):
     """Selects the AES-GCM engine ("bs": bitsliced, table-free; "table": LDS
     T-tables) for every later batch of this process; returns the previous one."""
+    if engine not in AES_GCM_ENGINES:
+        raise ValueError(f"unknown AES-GCM engine {engine!r} (one of {sorted(AES_GCM_ENGINES)})")
     prev = _lib.BSSL_AMD_set_aes_gcm_engine(AES_GCM_ENGINES[engine])
     if prev < 0:
-        raise ValueError(engine)
+        raise RuntimeError(f"BSSL_AMD_set_aes_gcm_engine refused {engine!r}")
     return {v: k for k, v in AES_GCM_ENGINES.items()}[prev]
+
+
+def test_set_bs_ek0_producers(on):
+    """Test support (include/bssl_amd/test_hooks.h): with False, the table-free
+    engine's launches skip the batched E_K(J0) production, so every record end
+    takes the bounded-wait fallback and computes its own E_K(J0).  Returns the
+    previous setting."""
+    return bool(_lib.BSSL_AMD_test_set_bs_ek0_producers(1 if on else 0))
 
 
 def aes_gcm_engine():

@@ -16,6 +16,7 @@
 
 #include "bssl_amd/aead.h"
 #include "bssl_amd/tls.h"
+#include "bssl_amd/test_hooks.h"
 #include "internal.h"
 
 using namespace bssl_amd;
@@ -156,6 +157,10 @@ KeyMaterial *make_keys(const EVP_AEAD *aead, const uint8_t *keys, size_t num_key
     km->bytes = bytes;
     if (gcm_key_setup_device(keys, aead->key_len, num_keys, reinterpret_cast<GcmKeyDev *>(km->dev),
                              nullptr) != 0) {
+      // The kernel may have written tables before the failure: wipe them as
+      // free_keys does before the memory goes back.
+      hipMemset(km->dev, 0, bytes);
+      hipDeviceSynchronize();
       hipFree(km->dev);
       delete km;
       return nullptr;
@@ -251,14 +256,23 @@ const KernelEvents *timing_pair() {
   return &t_timing.pending.back();
 }
 
+// Name of the dominant kernel of an AES-GCM launch on `engine` (the timing
+// records and bench.py's profile lookup key on it).
+const char *gcm_kernel_name(int engine) {
+  return engine == kGcmEngineBitsliced ? "gcm_bs_kernel" : "gcm_kernel";
+}
+
 // Launch the bulk kernels of the AEAD over a filled-in descriptor.  Returns 0
-// or a HIP error code.
-int launch_desc(const KeyMaterial *km, const BatchDesc &d, bool open, void *stream) {
+// or a HIP error code.  `gcm_eng`: the AES-GCM engine the caller already read
+// for this batch (-1: read it here), so one batch never sees two engines.
+int launch_desc(const KeyMaterial *km, const BatchDesc &d, bool open, void *stream,
+                int gcm_eng = -1) {
   int rc;
   const KernelEvents *ev = timing_pair();
   if (km->aead->kind == kAeadAesGcm) {
-    rc = launch_gcm(static_cast<const GcmKeyDev *>(km->dev), d, open, km->nr, stream, ev);
-    t_timing.last_name = "gcm_kernel";
+    const int eng = gcm_eng >= 0 ? gcm_eng : gcm_engine();
+    rc = launch_gcm(static_cast<const GcmKeyDev *>(km->dev), d, open, km->nr, stream, ev, eng);
+    t_timing.last_name = gcm_kernel_name(eng);
   } else if (km->aead->kind == kAeadAesGcmSiv) {
     rc = launch_gcm_siv(static_cast<const GcmKeyDev *>(km->dev), d, open, km->nr, stream, ev);
     t_timing.last_name = "gcm_siv_kernel";
@@ -302,11 +316,14 @@ int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch
   d.extra = nullptr;
   d.extra_out = nullptr;
   d.extra_len = d.extra_stride = d.extra_out_stride = d.tag_stride = 0;
+  // The AES-GCM engine is read once per batch: the completion-word decision
+  // below and the launch must agree on it.
+  const int gcm_eng = km->aead->kind == kAeadAesGcm ? gcm_engine() : -1;
   if (one) {
     // The completion word only when a one-record kernel will write it
     // (*done_armed tells one_record whether to spin on it).
     const AeadKind k = km->aead->kind;
-    const bool writes = k == kAeadAesGcm ? gcm_takes_one_record_kernel(d)
+    const bool writes = k == kAeadAesGcm ? gcm_takes_one_record_kernel(d, gcm_eng)
                         : k == kAeadAesGcmSiv ? false
                                               : chacha_takes_one_record_kernel(d);
     d.done = writes ? one->done : nullptr;
@@ -316,7 +333,7 @@ int run_batch(const KeyMaterial *km, size_t tag_len, const BSSL_AMD_BATCH *batch
     memcpy(d.inl_nonce, one->inl_nonce, sizeof(d.inl_nonce));
     memcpy(d.inl_ad, one->inl_ad, sizeof(d.inl_ad));
   }
-  if (launch_desc(km, d, open, stream) != 0) {
+  if (launch_desc(km, d, open, stream, gcm_eng) != 0) {
     PUT_ERROR(ERR_R_INTERNAL_ERROR);
     return 0;
   }
@@ -1340,6 +1357,7 @@ size_t BSSL_AMD_collect_kernel_times(double *out_ms, size_t max) {
 
 int BSSL_AMD_set_aes_gcm_engine(int engine) { return set_gcm_engine(engine); }
 int BSSL_AMD_aes_gcm_engine(void) { return gcm_engine(); }
+int BSSL_AMD_test_set_bs_ek0_producers(int on) { return set_bs_ek0_producers(on != 0) ? 1 : 0; }
 
 size_t BSSL_AMD_gcm_key_tables(const uint8_t *keys, size_t key_len, size_t n, int on_device,
                                uint8_t *out) {
@@ -1490,12 +1508,13 @@ int tls_records(BSSL_AMD_TLS_AEAD *t, const BSSL_AMD_TLS_RECORDS *r, void *strea
       }
     }
     const KernelEvents *ev = timing_pair();
+    const int eng = gcm_engine();
     const int rc = ctx->aead->kind == kAeadAesGcm
                        ? launch_gcm(static_cast<const GcmKeyDev *>(st->km->dev), d, !t->seal,
-                                    st->km->nr, stream, ev)
+                                    st->km->nr, stream, ev, eng)
                        : launch_chacha(static_cast<const ChaChaKeyDev *>(st->km->dev), d,
                                        !t->seal, false, stream, ev);
-    t_timing.last_name = ctx->aead->kind == kAeadAesGcm ? "gcm_kernel" : "chacha_poly_kernel";
+    t_timing.last_name = ctx->aead->kind == kAeadAesGcm ? gcm_kernel_name(eng) : "chacha_poly_kernel";
     ok = rc == 0;
     // TLS 1.2 open reports the header type (tls_record.cc:197-235).
     if (ok && !t->seal && !t->tls13 && r->types)

@@ -1206,15 +1206,15 @@ int set_gcm_engine(int engine) {
   return prev;
 }
 
-bool gcm_takes_one_record_kernel(const BatchDesc &b) {
-  return gcm_engine() != kGcmEngineBitsliced && one_record_batch(b);
+bool gcm_takes_one_record_kernel(const BatchDesc &b, int engine) {
+  return engine != kGcmEngineBitsliced && one_record_batch(b);
 }
 
 int launch_gcm(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, void *stream,
-               const KernelEvents *ev) {
+               const KernelEvents *ev, int engine) {
   if (b.num_records == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (gcm_engine() == kGcmEngineBitsliced) return launch_gcm_bs(keys, b, open, nr, s, ev);
+  if (engine == kGcmEngineBitsliced) return launch_gcm_bs(keys, b, open, nr, s, ev);
   switch (nr) {
     case 10: return open ? launch_nr<10, true>(keys, b, s, ev) : launch_nr<10, false>(keys, b, s, ev);
     case 12: return open ? launch_nr<12, true>(keys, b, s, ev) : launch_nr<12, false>(keys, b, s, ev);

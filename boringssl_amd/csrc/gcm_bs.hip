@@ -24,11 +24,14 @@
 //   GHASH multiply (acc * H^L, whose input is known before the block arrives)
 //   is issued before waiting for the block.
 // * Record start.  J0 and the AD hash by the record's lanes (gcm_common.h).
-//   E_K(J0) by a bitsliced batch per 1,024 records (64 lanes x 16 slots): the
-//   wave that claims a group's producer unit computes the whole group's E_K(J0)
-//   into a per-launch scratch and raises the group's flag; the record end reads
-//   its value (normally long ready).  The producer unit of group g + 1 is the
-//   middle unit of group g, so a group's values are ready half a group ahead.
+//   E_K(J0) by a bitsliced batch per 1,024 records (64 lanes x 16 slots, one
+//   "group"): the wave that claims the middle unit of group g computes the
+//   E_K(J0) of group g + kBsAhead (the first kBsAhead groups by units
+//   0..kBsAhead-1) and writes them as epoch-tagged granules to a per-launch
+//   scratch (zeroed by the launcher); the record end polls its granules
+//   (normally long ready) and, after kBsEk0Polls polls without them, computes
+//   its own E_K(J0) (self_ek0), so no record end depends on another wave for
+//   more than a bounded time.
 // * Record end.  finish_record (gcm_common.h): the lanes' weights H^(L-p), the
 //   L-lane XOR, length block, tag, check and zero-fill.
 #include <hip/hip_runtime.h>
@@ -283,9 +286,10 @@ __device__ __forceinline__ void produce_ek0(const GcmKeyDev *__restrict__ keys, 
 
 // E_K(J0) of processing position i (active lanes): sc1 loads of its two
 // granules until both carry `epoch` (the wave loops until every active lane
-// has its value).  `polls`: the retries.
+// has its value) or `max_polls` retries have passed.  Returns whether every
+// active lane got its value (wave-uniform); `polls`: the retries.
 __device__ __forceinline__ uint4 load_ek0(const uint4 *ek0, uint64_t i, bool active, uint32_t epoch,
-                                          uint32_t &polls) {
+                                          uint32_t max_polls, uint32_t &polls, bool &got) {
   u32x4 g0 = {0, 0, 0, 0}, g1 = {0, 0, 0, 0};
   polls = 0;
   for (;;) {
@@ -298,11 +302,50 @@ __device__ __forceinline__ uint4 load_ek0(const uint4 *ek0, uint64_t i, bool act
                    : "memory");
       ok = g0.y == epoch && g0.w == epoch && g1.y == epoch && g1.w == epoch;
     }
-    if (__ballot(!ok) == 0) break;
+    got = __ballot(!ok) == 0;
+    if (got || polls >= max_polls) break;
     __builtin_amdgcn_s_sleep(4);
     polls++;
   }
   return make_uint4(g0.x, g0.z, g1.x, g1.z);
+}
+
+// Polls of a record end before it computes its own E_K(J0): each is an L2
+// round trip plus a short sleep, so the bound is ~1 ms -- far above the
+// producer's lead in a normal launch (the values are ready ~200 us before the
+// record ends that read them), far below any watchdog.
+#ifndef BS_SELF_EK0
+#define BS_SELF_EK0 1  // (A/B builds: 0 = round 5's unbounded wait, no fallback)
+#endif
+constexpr uint32_t kBsEk0Polls = BS_SELF_EK0 ? 1024u : 0xffffffffu;
+
+// The wave's own E_K(J0) of the lane's record (live lanes; the others get
+// E_K(0^128), unused): one bitsliced batch with the record's J0 in slot 0 of
+// every lane.  The fallback of a record end whose granules did not arrive
+// (load_ek0 returned false), and with production switched off
+// (BSSL_AMD_test_set_bs_ek0_producers) the path of every record end.
+template <int NR>
+__device__ __forceinline__ uint4 self_ek0(const GcmKeyDev *__restrict__ key, const BatchDesc &b,
+                                       uint64_t rec, bool live) {
+  uint4 w[16];
+#pragma unroll
+  for (int s = 0; s < 16; s++) w[s] = make_uint4(0, 0, 0, 0);
+  if (live) {
+    if (b.nonce_len == 12) {
+      const uint4 nn = load_partial(b.nonces + rec * 12, 12);
+      w[0] = make_uint4(nn.x, nn.y, nn.z, 0x01000000u);
+    } else {
+      w[0] = record_j0(b, rec, key->hpow_ct);
+    }
+  }
+  uint32_t rk0[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) rk0[c] = key->rk_plain[0][c];
+  uint32_t p[4][2][8];
+  bs16_load_blocks(p, w, rk0);
+  bs16_cipher_tab<NR>(p, &key->bsmask[0][0]);
+  const v32u KA = bs16_words(p, 0), KB = bs16_words(p, 1);
+  return make_uint4(KA[0], KB[0], KA[16], KB[16]);
 }
 
 // The lane's index in its wave from a volatile asm statement: an opaque value
@@ -338,7 +381,7 @@ enum : int {
 template <int NR, bool OPEN, bool XT, bool IOV, int L>
 __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const BatchDesc &b,
                                         uint64_t first, uint64_t amask, uint8_t *smem,
-                                        const uint4 *ek0, uint32_t epoch) {
+                                        const uint4 *ek0, uint32_t epoch, uint32_t max_polls) {
   static_assert(L == 16 || L == 8 || L == 4 || L == 2, "lanes per record");
   static_assert(!(IOV && XT), "iovec records carry no extra bytes");
 #ifdef BSSL_AMD_BS_PROF
@@ -656,16 +699,11 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
       BS_LAP(4);
       continue;
     }
-    constexpr int kAhead = 4;
-    uint4 kt = make_uint4(0, 0, 0, 0);
-    uint32_t jt = 0xffffffffu;
-    int nv;  // the lane's full blocks of this chunk (hashed in pass 2)
-    // The loads are unconditional (a slot past the lane's full blocks reads
-    // the record's first block again, a valid address), so the plaintext
-    // registers are always defined and no control flow splits the pass; only
-    // the stores are predicated.
+    // iovec records (the contiguous path continued above): pass 1 walks the
+    // chunks with the load / store cursors, pass 2 hashes.  A record's
+    // partial last block is handled inside pass 1 (iov_load2 / iov_gather).
     if constexpr (IOV) {
-      nv = 0;
+      int nv = 0;  // the lane's blocks of this chunk (hashed in pass 2)
 #pragma unroll
       for (int n = 0; n < 16; n++) {
         const uint32_t j = jc + (uint32_t)L * (uint32_t)n;
@@ -721,75 +759,29 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
         KA[16 + n] = cv.z;
         KB[16 + n] = cv.w;
       }
-    } else {
-      const uint8_t *s1 = jc < nfull ? s0 : src;  // (any valid address for the
-      const uint32_t lim = nfull > jc ? (nfull - jc + L - 1) / L : 0u;  // slots past nfull)
-      nv = (int)min(lim, 16u);
-      const int tl = jc < nb ? (int)((nb - 1 - jc) / L) : -1;  // the lane's last slot
-      uint4 xs[16];
+      // (Pass 2 starts here: the pins keep the compiler from hoisting its
+      // lookups into pass 1, whose registers they would need.)
 #pragma unroll
-      for (int n = 0; n < kAhead; n++) xs[n] = load_blk_nt(s1 + (n < nv ? 16 * L * n : 0));
+      for (int k = 0; k < 32; k++) asm volatile("" : "+v"(KA[k]), "+v"(KB[k]));
+      const int gq = (int)(bs_lane() & 15);  // (GHASH lane constants, gcm_common.h Gh8)
+      const bool rs1 = (gq >> 2) & 1, rs2 = (gq >> 3) & 1;
+      const uint32_t rbs = (uint32_t)gq & 3u;
+      uint32_t P[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) v |= (((4u * k + e + gq) & 15u) << 4) << (8 * e);
+        P[k] = v;
+      }
+      uint4 acc = get4(kSacc0);
 #pragma unroll
       for (int n = 0; n < 16; n++) {
-        if (n + kAhead < 16)
-          xs[n + kAhead] = load_blk_nt(s1 + (n + kAhead < nv ? 16 * L * (n + kAhead) : 0));
-        const uint4 x = xs[n];
-        const uint4 y = make_uint4(x.x ^ KA[n], x.y ^ KB[n], x.z ^ KA[16 + n], x.w ^ KB[16 + n]);
-        if (n < nv) store_blk_nt(d0 + 16 * L * n, y);
-        // The partial / extra-byte block (slot tl when it is not full).
-        if (n == tl && n >= nv) {
-          kt = make_uint4(KA[n], KB[n], KA[16 + n], KB[16 + n]);
-          jt = jc + (uint32_t)L * (uint32_t)n;
-        }
-        const uint4 cv = OPEN ? x : y;
-        KA[n] = cv.x;
-        KB[n] = cv.y;
-        KA[16 + n] = cv.z;
-        KB[16 + n] = cv.w;
-      }
-    }
-    // (Pass 2 starts here: the pins keep the compiler from hoisting its
-    // lookups into pass 1, whose registers they would need.)
-#pragma unroll
-    for (int k = 0; k < 32; k++) asm volatile("" : "+v"(KA[k]), "+v"(KB[k]));
-    const int gq = (int)(bs_lane() & 15);  // (GHASH lane constants, gcm_common.h Gh8)
-    const bool rs1 = (gq >> 2) & 1, rs2 = (gq >> 3) & 1;
-    const uint32_t rbs = (uint32_t)gq & 3u;
-    uint32_t P[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int e = 0; e < 4; e++) v |= (((4u * k + e + gq) & 15u) << 4) << (8 * e);
-      P[k] = v;
-    }
-    uint4 acc = get4(kSacc0);
-#pragma unroll
-    for (int n = 0; n < 16; n++) {
-      const uint4 hm = g8_mul(acc, rs1, rs2, rbs, P, smem);
-      if (n < nv) acc = xor4(hm, make_uint4(KA[n], KB[n], KA[16 + n], KB[16 + n]));
-    }
-    if constexpr (!IOV) {
-      // The lane's partial / extra-byte block of this chunk, if any.
-      if (jt != 0xffffffffu) {
-        const uint64_t rec = (uint64_t)get(kSrec) | ((uint64_t)get(kSrecHi) << 32);
-        const RecordMeta m = record_meta(b, rec);
-        const uint32_t xlen = XT ? m.xlen : 0u;
         const uint4 hm = g8_mul(acc, rs1, rs2, rbs, P, smem);
-        const uint32_t nbytes = (uint32_t)umin64(m.len + xlen - (uint64_t)jt * 16, 16);
-        uint4 x, y;
-        if constexpr (XT) {
-          y = crypt_partial_x(src, dst, m.len, batch_extra_in(b, rec), batch_extra_out(b, rec),
-                              (uint64_t)jt * 16, kt, nbytes, x);
-        } else {
-          x = load_partial(src + (uint64_t)jt * 16, nbytes);
-          y = mask_block(xor4(x, kt), nbytes);
-          store_partial(dst + (uint64_t)jt * 16, y, nbytes);
-        }
-        acc = xor4(hm, OPEN ? x : y);
+        if (n < nv) acc = xor4(hm, make_uint4(KA[n], KB[n], KA[16 + n], KB[16 + n]));
       }
+      put4(kSacc0, acc);
     }
-    put4(kSacc0, acc);
   }
   // Record end.
 #if BS_EDGE_PRIO
@@ -810,9 +802,13 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
     atomicMin(&g_bs_grp[first / kBsGroupRecs][2], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
   uint32_t polls;
+  bool got;
   // (Live records only: the producer skips the others, whose output
   // finish_record zero-fills.)
-  const uint4 e0 = load_ek0(ek0, first + bs_lane() / L, act && live, epoch, polls);
+  uint4 e0 = load_ek0(ek0, first + bs_lane() / L, act && live, epoch, max_polls, polls, got);
+#if BS_SELF_EK0
+  if (!got) e0 = self_ek0<NR>(key, b, rec, act && live);  // (wave-uniform)
+#endif
   BS_LAP(8);
 #ifdef BSSL_AMD_BS_PROF
   if ((threadIdx.x & 63) == 0) {
@@ -846,7 +842,7 @@ template <int NR, bool OPEN, bool XT, bool IOV, int L>
 __global__ __launch_bounds__(kBsThreads) void gcm_bs_kernel(const GcmKeyDev *__restrict__ keys,
                                                              BatchDesc b, uint32_t *__restrict__ ctl,
                                                              uint4 *__restrict__ ek0,
-                                                             uint32_t epoch) {
+                                                             uint32_t epoch, uint32_t produce) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[kBsLdsBytes];
   const int tid = threadIdx.x, lane = tid & 63;
 #ifdef BSSL_AMD_BS_PROF
@@ -879,7 +875,7 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_kernel(const GcmKeyDev *__r
     uint32_t pg = 0xffffffffu;
     if (u < kBsAhead && u < kGroupUnits / 2) pg = u;
     if (u % kGroupUnits == kGroupUnits / 2) pg = g + kBsAhead;
-    if (pg != 0xffffffffu && lo + (uint64_t)pg * kBsGroupRecs < n) {
+    if (produce && pg != 0xffffffffu && lo + (uint64_t)pg * kBsGroupRecs < n) {
 #ifdef BSSL_AMD_BS_PROF
       const uint64_t t0 = __builtin_amdgcn_s_memtime();
       const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
@@ -898,7 +894,7 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_kernel(const GcmKeyDev *__r
 #ifdef BSSL_AMD_BS_PROF
     if (lane == 0 && u % kGroupUnits == 0 && g < 4096) g_bs_grp[g][3] = __builtin_amdgcn_s_memrealtime();
 #endif
-    bs_unit<NR, OPEN, XT, IOV, L>(keys, b, first, amask, smem, ek0, epoch);
+    bs_unit<NR, OPEN, XT, IOV, L>(keys, b, first, amask, smem, ek0, epoch, kBsEk0Polls);
   }
 #ifdef BSSL_AMD_BS_PROF
   if (lane == 0) {
@@ -917,7 +913,7 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_kernel(const GcmKeyDev *__r
 template <int NR, bool OPEN, bool XT>
 __global__ __launch_bounds__(kBsThreads) void gcm_bs_keyset_kernel(
     const GcmKeyDev *__restrict__ keys, BatchDesc b, uint32_t *__restrict__ ctl,
-    uint4 *__restrict__ ek0, uint32_t epoch) {
+    uint4 *__restrict__ ek0, uint32_t epoch, uint32_t produce) {
   constexpr int kRecPerTile = 16 * 4;
   __shared__ __attribute__((aligned(16))) uint8_t smem[kBsLdsBytes + 64 * 16 + 16];
   uint32_t *s_pass_key = reinterpret_cast<uint32_t *>(smem + kBsLdsBytes);
@@ -962,7 +958,7 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_keyset_kernel(
         uint32_t pg = 0xffffffffu;
         if (t < kBsAhead && t < kGroupTiles / 2) pg = t;
         if (t % kGroupTiles == kGroupTiles / 2) pg = g + kBsAhead;
-        if (pg != 0xffffffffu && (uint64_t)pg * kBsGroupRecs < n)
+        if (produce && pg != 0xffffffffu && (uint64_t)pg * kBsGroupRecs < n)
           produce_ek0<NR, true>(keys, b, (uint64_t)pg * kBsGroupRecs, n, ek0, epoch);
       }
     }
@@ -980,7 +976,7 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_keyset_kernel(
         loaded = k;
       }
       bs_unit<NR, OPEN, XT, false, 16>(keys + k, b, base + 4 * wave, (mask >> (4 * wave)) & 15u,
-                                       smem, ek0, epoch);
+                                       smem, ek0, epoch, kBsEk0Polls);
     }
   }
 }
@@ -1009,25 +1005,36 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_keyset_kernel(
 constexpr int kBsLongL = BS_LONG_L, kBsShortL = BS_SHORT_L;  // (A/B builds: -DBS_LONG_L=8 ...)
 constexpr int kBsRaggedL = 8;
 
+namespace {
+std::atomic<bool> g_bs_producers{true};
+}  // namespace
+
+bool set_bs_ek0_producers(bool on) { return g_bs_producers.exchange(on); }
+
 int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, hipStream_t s,
                   const KernelEvents *ev) {
   const int num_cus = device_cu_count();
   if (!num_cus) return 1;
   const uint64_t n = b.num_records;
-  // Two control blocks (one per launch of a split batch): the unit counters,
-  // zeroed; then the E_K(J0) granules of every processing position (not
-  // cleared: they carry the launch's epoch, never 0).
+  // Two control blocks (one per launch of a split batch): the unit counters;
+  // then the E_K(J0) granules of every processing position.  All of it is
+  // zeroed: a granule's tag is the launch's epoch (never 0), and a pool
+  // allocation recycled from any earlier use (this library's counters,
+  // flags, histograms) cannot hold a value the poll would take for this
+  // launch's.  n * 32 bytes: ~0.25 % of a 16 KiB-record batch.
   static std::atomic<uint32_t> s_epoch{0};
   uint32_t epoch = s_epoch.fetch_add(1, std::memory_order_relaxed) + 1;
   if (!epoch) epoch = s_epoch.fetch_add(1, std::memory_order_relaxed) + 1;
+  const uint32_t produce = g_bs_producers.load(std::memory_order_relaxed) ? 1u : 0u;
   const size_t ctl_bytes = 256;
+  const size_t scratch_bytes = 2 * ctl_bytes + n * 32;
   uint8_t *scratch = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void **>(&scratch), 2 * ctl_bytes + n * 32, s) != hipSuccess)
+  if (hipMallocAsync(reinterpret_cast<void **>(&scratch), scratch_bytes, s) != hipSuccess)
     return 2;
   uint32_t *ctl = reinterpret_cast<uint32_t *>(scratch);
   uint32_t *ctl2 = reinterpret_cast<uint32_t *>(scratch + ctl_bytes);
   uint4 *ek0 = reinterpret_cast<uint4 *>(scratch + 2 * ctl_bytes);
-  if (hipMemsetAsync(ctl, 0, 2 * ctl_bytes, s) != hipSuccess) {
+  if (hipMemsetAsync(scratch, 0, scratch_bytes, s) != hipSuccess) {
     hipFreeAsync(scratch, s);
     return 2;
   }
@@ -1050,7 +1057,7 @@ int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, 
   if (ev) hipEventRecord(reinterpret_cast<hipEvent_t>(ev->start), s);
   const unsigned grid = (unsigned)((n + 3) / 4 < (uint64_t)num_cus ? (n + 3) / 4 : (uint64_t)num_cus);
   auto go = [&](auto kern, const BatchDesc &d, uint32_t *c) {
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBsThreads), 0, s, keys, d, c, ek0, epoch);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBsThreads), 0, s, keys, d, c, ek0, epoch, produce);
   };
   // Length classes (one-key, not iovec): short uniform records take L = 2;
   // a ragged batch in length order splits at 4 KiB.

@@ -167,8 +167,10 @@ struct KernelEvents {
 
 // Kernel launchers (gcm.hip / chacha.hip).  Return 0 on success or a HIP
 // error code.  `ev` (optional) brackets the bulk kernel.
+// `engine`: the AES-GCM engine for this batch (GcmEngine; the caller reads
+// gcm_engine() once per batch).
 int launch_gcm(const GcmKeyDev *keys, const BatchDesc &b, bool open,
-               int nr, void *stream, const KernelEvents *ev);
+               int nr, void *stream, const KernelEvents *ev, int engine);
 // AES-GCM engine of the bulk path: the bitsliced table-free engine
 // (gcm_bs.hip) or the LDS T-table engine (gcm.hip).  Process-wide; the
 // initial value comes from BSSL_AMD_GCM_MODE ("bs" / "bs16" or "table"),
@@ -178,6 +180,10 @@ int gcm_engine();
 int set_gcm_engine(int engine);  // returns the previous engine, or -1 (bad value)
 int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr,
                   hipStream_t stream, const KernelEvents *ev);
+// Test switch of the table-free engine's batched E_K(J0) production (on by
+// default; off: every record end computes its own after the bounded wait).
+// Returns the previous setting.
+bool set_bs_ek0_producers(bool on);
 // Builds `order` (n entries) grouping records by length class, longest first;
 // `scratch` holds 128 uint32.  Returns 0 or a HIP error code.
 int build_length_order(const uint64_t *lengths, uint64_t n, uint32_t *order, uint32_t *scratch,
@@ -213,7 +219,7 @@ int launch_chacha(const ChaChaKeyDev *keys, const BatchDesc &b, bool open, bool 
                   void *stream, const KernelEvents *ev);
 // Whether launch_gcm / launch_chacha would run this batch on a one-record
 // kernel, the only kernels that write the completion word BatchDesc::done.
-bool gcm_takes_one_record_kernel(const BatchDesc &b);
+bool gcm_takes_one_record_kernel(const BatchDesc &b, int engine);
 bool chacha_takes_one_record_kernel(const BatchDesc &b);
 // tls12 / tls13 nonce checks over a batch of seal calls (tls_scan.hip):
 // writes valid[i] (device) and advances the context's nonce state in place

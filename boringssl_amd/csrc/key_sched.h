@@ -128,13 +128,21 @@ BSSL_GF_HD Gf128 ks_mulx(Gf128 v) {
   return v;
 }
 
-// Wipes key-derived temporaries of the host path (the reference cleanses
-// key state, OPENSSL_cleanse); on the device they are the key-setup lane's
-// own registers.
+// Wipes key-derived temporaries (the reference cleanses key state,
+// OPENSSL_cleanse).  On the device the setup kernel's arrays indexed by the
+// key length (the round keys, the raw key bytes) live in private scratch
+// memory, which outlives the kernel and is handed to later ones unwiped, so
+// the device form overwrites them through volatile stores the compiler cannot
+// drop.
 BSSL_GF_HD void ks_wipe(void *p, size_t n) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  (void)p;
-  (void)n;
+  if (((uintptr_t)p | n) % 4 == 0) {
+    volatile uint32_t *q = static_cast<volatile uint32_t *>(p);
+    for (size_t i = 0; i < n / 4; i++) q[i] = 0;
+  } else {
+    volatile uint8_t *q = static_cast<volatile uint8_t *>(p);
+    for (size_t i = 0; i < n; i++) q[i] = 0;
+  }
 #else
   explicit_bzero(p, n);
 #endif

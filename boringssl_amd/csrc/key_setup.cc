@@ -33,6 +33,7 @@ __global__ __launch_bounds__(64) void gcm_key_setup_kernel(const uint8_t *__rest
   uint8_t k[32];
   for (int j = 0; j < 32; j++) k[j] = j < key_len ? keys[i * key_len + j] : 0;
   gcm_key_tables(k, key_len, out + i);
+  ks_wipe(k, sizeof(k));
 }
 
 }  // namespace

@@ -324,14 +324,8 @@ BSSL_AMD_EXPORT const char *BSSL_AMD_last_kernel_name(void);
 BSSL_AMD_EXPORT int BSSL_AMD_set_aes_gcm_engine(int engine);
 BSSL_AMD_EXPORT int BSSL_AMD_aes_gcm_engine(void);
 
-/* The per-key AES-GCM device tables (internal layout, sizeof GcmKeyDev bytes
- * per key) of n keys of key_len bytes, built on the host (on_device = 0, the
- * EVP_AEAD_CTX_init path) or by the device key-setup kernel (1, the keyset
- * path) and copied to `out`.  Returns n, 0 on error; with out == NULL
- * returns the per-key table size.  Test support: the two paths must agree
- * byte for byte. */
-BSSL_AMD_EXPORT size_t BSSL_AMD_gcm_key_tables(const uint8_t *keys, size_t key_len, size_t n,
-                                               int on_device, uint8_t *out);
+/* Test-only entry points (the internal key-table layout, diagnostic switches)
+ * are declared in bssl_amd/test_hooks.h, not here. */
 
 #ifdef __cplusplus
 }

@@ -10,7 +10,7 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", "bssl_amd", h) for h in ("aead.h", "tls.h")]
+HEADERS = [os.path.join(ROOT, "include", "bssl_amd", h) for h in ("aead.h", "tls.h", "test_hooks.h")]
 
 
 def header_functions():

@@ -165,3 +165,33 @@ def test_bench_layout_vs_oracle(config, records):
     got = w.d_ct[:pt.size].cpu().numpy()
     assert np.array_equal(got, out)
     assert np.array_equal(w.d_tags[:16 * n].cpu().numpy(), tags)
+
+
+# The record end's own E_K(J0) (gcm_bs.hip self_ek0): with
+# the batched production switched off (include/bssl_amd/test_hooks.h), every
+# record end waits its bounded number of polls for granules that never come,
+# then computes its E_K(J0) itself -- one-key (uniform and ragged, both
+# lane counts), keyset and non-96-bit-nonce batches, seal and open.
+@pytest.fixture
+def no_ek0_producers():
+    prev = ba.test_set_bs_ek0_producers(False)
+    yield
+    ba.test_set_bs_ek0_producers(prev)
+
+
+@pytest.mark.parametrize("aead", GCM)
+def test_ek0_fallback_ragged_vs_oracle(aead, no_ek0_producers):
+    par.test_batch_ragged_vs_oracle(aead, "aligned")
+
+
+@pytest.mark.parametrize("multikey", [False, True])
+def test_ek0_fallback_large_ragged(multikey, no_ek0_producers):
+    par.test_batch_large_ragged_reordered("aes-128-gcm", multikey)
+
+
+def test_ek0_fallback_nonce_lengths(no_ek0_producers):
+    par.test_batch_gcm_nonce_lengths_and_truncated_tags()
+
+
+def test_ek0_fallback_bench_layout(no_ek0_producers):
+    test_bench_layout_reference_digest("config2", 4096)
