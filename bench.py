@@ -396,7 +396,9 @@ def load_profile(config, kernel_prefix):
     try:
         d = json.load(open(p)).get(config, {})
         # (the keyset kernel of config 5 is a gcm_kernel for the bench line)
+        # (the table-free engine's lines: gcm_bs_kernel, config 5 gcm_bs_keyset_kernel)
         family = ("gcm_kernel", "gcm_keyset_kernel") if kernel_prefix == "gcm_kernel" else \
+            ("gcm_bs_kernel", "gcm_bs_keyset_kernel") if kernel_prefix == "gcm_bs_kernel" else \
             (kernel_prefix,)
         for k, v in d.items():
             if isinstance(v, dict) and k.startswith(family):

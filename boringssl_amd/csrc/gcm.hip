@@ -794,10 +794,11 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
 // weighted by H^(16 * seg_iters * (nseg - 1 - s)) = the key's prepared
 // power s_gt[nseg - 1 - s], computed per key by one wave); the weighted values
 // are XORed into the record's 16 lane slots in LDS (ds_xor), and the wave
-// whose segment completes the record (an LDS count per record, acquire /
-// release at workgroup scope: its reads see every other segment's XORs and,
-// when opening, their plaintext stores precede its zero-fill of a failed
-// record) computes E_K(J0) and runs the record end.  (The reference handles
+// whose segment completes the record (an LDS count per record after the
+// XORs: LDS operations of a wave complete in order, so its reads see every
+// other segment's XORs; when opening, a release orders each segment's
+// plaintext stores before its count, so they precede the zero-fill of a
+// failed record) computes E_K(J0) and runs the record end.  (The reference handles
 // each key's records independently, gcm.cc.inc:253-296, aead.cc.inc:70-106.)
 constexpr uint32_t kLdsSegSlots = (kLdsBytes + 15u) & ~15u;  // 64 records x 16 lanes x 16 B
 constexpr uint32_t kLdsSegCnt = kLdsSegSlots + 64 * 16 * 16;  // per-record segment counts
@@ -915,14 +916,27 @@ __global__ __launch_bounds__(1024) void gcm_keyset_kernel(const GcmKeyDev *__res
           atomicXor(slot + 1, acc.y);
           atomicXor(slot + 2, acc.z);
           atomicXor(slot + 3, acc.w);
+          asm volatile("" ::: "memory");  // (the XORs stay before the count)
+          // The count after the XORs: a wave's LDS operations complete in
+          // order, so the segment that brings the count to nseg reads every
+          // other segment's XORs.  Opening also orders this segment's
+          // plaintext stores before the count (release: they complete before
+          // the record's last segment may zero-fill it); sealing needs only
+          // the LDS order.
           uint32_t old = 0;
-          if (q == 0)
-            old = __hip_atomic_fetch_add(s_cnt + t, 1u, __ATOMIC_ACQ_REL,
-                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (q == 0) {
+            if constexpr (OPEN)
+              old = __hip_atomic_fetch_add(s_cnt + t, 1u, __ATOMIC_RELEASE,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+            else
+              old = __hip_atomic_fetch_add(s_cnt + t, 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
           const bool fin = __shfl(old, lane & 48, 64) == (uint32_t)nseg - 1;
           if (__ballot(fin) == 0) continue;
-          // Record end of the groups whose record this segment completed.
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          // Record end of the groups whose record this segment completed
+          // (the slot reads stay after the count: compiler barrier).
+          asm volatile("" ::: "memory");
           const RecordMeta &m = in.m;
           uint4 j0 = make_uint4(0, 0, 0, 0);
           if (in.live) {

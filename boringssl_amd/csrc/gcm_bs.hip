@@ -103,8 +103,8 @@ constexpr uint32_t kBsLdsBytes = kBsLdsSink + 256;
 #endif
 // Launch control words (zeroed by the launcher): the unit counter.
 // E_K(J0) of processing position i: four data-tagged 8-byte granules {E word
-// k, epoch} at ek0[2i], ek0[2i + 1] (two per 16-byte write-through (sc1)
-// store), read by sc1 loads until all four carry this launch's epoch (a
+// k, epoch} at ek0[2i] (words 0 and 2), ek0[2i + 1] (words 1 and 3), two per
+// 16-byte write-through (sc1) store, read by sc1 loads until all four carry this launch's epoch (a
 // per-launch number): no flag, no ordering, no reliance on a 16-byte store
 // landing whole, and a line left in an XCD's L2 by an earlier launch cannot
 // pass for this one's (MI355X_MICROARCH.md, inter-workgroup visibility:
@@ -214,7 +214,7 @@ __device__ __forceinline__ uint4 g8_mul(uint4 x, bool rs1, bool rs2, uint32_t rb
 // that key's masks per lane; one-key batches take one cipher with the key's
 // wave-uniform masks.  Results to the granules of ek0 (above).
 template <int NR, bool KS>
-__device__ __forceinline__ void produce_ek0(const GcmKeyDev *__restrict__ keys, const BatchDesc &b,
+__device__ __forceinline__ void produce_ek0_ks(const GcmKeyDev *__restrict__ keys, const BatchDesc &b,
                                          uint64_t i0, uint64_t end, uint4 *__restrict__ ek0,
                                          uint32_t epoch) {
   const int lane = threadIdx.x & 63;
@@ -269,7 +269,7 @@ __device__ __forceinline__ void produce_ek0(const GcmKeyDev *__restrict__ keys, 
 #pragma unroll
     for (int s = 0; s < 16; s++)
       if ((mine >> s) & 1u) {
-        const u32x4 g0 = {KA[s], epoch, KB[s], epoch}, g1 = {KA[16 + s], epoch, KB[16 + s], epoch};
+        const u32x4 g0 = {KA[s], epoch, KA[16 + s], epoch}, g1 = {KB[s], epoch, KB[16 + s], epoch};
         // (s_nop 1: a store of more than 8 bytes reads its data registers a
         // cycle late, and the compiler's hazard check does not see inside
         // inline asm -- without it the next VALU write of those registers
@@ -281,6 +281,100 @@ __device__ __forceinline__ void produce_ek0(const GcmKeyDev *__restrict__ keys, 
       }
     todo &= ~mine;
   }
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <int NR, bool KS>
+__device__ __forceinline__ void produce_ek0(const GcmKeyDev *__restrict__ keys, const BatchDesc &b,
+                                         uint64_t i0, uint64_t end, uint4 *__restrict__ ek0,
+                                         uint32_t epoch) {
+  if constexpr (KS) {
+    produce_ek0_ks<NR, true>(keys, b, i0, end, ek0, epoch);
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  const uint64_t base = i0 + 16u * (uint64_t)lane;
+  // Top priority while producing (as produce_ek0_ks).
+  __builtin_amdgcn_s_setprio(3);
+  // The live slots (and, for keysets, their keys).  No J0 array is kept: each
+  // cipher pass re-reads its slots' nonces straight into the round-0
+  // transpose inputs, so the 64 words of 16 J0 blocks are never live beside
+  // the cipher state (kept, they spilled: 162 of the kernel's 178 VGPR
+  // spills were here).
+  uint32_t todo = 0;
+#pragma unroll
+  for (int s = 0; s < 16; s++) {
+    const uint64_t i = base + s;
+    if (i < end) {
+      const uint64_t rec = rec_at(b, i);
+      if (record_live(b, rec, record_meta(b, rec))) todo |= 1u << s;
+    }
+  }
+  auto key_of = [&](int s) -> uint32_t {  // (KS: a live slot's key)
+    return KS ? b.key_index[rec_at(b, base + s)] : 0u;
+  };
+  do {
+    uint32_t mine = todo, k = 0;
+    if constexpr (KS) {
+      k = todo ? key_of(__builtin_ctz(todo)) : 0u;
+      mine = 0;
+#pragma unroll
+      for (int s = 0; s < 16; s++)
+        if ((todo >> s) & 1u) mine |= (uint32_t)(key_of(s) == k) << s;
+    }
+    const GcmKeyDev *key = keys + k;
+    // Round 0, one state pair at a time (pair h: columns h and h + 2 of
+    // J0 ^ rk0 through one 32x32 transpose; the nonces are read once per pair).
+    uint32_t p[4][2][8];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t ra = key->rk_plain[0][h], rb = key->rk_plain[0][h + 2];
+      uint32_t t[32];
+#pragma unroll
+      for (int s = 0; s < 16; s++) {
+        uint4 j0 = make_uint4(0, 0, 0, 0);
+        if ((mine >> s) & 1u) {
+          const uint64_t rec = rec_at(b, base + s);
+          if (b.nonce_len == 12) {
+            const uint4 nn = load_partial(b.nonces + rec * 12, 12);
+            j0 = make_uint4(nn.x, nn.y, nn.z, 0x01000000u);
+          } else {
+            j0 = record_j0(b, rec, key->hpow_ct);
+          }
+        }
+        t[s] = (h ? j0.y : j0.x) ^ ra;
+        t[16 + s] = (h ? j0.w : j0.z) ^ rb;
+      }
+      transpose32(t);
+#pragma unroll
+      for (int q = 0; q < 32; q++) p[q / 8][h][q % 8] = t[q];
+    }
+    if constexpr (KS)
+      bs16_cipher<NR, false>(p, &key->rk_plain[0][0]);
+    else
+      bs16_cipher_tab<NR>(p, &key->bsmask[0][0]);
+    // Granule quad 0 = {E word 0, epoch, E word 2, epoch} comes from pair 0
+    // of the state alone and quad 1 = {E word 1, epoch, word 3, epoch} from
+    // pair 1, so each half is stored as soon as its transpose is done and the
+    // two never hold 64 registers together.
+    auto store_half = [&](const v32u &K, int half) {
+#pragma unroll
+      for (int s = 0; s < 16; s++)
+        if ((mine >> s) & 1u) {
+          const u32x4 g = {K[s], epoch, K[16 + s], epoch};
+          // (s_nop 1: a store of more than 8 bytes reads its data registers a
+          // cycle late, and the compiler's hazard check does not see inside
+          // inline asm -- without it the next VALU write of those registers
+          // went into the granule.)
+          asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc1\n\ts_nop 1"
+                       ::"v"(ek0 + 2 * (base + s)), "v"(g), "i"(16 * half)
+                       : "memory");
+        }
+    };
+    store_half(bs16_words(p, 0), 0);
+    store_half(bs16_words(p, 1), 1);
+    todo &= ~mine;
+  } while (KS && __ballot(todo != 0));
   __builtin_amdgcn_s_setprio(0);
 }
 
@@ -307,7 +401,7 @@ __device__ __forceinline__ uint4 load_ek0(const uint4 *ek0, uint64_t i, bool act
     __builtin_amdgcn_s_sleep(4);
     polls++;
   }
-  return make_uint4(g0.x, g0.z, g1.x, g1.z);
+  return make_uint4(g0.x, g1.x, g0.z, g1.z);  // (quad 0: words 0, 2; quad 1: words 1, 3)
 }
 
 // Polls of a record end before it computes its own E_K(J0): each is an L2
@@ -672,7 +766,14 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
 #undef BS_IO
       BS_LAP(3);
       if (tl >= 0) {
-        const uint32_t jt = jc + (uint32_t)L * (uint32_t)tl;
+        // (The record's buffers re-derived from the parked offset: kept live
+        // across the pass, the two pointers spilled once per chunk.)
+        const uint32_t jt = (uint32_t)(16 * L) * (uint32_t)c + (bs_lane() & (L - 1)) +
+                            (uint32_t)L * (uint32_t)tl;
+        const uint4 rt = get4(kSnb);
+        const uint64_t offt = (uint64_t)rt.z | ((uint64_t)rt.w << 32);
+        const uint8_t *src = b.in + offt;
+        uint8_t *dst = b.out + offt;
         const uint64_t rec = (uint64_t)get(kSrec) | ((uint64_t)get(kSrecHi) << 32);
         const RecordMeta m = record_meta(b, rec);
         const uint32_t xlen = XT ? m.xlen : 0u;

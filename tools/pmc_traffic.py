@@ -21,7 +21,8 @@ import os
 import re
 import sys
 
-CALIB_PATTERNS = ("copy_stream", "copy_chacha", "copy_quad", "copy_gcm", "copy_gcm8")
+CALIB_PATTERNS = ("copy_stream", "copy_chacha", "copy_quad", "copy_gcm", "copy_gcm8",
+                  "copy_quad_slow")
 # Record geometry of each config's bench layout (length x stride): the
 # counters' ratio to the bytes moved depends on it, so every config reads the
 # calibration copy of its own geometry (calib_{fetch,write}_LENxSTRIDExRECS).
@@ -139,6 +140,7 @@ def main():
         geo = m.group(2)
         for (k, _), c in load(os.path.join(src, sub)).items():
             name = {"copy_rec4<0>": "copy_chacha", "copy_rec4<1>": "copy_quad",
+                    "copy_rec4<2>": "copy_quad_slow",
                     "copy_gcm<16>": "copy_gcm", "copy_gcm<8>": "copy_gcm8"}.get(k, k.split("<")[0])
             if name not in CALIB_PATTERNS or key not in c:
                 continue
@@ -155,7 +157,7 @@ def main():
     calib_now = res.get("calibration", {})
     per_cfg = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(list)))
     for sub in sorted(os.listdir(src)):
-        m = re.match(r"pmc_(config\w+?)_(fetch|write|sq)$", sub)
+        m = re.match(r"(?:bs_)?pmc_(config\w+?)_(fetch|write|sq)$", sub)
         if not m:
             continue
         for k, c in load(os.path.join(src, sub)).items():
@@ -169,8 +171,17 @@ def main():
                 geo = "1350x1408" if calib_pattern(full) == "copy_quad" else "16384x16384"
             cal = next((v for g, v in calib_now.items() if geo and g.startswith(geo + "x")), None)
             fam[family].append(summarise(c, full, cal))
-        res[cfg] = {k: combine(v) for k, v in fam.items()}
-        res[cfg]["source"] = src
+        # Merge by kernel family: a pass over one engine (ENGINE=bs runs of
+        # tools/profile.sh) keeps the other engine's entries of the config.
+        cur = res.get(cfg, {}) if isinstance(res.get(cfg), dict) else {}
+        old_src = cur.pop("source", None)
+        for k in cur:
+            if isinstance(cur[k], dict) and old_src:
+                cur[k].setdefault("source", old_src)
+        for k, v in fam.items():
+            cur[k] = combine(v)
+            cur[k]["source"] = src
+        res[cfg] = cur
     json.dump(res, open(dst, "w"), indent=1, sort_keys=True)
     for cfg, ks in res.items():
         if not isinstance(ks, dict):

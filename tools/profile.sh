@@ -7,7 +7,12 @@
 # step has its own time limit; the chain stops at the first failure.
 # Summarise the PMC passes with: tools/pmc_traffic.py $O [profiles/traffic.json]
 #   O=gpurun_out/r03a CONFIGS="config2 config3" PASSES="stats pmc" tools/profile.sh
+# ENGINE=bs: the AES-GCM configs on the table-free engine (BSSL_AMD_GCM_MODE=bs,
+# kernels gcm_bs_kernel / gcm_bs_keyset_kernel), output dirs prefixed bs_.
 set -u
+ENGINE=${ENGINE:-table}
+EP=""
+if [ "$ENGINE" = bs ]; then export BSSL_AMD_GCM_MODE=bs; EP=bs_; fi
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 O=${O:-gpurun_out/prof}
 CONFIGS=${CONFIGS:-config2 config3 config3x config4 config5 configS}
@@ -37,16 +42,17 @@ if has calib; then
 fi
 for cfg in $CONFIGS; do
   case $cfg in config3|config3x) K=chacha_poly_kernel ;; configS) K=gcm_siv_kernel ;; config5) K=gcm_keyset_kernel ;; *) K=gcm_kernel ;; esac
+  if [ "$ENGINE" = bs ]; then case $cfg in config5) K=gcm_bs_keyset_kernel ;; *) K=gcm_bs_kernel ;; esac; fi
   if has stats; then
-    step stats_$cfg 300 rocprofv3 --kernel-trace --stats -d $O/prof_$cfg -o run --output-format csv -- \
+    step ${EP}stats_$cfg 300 rocprofv3 --kernel-trace --stats -d $O/${EP}prof_$cfg -o run --output-format csv -- \
       python3 bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline --no-parity
   fi
   if has pmc; then
     B="python3 bench.py --config $cfg --steps 2 --warmup 1 --no-cpu-baseline --no-parity"
-    step pmc_${cfg}_fetch 200 rocprofv3 --kernel-include-regex $K --pmc FETCH_SIZE -d $O/pmc_${cfg}_fetch -o run --output-format csv -- $B
-    step pmc_${cfg}_write 200 rocprofv3 --kernel-include-regex $K --pmc WRITE_SIZE -d $O/pmc_${cfg}_write -o run --output-format csv -- $B
-    step pmc_${cfg}_sq 200 rocprofv3 --kernel-include-regex $K --pmc SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU \
-      SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_WAVES GRBM_GUI_ACTIVE -d $O/pmc_${cfg}_sq -o run --output-format csv -- $B
+    step ${EP}pmc_${cfg}_fetch 200 rocprofv3 --kernel-include-regex $K --pmc FETCH_SIZE -d $O/${EP}pmc_${cfg}_fetch -o run --output-format csv -- $B
+    step ${EP}pmc_${cfg}_write 200 rocprofv3 --kernel-include-regex $K --pmc WRITE_SIZE -d $O/${EP}pmc_${cfg}_write -o run --output-format csv -- $B
+    step ${EP}pmc_${cfg}_sq 200 rocprofv3 --kernel-include-regex $K --pmc SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU \
+      SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_WAVES GRBM_GUI_ACTIVE -d $O/${EP}pmc_${cfg}_sq -o run --output-format csv -- $B
   fi
   if has e2e; then
     case $cfg in
