@@ -74,7 +74,7 @@ EXPORTED_SYMBOLS = [
     "BSSL_AMD_set_kernel_timing", "BSSL_AMD_collect_kernel_times", "BSSL_AMD_last_kernel_ms",
     "BSSL_AMD_last_kernel_name", "BSSL_AMD_set_aes_gcm_engine", "BSSL_AMD_aes_gcm_engine",
     # include/bssl_amd/test_hooks.h (test support, not part of the EVP surface)
-    "BSSL_AMD_gcm_key_tables", "BSSL_AMD_test_set_bs_ek0_producers",
+    "BSSL_AMD_gcm_key_tables", "BSSL_AMD_test_set_bs_ek0_producers", "BSSL_AMD_test_set_gcm_mix",
     # include/bssl_amd/tls.h
     "BSSL_AMD_TLS_AEAD_new", "BSSL_AMD_TLS_AEAD_free", "BSSL_AMD_TLS_AEAD_prefix_len",
     "BSSL_AMD_TLS_AEAD_suffix_len", "BSSL_AMD_TLS_AEAD_sequence",
@@ -169,6 +169,7 @@ _SIGS = {
     "BSSL_AMD_aes_gcm_engine": (_I, []),
     "BSSL_AMD_gcm_key_tables": (_S, [_P, _S, _S, _I, _P]),
     "BSSL_AMD_test_set_bs_ek0_producers": (_I, [_I]),
+    "BSSL_AMD_test_set_gcm_mix": (_I, [_I]),
     "BSSL_AMD_TLS_AEAD_new": (_P, [_I, ctypes.c_uint16, _P, _P, _S, _P, _S, ctypes.c_uint64]),
     "BSSL_AMD_TLS_AEAD_free": (None, [_P]),
     "BSSL_AMD_TLS_AEAD_prefix_len": (_S, [_P]),
@@ -484,6 +485,8 @@ def collect_kernel_times(max_n=4096):
 
 
 AES_GCM_ENGINES = {"table": 0, "bs": 1}
+# (2: the experimental mixed engine, selected only by BSSL_AMD_GCM_MODE=mixN)
+_ENGINE_NAMES = {0: "table", 1: "bs", 2: "mix"}
 
 
 def gcm_key_tables(keys, key_len, on_device):
@@ -508,7 +511,7 @@ def set_aes_gcm_engine(engine):
     prev = _lib.BSSL_AMD_set_aes_gcm_engine(AES_GCM_ENGINES[engine])
     if prev < 0:
         raise RuntimeError(f"BSSL_AMD_set_aes_gcm_engine refused {engine!r}")
-    return {v: k for k, v in AES_GCM_ENGINES.items()}[prev]
+    return _ENGINE_NAMES[prev]
 
 
 def test_set_bs_ek0_producers(on):
@@ -519,8 +522,17 @@ def test_set_bs_ek0_producers(on):
     return bool(_lib.BSSL_AMD_test_set_bs_ek0_producers(1 if on else 0))
 
 
+def test_set_gcm_mix(bitsliced_waves):
+    """Test support: selects the experimental mixed-role engine
+    (include/bssl_amd/test_hooks.h); returns the previous engine's name."""
+    prev = _lib.BSSL_AMD_test_set_gcm_mix(bitsliced_waves)
+    if prev < 0:
+        raise ValueError(bitsliced_waves)
+    return _ENGINE_NAMES[prev]
+
+
 def aes_gcm_engine():
-    return {v: k for k, v in AES_GCM_ENGINES.items()}[_lib.BSSL_AMD_aes_gcm_engine()]
+    return _ENGINE_NAMES[_lib.BSSL_AMD_aes_gcm_engine()]
 
 
 def last_kernel_name():

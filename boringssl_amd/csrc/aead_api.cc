@@ -259,7 +259,9 @@ const KernelEvents *timing_pair() {
 // Name of the dominant kernel of an AES-GCM launch on `engine` (the timing
 // records and bench.py's profile lookup key on it).
 const char *gcm_kernel_name(int engine) {
-  return engine == kGcmEngineBitsliced ? "gcm_bs_kernel" : "gcm_kernel";
+  return engine == kGcmEngineBitsliced ? "gcm_bs_kernel"
+         : engine == kGcmEngineMix        ? "gcm_mix_kernel"
+                                          : "gcm_kernel";
 }
 
 // Launch the bulk kernels of the AEAD over a filled-in descriptor.  Returns 0
@@ -1358,6 +1360,7 @@ size_t BSSL_AMD_collect_kernel_times(double *out_ms, size_t max) {
 int BSSL_AMD_set_aes_gcm_engine(int engine) { return set_gcm_engine(engine); }
 int BSSL_AMD_aes_gcm_engine(void) { return gcm_engine(); }
 int BSSL_AMD_test_set_bs_ek0_producers(int on) { return set_bs_ek0_producers(on != 0) ? 1 : 0; }
+int BSSL_AMD_test_set_gcm_mix(int bitsliced_waves) { return set_gcm_mix(bitsliced_waves); }
 
 size_t BSSL_AMD_gcm_key_tables(const uint8_t *keys, size_t key_len, size_t n, int on_device,
                                uint8_t *out) {

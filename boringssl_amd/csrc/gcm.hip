@@ -446,20 +446,12 @@ constexpr bool kIovHandoff = GCM_IOV_HANDOFF != 0;
 #endif
 constexpr bool kIovKeepEnd = GCM_IOV_KEEP_END != 0;
 
-// SEG (the keyset kernel's record segments, gcm_keyset_kernel): only the
-// iterations [it0, it1) of the records (blocks it*L + q; in.x0 holds block
-// it0*L + q), the AD hash folded in only by the segment that starts at 0, no
-// E_K(J0) and no record end -- the lane's accumulator over the segment is
-// returned for the caller to weight and combine.  Otherwise the whole record
-// and its end (the return value is unused).
-template <int NR, bool OPEN, bool XT, int L = 16, bool RP = false, bool IOV = false,
-          bool SEG = false>
-__device__ __forceinline__ uint4 process_records(const RoundKeys &rk, const BatchDesc &b,
-                                                 const UnitIn &in, const uint8_t *smem,
-                                                 const GcmKeyDev *key, uint32_t lc0, uint32_t lc1,
-                                                 int prio_base = 0, int it0 = 0, int it1 = 0) {
+template <int NR, bool OPEN, bool XT, int L = 16, bool RP = false, bool IOV = false>
+__device__ __forceinline__ void process_records(const RoundKeys &rk, const BatchDesc &b,
+                                                const UnitIn &in, const uint8_t *smem,
+                                                const GcmKeyDev *key, uint32_t lc0, uint32_t lc1,
+                                                int prio_base = 0) {
   static_assert(L == 16 || L == 8 || L == 4, "lanes per record");
-  static_assert(!SEG || (!IOV && !XT), "segments of plain records");
   const int q = threadIdx.x & (L - 1);
   const uint64_t rec = in.rec;
   const bool active = in.active, live = in.live;
@@ -472,7 +464,7 @@ __device__ __forceinline__ uint4 process_records(const RoundKeys &rk, const Batc
     else
       j0 = record_j0(b, rec, key->hpow_ct);
   }
-  const bool many_ad = (!SEG || it0 == 0) && __ballot(live && m.ad_len > 16) != 0;
+  const bool many_ad = __ballot(live && m.ad_len > 16) != 0;
   const uint4 ya = many_ad ? record_ad_hash<L>(b, rec, m, live, true, key->hpow_ct) : in.ad0;
   // (< 2^32: the GCM length limit holds for a live record)
   const uint32_t nb = live ? (uint32_t)((m.len + m.xlen + 15) / 16) : 0u;
@@ -485,12 +477,10 @@ __device__ __forceinline__ uint4 process_records(const RoundKeys &rk, const Batc
   const uint32_t c0 = j0.x ^ rk.w[0][0], c1 = j0.y ^ rk.w[0][1], c2 = j0.z ^ rk.w[0][2];
   // E_K(J0), one column per lane of each quad (from the same bank-replicated
   // LDS tables; computed while the unit's first block is in flight).
-  uint32_t ek0w = 0;
-  if constexpr (!SEG)
-    ek0w = ek0_quad<NR, 0>(c0, c1, c2, bswap32(ctr0) ^ rk.w[0][3], rk, smem, lc0, lc1);
+  const uint32_t ek0w = ek0_quad<NR, 0>(c0, c1, c2, bswap32(ctr0) ^ rk.w[0][3], rk, smem, lc0, lc1);
   const uint8_t *src = b.in + m.off;
   uint8_t *dst = b.out + m.off;
-  uint4 acc = (q == L - 1 && live && (!SEG || it0 == 0)) ? ya : make_uint4(0, 0, 0, 0);
+  uint4 acc = (q == L - 1 && live) ? ya : make_uint4(0, 0, 0, 0);
   // GHASH lane constants (Gh8): rotation by gq bytes and the slot offsets.
   // gq = the lane's index in its 16-lane row whatever L is: the 16 lanes of a
   // ds_read_b128 lane group then always read 16 different slots (the
@@ -514,8 +504,7 @@ __device__ __forceinline__ uint4 process_records(const RoundKeys &rk, const Batc
   const uint32_t k0 = tload<T>(smem, taddr<0>(lc0, c0)) ^ tload<T>(smem, taddr<1>(lc1, c1)) ^
                       rotl(tload<T>(smem, taddr<2>(lc0, c2)) ^ rk.w[1][0], 16);
   WindowCache wc;
-  int iters = group_max<L>((int)((nb + L - 1) / L));
-  if constexpr (SEG) iters = min(iters, it1);
+  const int iters = group_max<L>((int)((nb + L - 1) / L));
   // Full 16-byte blocks of this lane's record, at any alignment (one
   // dwordx4 each, load_blk_nt); the partial last block takes the byte path.
   // (iovec records: their own paths below.)
@@ -607,7 +596,7 @@ __device__ __forceinline__ uint4 process_records(const RoundKeys &rk, const Batc
   // block j + 16 are interleaved with this block's rounds 3..NR.
   uint32_t cur[4];
   {
-    const uint32_t ctr = ctr0 + 1u + (uint32_t)(SEG ? it0 * L : 0) + (uint32_t)q;  // block q
+    const uint32_t ctr = ctr0 + 1u + (uint32_t)q;  // block q
     const uint32_t s3 = bswap32(ctr) ^ rk.w[0][3];
     wc.update<T>(ctr, s3, c0, c1, c2, rk, smem, lc0, lc1);
     wc.rounds12<T>(k0, s3, cur[0], cur[1], cur[2], cur[3], smem, lc0, lc1);
@@ -694,7 +683,7 @@ __device__ __forceinline__ uint4 process_records(const RoundKeys &rk, const Batc
     x0 = load_full(q);
   else
     x0 = in.x0;
-  int it = SEG ? it0 : 0;
+  int it = 0;
   for (; it + 1 < iters; it += 2) {
     const uint4 x1 = load_full((uint64_t)(it + 1) * L + q);
     step(it, x0);
@@ -702,10 +691,8 @@ __device__ __forceinline__ uint4 process_records(const RoundKeys &rk, const Batc
     step(it + 1, x1);
   }
   if (it < iters) step(it, x0);
-  if constexpr (!SEG)
-    finish_record<OPEN, L>(acc, nb, m, quad_gather(ek0w), b, rec, active, live, dst,
-                           key->hpow_ct);
-  return acc;
+  finish_record<OPEN, L>(acc, nb, m, quad_gather(ek0w), b, rec, active, live, dst,
+                         key->hpow_ct);
 }
 
 // The AES tables of the bulk kernels, replicated per bank: entry idx, slot t,
@@ -778,43 +765,13 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
 // records are visited in tiles of W * 4; a tile whose records use several
 // keys is processed in one pass per distinct key, since the LDS byte table is
 // per key.
-//
-// Record segments (round 6).  A tile of one key's 64
-// records used to be 16 units of 4 whole records, one per wave: the SIMD
-// arbiter favours older waves (1.6-1.9x skew), so the tile lasted as long as
-// its slowest wave's 4 records and the others idled at the next tile's
-// barrier (config 5: SQ_WAIT_ANY 44 % against 26 % for config 2).  When every
-// record of the batch has the same length, a multiple of nseg * seg_iters * 16
-// blocks, and a tile holds one key's 64 records, the tile is split into
-// 16 * nseg units (4 records x one segment of seg_iters iterations), claimed
-// from an LDS counter, so a fast wave takes more of them and the tile ends at
-// most one short segment after its average.  A segment's lane accumulator
-// covers its blocks by Horner's rule at stride H^16 (GHASH is linear: the
-// record's accumulator is the XOR of the segments' accumulators, segment s
-// weighted by H^(16 * seg_iters * (nseg - 1 - s)) = the key's prepared
-// power s_gt[nseg - 1 - s], computed per key by one wave); the weighted values
-// are XORed into the record's 16 lane slots in LDS (ds_xor), and the wave
-// whose segment completes the record (an LDS count per record after the
-// XORs: LDS operations of a wave complete in order, so its reads see every
-// other segment's XORs; when opening, a release orders each segment's
-// plaintext stores before its count, so they precede the zero-fill of a
-// failed record) computes E_K(J0) and runs the record end.  (The reference handles
-// each key's records independently, gcm.cc.inc:253-296, aead.cc.inc:70-106.)
-constexpr uint32_t kLdsSegSlots = (kLdsBytes + 15u) & ~15u;  // 64 records x 16 lanes x 16 B
-constexpr uint32_t kLdsSegCnt = kLdsSegSlots + 64 * 16 * 16;  // per-record segment counts
-constexpr uint32_t kLdsSegUnit = kLdsSegCnt + 64 * 4;         // unit counter, tile flag
-constexpr uint32_t kLdsSegPow = kLdsSegUnit + 16;             // up to kMaxSegs prepared powers
-constexpr int kMaxSegs = 8;
-constexpr uint32_t kLdsKeysetBytes = kLdsSegPow + kMaxSegs * 16;
-
 template <int NR, bool OPEN, bool XT, int W>
 __global__ __launch_bounds__(1024) void gcm_keyset_kernel(const GcmKeyDev *__restrict__ keys,
-                                                           BatchDesc b, int nseg, int seg_iters) {
+                                                           BatchDesc b) {
   constexpr int kThreads = W * 64;
   constexpr int kRecPerTile = W * kRecPerWave;
   static_assert(kRecPerTile <= 64, "one wave plans a tile with ballots");
-  static_assert(kRecPerTile == 64 || XT, "segmented tiles hold 64 records");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[XT ? kLdsBytes : kLdsKeysetBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
   // Pass list of the current tile: key and 64-bit record mask per pass.
   uint32_t *s_pass_key = reinterpret_cast<uint32_t *>(smem + kLdsPlan);
   uint64_t *s_pass_mask = reinterpret_cast<uint64_t *>(smem + kLdsPlan + 64 * 4);
@@ -828,12 +785,6 @@ __global__ __launch_bounds__(1024) void gcm_keyset_kernel(const GcmKeyDev *__res
   const uint32_t lc1 = lc0 + 128u;
   uint32_t loaded = 0xffffffffu;
   const uint64_t n = b.num_records;
-  // (Segments: XT batches never take them -- the launcher passes nseg 0.)
-  uint4 *s_slot = reinterpret_cast<uint4 *>(smem + kLdsSegSlots);
-  uint32_t *s_cnt = reinterpret_cast<uint32_t *>(smem + kLdsSegCnt);
-  uint32_t *s_unit = reinterpret_cast<uint32_t *>(smem + kLdsSegUnit);
-  if constexpr (!XT)
-    for (int e = tid; e < 64 * 16; e += kThreads) s_slot[e] = make_uint4(0, 0, 0, 0);
   for (uint64_t base = (uint64_t)blockIdx.x * kRecPerTile; base < n;
        base += (uint64_t)gridDim.x * kRecPerTile) {
     __syncthreads();
@@ -855,112 +806,10 @@ __global__ __launch_bounds__(1024) void gcm_keyset_kernel(const GcmKeyDev *__res
         pending &= ~mask;
         np++;
       }
-      // A segmented tile: one key for all 64 records.
-      const bool segt = !XT && nseg > 1 && np == 1 && __ballot(k != 0xffffffffu) == ~0ull;
-      if (lane == 0) {
-        *s_npass = segt ? -np : np;
-        if constexpr (!XT) s_unit[0] = 0;
-      }
-      if constexpr (!XT) s_cnt[lane] = 0;
+      if (lane == 0) *s_npass = np;
     }
     __syncthreads();
-    const int npass_s = *s_npass;
-    if constexpr (!XT) {
-      if (npass_s < 0) {
-        const uint32_t k = __builtin_amdgcn_readfirstlane(s_pass_key[0]);
-        Gf128 *s_pow = reinterpret_cast<Gf128 *>(smem + kLdsSegPow);
-        if (k != loaded) {
-          __syncthreads();
-          build_g8<kThreads>(smem, reinterpret_cast<const uint4 *>(keys[k].htab16), tid);
-          if (wave == 0) {
-            // s_pow[t] = prepared H^(16 * seg_iters * t), lane t (< nseg).
-            Gf128 one = {{0u, 0u, 0u, 0x80000000u}};
-            const Gf128 h16 = gf_mul(one, gf_load(keys[k].hpow_ct[16]));
-            Gf128 step = one, sq = h16;  // step = H^(16 * seg_iters), square-and-multiply
-            for (int e = seg_iters; e; e >>= 1) {
-              if (e & 1) step = gf_mul(step, gf_prep(sq));
-              sq = gf_mul(sq, gf_prep(sq));
-            }
-            Gf128 r = one;
-            const Gf128 sp = gf_prep(step);
-            for (int t = 0; t < kMaxSegs - 1; t++)
-              if (t < lane) r = gf_mul(r, sp);
-            if (lane < kMaxSegs) s_pow[lane] = gf_prep(r);
-          }
-          __syncthreads();
-          loaded = k;
-        }
-        RoundKeys rk;
-#pragma unroll
-        for (int r = 0; r <= NR; r++)
-#pragma unroll
-          for (int c = 0; c < 4; c++) rk.w[r][c] = keys[k].rk[r][c];
-        const int q = lane & 15;
-        for (;;) {
-          uint32_t u = 0;
-          if (lane == 0) u = atomicAdd(s_unit, 1u);
-          u = __builtin_amdgcn_readfirstlane(u);
-          if (u >= 16u * (uint32_t)nseg) break;
-          const int sidx = (int)(u >> 4);
-          const int t = 4 * (int)(u & 15u) + g;  // the group's record in the tile
-          const int it0 = sidx * seg_iters;
-          UnitIn in;
-          unit_load<false, false>(in, b, base + t, q, n, (uint64_t)it0 * 16);
-          uint4 acc = process_records<NR, OPEN, false, 16, true, false, true>(
-              rk, b, in, smem, keys + k, lc0, lc1, wave >> 2, it0, it0 + seg_iters);
-          __builtin_amdgcn_s_setprio(0);
-          if (sidx != nseg - 1)
-            acc = from_gf(gf_mul(to_gf(acc), s_pow[nseg - 1 - sidx]));
-          uint32_t *slot = reinterpret_cast<uint32_t *>(s_slot + t * 16 + q);
-          atomicXor(slot + 0, acc.x);
-          atomicXor(slot + 1, acc.y);
-          atomicXor(slot + 2, acc.z);
-          atomicXor(slot + 3, acc.w);
-          asm volatile("" ::: "memory");  // (the XORs stay before the count)
-          // The count after the XORs: a wave's LDS operations complete in
-          // order, so the segment that brings the count to nseg reads every
-          // other segment's XORs.  Opening also orders this segment's
-          // plaintext stores before the count (release: they complete before
-          // the record's last segment may zero-fill it); sealing needs only
-          // the LDS order.
-          uint32_t old = 0;
-          if (q == 0) {
-            if constexpr (OPEN)
-              old = __hip_atomic_fetch_add(s_cnt + t, 1u, __ATOMIC_RELEASE,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-            else
-              old = __hip_atomic_fetch_add(s_cnt + t, 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
-          const bool fin = __shfl(old, lane & 48, 64) == (uint32_t)nseg - 1;
-          if (__ballot(fin) == 0) continue;
-          // Record end of the groups whose record this segment completed
-          // (the slot reads stay after the count: compiler barrier).
-          asm volatile("" ::: "memory");
-          const RecordMeta &m = in.m;
-          uint4 j0 = make_uint4(0, 0, 0, 0);
-          if (in.live) {
-            if (b.nonce_len == 12)
-              j0 = make_uint4(in.nonce.x, in.nonce.y, in.nonce.z, 0x01000000u);
-            else
-              j0 = record_j0(b, in.rec, keys[k].hpow_ct);
-          }
-          const uint32_t ek0w =
-              ek0_quad<NR, 0>(j0.x ^ rk.w[0][0], j0.y ^ rk.w[0][1], j0.z ^ rk.w[0][2],
-                              j0.w ^ rk.w[0][3], rk, smem, lc0, lc1);
-          uint4 tot = make_uint4(0, 0, 0, 0);
-          if (fin) {
-            tot = s_slot[t * 16 + q];
-            s_slot[t * 16 + q] = make_uint4(0, 0, 0, 0);
-          }
-          const uint64_t nb = in.live ? (in.m.len + 15) / 16 : 0;
-          finish_record<OPEN, 16>(tot, nb, m, quad_gather(ek0w), b, in.rec, in.active && fin,
-                                  in.live && fin, b.out + m.off, keys[k].hpow_ct);
-        }
-        continue;
-      }
-    }
-    const int npass = npass_s < 0 ? -npass_s : npass_s;
+    const int npass = *s_npass;
     for (int pi = 0; pi < npass; pi++) {
       const uint32_t k = __builtin_amdgcn_readfirstlane(s_pass_key[pi]);
       const uint64_t mask = s_pass_mask[pi];
@@ -1237,29 +1086,6 @@ bool runs_in_lines(const BatchDesc &b) {
 #endif
 constexpr int kIovLongL = GCM_IOV_LONG_L, kIovShortL = GCM_IOV_SHORT_L;
 
-// Record segments of a keyset batch (gcm_keyset_kernel): uniform records of
-// R iterations (16 blocks each) split into nseg segments of R / nseg
-// iterations, nseg the largest divisor of R up to GCM_KEYSET_SEGS with
-// segments of at least kMinSegIters iterations; nseg 0 (whole records)
-// otherwise -- ragged, iovec or extra-byte batches, short records.
-#ifndef GCM_KEYSET_SEGS
-#define GCM_KEYSET_SEGS 4
-#endif
-constexpr int kKeysetSegs = GCM_KEYSET_SEGS;
-static_assert(kKeysetSegs <= kMaxSegs, "segment powers in LDS");
-constexpr uint64_t kMinSegIters = 8;
-void keyset_segments(const BatchDesc &b, int &nseg, int &seg_iters) {
-  nseg = seg_iters = 0;
-  if (!b.key_index || b.lengths || b.iovecs || b.extra_len || b.record_len % 256 != 0) return;
-  const uint64_t iters = b.record_len / 256;
-  for (int k = kKeysetSegs; k >= 2; k--)
-    if (iters % (uint64_t)k == 0 && iters / (uint64_t)k >= kMinSegIters) {
-      nseg = k;
-      seg_iters = (int)(iters / (uint64_t)k);
-      return;
-    }
-}
-
 template <int NR, bool OPEN>
 int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const KernelEvents *ev) {
   if (one_record_batch(b)) {
@@ -1303,14 +1129,12 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
     const uint64_t tiles = (b.num_records + kWaves * kRecPerWave - 1) / (kWaves * kRecPerWave);
     const unsigned grid = (unsigned)(tiles < (uint64_t)num_cus ? tiles : (uint64_t)num_cus);
     if (b.key_index) {
-      int nseg = 0, seg_iters = 0;
-      keyset_segments(b, nseg, seg_iters);
       if (b.extra_len)
         hipLaunchKernelGGL((gcm_keyset_kernel<NR, OPEN, true, kWaves>), dim3(grid),
-                           dim3(kWaves * 64), 0, s, keys, bo, 0, 0);
+                           dim3(kWaves * 64), 0, s, keys, bo);
       else
         hipLaunchKernelGGL((gcm_keyset_kernel<NR, OPEN, false, kWaves>), dim3(grid),
-                           dim3(kWaves * 64), 0, s, keys, bo, nseg, seg_iters);
+                           dim3(kWaves * 64), 0, s, keys, bo);
     } else if (b.iovecs && order) {  // (one key: the ctx API)
       // iovec records in length order (their totals are `lengths`): 16 lanes
       // for the records of 4 KiB or more, 8 from 2 KiB, 4 below (1M x 1350 B
@@ -1361,15 +1185,23 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
 
 }  // namespace
 
+#ifndef BSSL_AMD_MIX_TU  // (gcm_mix.hip includes this file for process_records)
 namespace {
 std::atomic<int> g_gcm_engine{-1};
+std::atomic<int> g_gcm_mix_nb{4};
 }  // namespace
+
+int gcm_mix_waves() { return g_gcm_mix_nb.load(std::memory_order_relaxed); }
 
 int gcm_engine() {
   int e = g_gcm_engine.load(std::memory_order_relaxed);
   if (e >= 0) return e;
   const char *v = getenv("BSSL_AMD_GCM_MODE");
   e = v && (!strcmp(v, "bs") || !strcmp(v, "bs16")) ? kGcmEngineBitsliced : kGcmEngineTable;
+  if (v && !strncmp(v, "mix", 3)) {  // (experimental mixed engine, gcm_mix.hip: mix2|mix4|mix6)
+    e = kGcmEngineMix;
+    g_gcm_mix_nb.store(v[3] == '2' ? 2 : v[3] == '6' ? 6 : 4, std::memory_order_relaxed);
+  }
   int expect = -1;
   g_gcm_engine.compare_exchange_strong(expect, e, std::memory_order_relaxed);
   return g_gcm_engine.load(std::memory_order_relaxed);
@@ -1382,6 +1214,14 @@ int set_gcm_engine(int engine) {
   return prev;
 }
 
+int set_gcm_mix(int nb) {
+  if (nb != 2 && nb != 4 && nb != 6) return -1;
+  const int prev = gcm_engine();
+  g_gcm_mix_nb.store(nb, std::memory_order_relaxed);
+  g_gcm_engine.store(kGcmEngineMix, std::memory_order_relaxed);
+  return prev;
+}
+
 bool gcm_takes_one_record_kernel(const BatchDesc &b, int engine) {
   return engine != kGcmEngineBitsliced && one_record_batch(b);
 }
@@ -1391,6 +1231,8 @@ int launch_gcm(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, voi
   if (b.num_records == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (engine == kGcmEngineBitsliced) return launch_gcm_bs(keys, b, open, nr, s, ev);
+  if (engine == kGcmEngineMix && gcm_mix_eligible(b, nr))
+    return launch_gcm_mix(keys, b, open, gcm_mix_waves(), s, ev);
   switch (nr) {
     case 10: return open ? launch_nr<10, true>(keys, b, s, ev) : launch_nr<10, false>(keys, b, s, ev);
     case 12: return open ? launch_nr<12, true>(keys, b, s, ev) : launch_nr<12, false>(keys, b, s, ev);
@@ -1398,5 +1240,6 @@ int launch_gcm(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, voi
     default: return 1;
   }
 }
+#endif  // BSSL_AMD_MIX_TU
 
 }  // namespace bssl_amd

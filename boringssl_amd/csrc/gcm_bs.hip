@@ -451,6 +451,83 @@ __device__ __forceinline__ uint32_t bs_lane() {
   return v;
 }
 
+// iovec records: the chunk cursors of a lane (gcm.hip process_records' form:
+// chunk index + stream start, and running pointers / bytes left in the chunk
+// between chunk boundaries).  Input and output chunks have the same lengths,
+// so both runs advance together.
+struct BsIovCur {
+  uint64_t ld_c, ld_cs, st_c, st_cs;
+  const uint8_t *ld_ptr;
+  uint8_t *st_ptr;
+  int32_t left;  // bytes left in the current chunk run (-1: none yet)
+};
+
+// One block of an iovec record that is not a whole block inside the current
+// chunk run (a chunk boundary, a straddle, the record's last block, the first
+// block): walk the chunk table for the load and the store, re-anchor the runs.
+// Out of line: inlined into each of the 16 slots of the unrolled pass it held
+// the 64 keystream registers through 16 copies of the walk and spilled
+// 8 KiB per lane; as a call the walks' registers are its own.  Returns the
+// hashed block (OPEN: the input, else the output).
+// (The batch's fields by value: a reference to the kernel's by-value
+// descriptor would make the compiler copy it to the stack.)
+template <int L, bool OPEN>
+__device__ __noinline__ uint4 bs_iov_slow(const IovecDev *iovecs, const uint64_t *iovec_start,
+                                          uint64_t rlen, BsIovCur &cur, uint64_t rec, uint32_t j,
+                                          uint4 ks) {
+  BatchDesc b;  // (the iovec helpers read only b.iovecs)
+  b.iovecs = iovecs;
+  const uint64_t pb = (uint64_t)j * 16;
+  const uint64_t c_end = iovec_start[rec + 1];
+  const uint32_t nbytes = (uint32_t)umin64(rlen - pb, 16);
+  uint4 x;
+  {
+    IovCur k;
+    iov_at(k, b, cur.ld_c, cur.ld_cs);
+    iov_seek(k, b, pb, c_end);
+    if (nbytes == 16 && pb + 16 <= k.ce)
+      x = load_blk_nt(k.in + (pb - k.cs));
+    else if (!iov_load2(b, k, pb, nbytes, c_end, x))
+      x = iov_gather(b, k, pb, nbytes, c_end);
+    cur.ld_c = k.c;
+    cur.ld_cs = k.cs;
+    cur.ld_ptr = k.in + (pb - k.cs) + 16 * L;
+    cur.left = (int32_t)umin64(k.ce - pb, 1u << 30) - 16 * L;
+  }
+  const uint4 y = mask_block(xor4(x, ks), nbytes);
+  {
+    IovCur k;
+    iov_at(k, b, cur.st_c, cur.st_cs);
+    iov_seek(k, b, pb, c_end);
+    if (nbytes == 16 && pb + 16 <= k.ce)
+      store_blk_nt(k.out + (pb - k.cs), y);
+    else if (!iov_store2(b, k, pb, y, nbytes, c_end))
+      iov_scatter(b, k, pb, y, nbytes, c_end);
+    cur.st_c = k.c;
+    cur.st_cs = k.cs;
+    cur.st_ptr = k.out + (pb - k.cs) + 16 * L;
+  }
+  return OPEN ? x : y;
+}
+
+// Where a record end gets its E_K(J0): the epoch-tagged granules of the
+// batched production (polled, with the bounded-wait fallback).  The mixed
+// engine (gcm_mix.hip) passes its own source.
+struct BsEk0Granules {
+  const uint4 *ek0;
+  uint32_t epoch, max_polls;
+  template <int NR>
+  __device__ __forceinline__ uint4 get(uint64_t pos, bool act_live, const GcmKeyDev *key,
+                                       const BatchDesc &b, uint64_t rec, uint32_t &polls) const {
+    bool got;
+    uint4 e0 = load_ek0(ek0, pos, act_live, epoch, max_polls, polls, got);
+#if BS_SELF_EK0
+    if (!got) e0 = self_ek0<NR>(key, b, rec, act_live);  // (wave-uniform)
+#endif
+    return e0;
+  }
+};
+
 // ---------------------------------------------------------------------------
 // Per-lane unit state parked in LDS while the rounds hold the registers
 // (word k of thread t at kBsLdsState + (k * kBsThreads + t) * 4: consecutive
@@ -472,10 +549,15 @@ enum : int {
 // processing position first + r for r = lane / L (wave-uniform `first`; bit r
 // of the wave-uniform `amask`: the unit has a record there).  The lane's own
 // position and flag are recomputed from the lane index where needed.
-template <int NR, bool OPEN, bool XT, bool IOV, int L>
+// PARK / PTHREADS: LDS offset of the parked unit state and the threads it is
+// laid out for (the bitsliced kernels: kBsLdsState for all 1,024 threads; the
+// mixed engine: its bitsliced waves only).  EK0: the record ends' E_K(J0)
+// source (BsEk0Granules).
+template <int NR, bool OPEN, bool XT, bool IOV, int L, uint32_t PARK = kBsLdsState,
+          int PTHREADS = kBsThreads, class EK0 = BsEk0Granules>
 __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const BatchDesc &b,
                                         uint64_t first, uint64_t amask, uint8_t *smem,
-                                        const uint4 *ek0, uint32_t epoch, uint32_t max_polls) {
+                                        const EK0 &ek0src) {
   static_assert(L == 16 || L == 8 || L == 4 || L == 2, "lanes per record");
   static_assert(!(IOV && XT), "iovec records carry no extra bytes");
 #ifdef BSSL_AMD_BS_PROF
@@ -497,7 +579,7 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
 #endif
   const uint32_t lbase =
       (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t *)smem) +
-      kBsLdsState + 16u * 64u * (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      PARK + 16u * 64u * (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   auto addr = [&]() -> uint32_t {
     uint32_t a;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\t"
@@ -510,29 +592,26 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
     uint32_t v;
     asm volatile("ds_read_b32 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
                  : "=v"(v)
-                 : "v"(addr()), "i"((k >> 2) * 16 * kBsThreads + 4 * (k & 3)));
+                 : "v"(addr()), "i"((k >> 2) * 16 * PTHREADS + 4 * (k & 3)));
     return v;
   };
   auto put4 = [&](int k, uint4 v) {  // words k..k+3 (k % 4 == 0)
     const u32x4 w = {v.x, v.y, v.z, v.w};
     asm volatile("ds_write_b128 %0, %1 offset:%2\n\ts_nop 1" ::"v"(addr()), "v"(w),
-                 "i"((k >> 2) * 16 * kBsThreads));
+                 "i"((k >> 2) * 16 * PTHREADS));
   };
   auto get4 = [&](int k) -> uint4 {  // words k..k+3 (k % 4 == 0)
     u32x4 w;
     asm volatile("ds_read_b128 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
                  : "=v"(w)
-                 : "v"(addr()), "i"((k >> 2) * 16 * kBsThreads));
+                 : "v"(addr()), "i"((k >> 2) * 16 * PTHREADS));
     return make_uint4(w.x, w.y, w.z, w.w);
   };
   const int q = (int)(bs_lane() & (L - 1));
   int nchunks;
   // IOV: chunk cursors (as gcm.hip process_records: chunk index + stream
   // start; between chunk boundaries only the running pointers move).
-  uint64_t ld_c = 0, ld_cs = 0, st_c = 0, st_cs = 0;
-  const uint8_t *ld_ptr = nullptr;
-  uint8_t *st_ptr = nullptr;
-  int32_t ld_left = -1, st_left = -1;
+  BsIovCur iov = {0, 0, 0, 0, nullptr, nullptr, -1};
 #if BS_EDGE_PRIO
   __builtin_amdgcn_s_setprio(BS_EDGE_PRIO);  // (A/B: the record start's loads and products)
 #endif
@@ -590,7 +669,7 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
     put4(kSflags, make_uint4((active ? 1u : 0u) | (live ? 2u : 0u), (uint32_t)rec,
                              (uint32_t)(rec >> 32), 0u));
     if constexpr (IOV) {
-      if (live) ld_c = st_c = b.iovec_start[rec];
+      if (live) iov.ld_c = iov.st_c = b.iovec_start[rec];
     }
   }
   const uint32_t *__restrict__ mk = &key->bsmask[0][0];
@@ -805,54 +884,33 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
     // partial last block is handled inside pass 1 (iov_load2 / iov_gather).
     if constexpr (IOV) {
       int nv = 0;  // the lane's blocks of this chunk (hashed in pass 2)
+      // (the record's bytes: its total, parked as its block count and full
+      // blocks would not tell a partial last block; re-read per chunk)
+      uint64_t nbytes_total = 0;
+      {
+        const uint64_t rec = (uint64_t)get(kSrec) | ((uint64_t)get(kSrecHi) << 32);
+        if (nb) nbytes_total = b.lengths ? b.lengths[rec] : b.record_len;
+      }
 #pragma unroll
       for (int n = 0; n < 16; n++) {
         const uint32_t j = jc + (uint32_t)L * (uint32_t)n;
         const uint4 ks = make_uint4(KA[n], KB[n], KA[16 + n], KB[16 + n]);
         uint4 cv = make_uint4(0, 0, 0, 0);
         if (j < nb) {
-          const uint64_t rec = (uint64_t)get(kSrec) | ((uint64_t)get(kSrecHi) << 32);
-          const uint64_t pb = (uint64_t)j * 16;
-          const uint64_t c_end = b.iovec_start[rec + 1];
-          const uint64_t rlen = b.lengths ? b.lengths[rec] : b.record_len;
-          const uint32_t nbytes = (uint32_t)umin64(rlen - pb, 16);
-          uint4 x;
-          if (ld_left >= 16 && nbytes == 16) {
-            x = load_blk_nt(ld_ptr);
+          // A whole block inside the current chunk run: one load and one
+          // store at the running pointers; anything else out of line.
+          if (iov.left >= 16 && (j + 1) * 16 <= nbytes_total) {
+            const uint4 x = load_blk_nt(iov.ld_ptr);
+            const uint4 y = xor4(x, ks);
+            store_blk_nt(iov.st_ptr, y);
+            iov.ld_ptr += 16 * L;
+            iov.st_ptr += 16 * L;
+            iov.left -= 16 * L;
+            cv = OPEN ? x : y;
           } else {
-            IovCur k;
-            iov_at(k, b, ld_c, ld_cs);
-            iov_seek(k, b, pb, c_end);
-            if (nbytes == 16 && pb + 16 <= k.ce)
-              x = load_blk_nt(k.in + (pb - k.cs));
-            else if (!iov_load2(b, k, pb, nbytes, c_end, x))
-              x = iov_gather(b, k, pb, nbytes, c_end);
-            ld_c = k.c;
-            ld_cs = k.cs;
-            ld_ptr = k.in + (pb - k.cs);
-            ld_left = (int32_t)umin64(k.ce - pb, 1u << 30);
+            const uint64_t rec = (uint64_t)get(kSrec) | ((uint64_t)get(kSrecHi) << 32);
+            cv = bs_iov_slow<L, OPEN>(b.iovecs, b.iovec_start, nbytes_total, iov, rec, j, ks);
           }
-          ld_ptr += 16 * L;
-          ld_left -= 16 * L;
-          const uint4 y = mask_block(xor4(x, ks), nbytes);
-          if (st_left >= 16 && nbytes == 16) {
-            store_blk_nt(st_ptr, y);
-          } else {
-            IovCur k;
-            iov_at(k, b, st_c, st_cs);
-            iov_seek(k, b, pb, c_end);
-            if (nbytes == 16 && pb + 16 <= k.ce)
-              store_blk_nt(k.out + (pb - k.cs), y);
-            else if (!iov_store2(b, k, pb, y, nbytes, c_end))
-              iov_scatter(b, k, pb, y, nbytes, c_end);
-            st_c = k.c;
-            st_cs = k.cs;
-            st_ptr = k.out + (pb - k.cs);
-            st_left = (int32_t)umin64(k.ce - pb, 1u << 30);
-          }
-          st_ptr += 16 * L;
-          st_left -= 16 * L;
-          cv = OPEN ? x : y;
           nv = n + 1;
         }
         KA[n] = cv.x;
@@ -902,14 +960,10 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
   if ((threadIdx.x & 63) == 0 && first / kBsGroupRecs < 4096)
     atomicMin(&g_bs_grp[first / kBsGroupRecs][2], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
-  uint32_t polls;
-  bool got;
+  uint32_t polls = 0;
   // (Live records only: the producer skips the others, whose output
   // finish_record zero-fills.)
-  uint4 e0 = load_ek0(ek0, first + bs_lane() / L, act && live, epoch, max_polls, polls, got);
-#if BS_SELF_EK0
-  if (!got) e0 = self_ek0<NR>(key, b, rec, act && live);  // (wave-uniform)
-#endif
+  const uint4 e0 = ek0src.template get<NR>(first + bs_lane() / L, act && live, key, b, rec, polls);
   BS_LAP(8);
 #ifdef BSSL_AMD_BS_PROF
   if ((threadIdx.x & 63) == 0) {
@@ -995,7 +1049,8 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_kernel(const GcmKeyDev *__r
 #ifdef BSSL_AMD_BS_PROF
     if (lane == 0 && u % kGroupUnits == 0 && g < 4096) g_bs_grp[g][3] = __builtin_amdgcn_s_memrealtime();
 #endif
-    bs_unit<NR, OPEN, XT, IOV, L>(keys, b, first, amask, smem, ek0, epoch, kBsEk0Polls);
+    bs_unit<NR, OPEN, XT, IOV, L>(keys, b, first, amask, smem,
+                                  BsEk0Granules{ek0, epoch, kBsEk0Polls});
   }
 #ifdef BSSL_AMD_BS_PROF
   if (lane == 0) {
@@ -1077,7 +1132,7 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_keyset_kernel(
         loaded = k;
       }
       bs_unit<NR, OPEN, XT, false, 16>(keys + k, b, base + 4 * wave, (mask >> (4 * wave)) & 15u,
-                                       smem, ek0, epoch, kBsEk0Polls);
+                                       smem, BsEk0Granules{ek0, epoch, kBsEk0Polls});
     }
   }
 }
@@ -1106,6 +1161,7 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_keyset_kernel(
 constexpr int kBsLongL = BS_LONG_L, kBsShortL = BS_SHORT_L;  // (A/B builds: -DBS_LONG_L=8 ...)
 constexpr int kBsRaggedL = 8;
 
+#ifndef BSSL_AMD_MIX_TU  // (gcm_mix.hip includes this file for bs_unit)
 namespace {
 std::atomic<bool> g_bs_producers{true};
 }  // namespace
@@ -1253,5 +1309,6 @@ int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr, 
   hipFreeAsync(scratch, s);
   return rc;
 }
+#endif  // BSSL_AMD_MIX_TU
 
 }  // namespace bssl_amd

@@ -448,10 +448,9 @@ struct UnitIn {
   bool active, live;
 };
 
-// jb: the lane's first block is q + jb (a segment of the record, gcm.hip).
 template <bool XT, bool IOV>
 __device__ __forceinline__ void unit_load(UnitIn &u, const BatchDesc &b, uint64_t i, int q,
-                                          uint64_t end, uint64_t jb = 0) {
+                                          uint64_t end) {
   u.active = i < end;
   u.rec = u.active ? rec_at(b, i) : 0;
   u.m = {0, 0, 0, 0, 0};
@@ -466,8 +465,7 @@ __device__ __forceinline__ void unit_load(UnitIn &u, const BatchDesc &b, uint64_
   u.ad0 = make_uint4(0, 0, 0, 0);
   if (u.live && u.m.ad_len) u.ad0 = ad_block(b, u.rec, u.m, 0);
   if constexpr (!IOV)
-    if (u.live && (uint64_t)q + jb < u.m.len / 16)
-      u.x0 = load_blk_nt(b.in + u.m.off + 16 * ((uint64_t)q + jb));
+    if (u.live && (uint64_t)q < u.m.len / 16) u.x0 = load_blk_nt(b.in + u.m.off + 16 * q);
 }
 
 // Byte table of H^16 from the key's nibble tables (power 4): entry (e, p) =

@@ -175,11 +175,18 @@ int launch_gcm(const GcmKeyDev *keys, const BatchDesc &b, bool open,
 // (gcm_bs.hip) or the LDS T-table engine (gcm.hip).  Process-wide; the
 // initial value comes from BSSL_AMD_GCM_MODE ("bs" / "bs16" or "table"),
 // read once; BSSL_AMD_set_aes_gcm_engine changes it.
-enum GcmEngine : int { kGcmEngineTable = 0, kGcmEngineBitsliced = 1 };
+enum GcmEngine : int { kGcmEngineTable = 0, kGcmEngineBitsliced = 1, kGcmEngineMix = 2 };
 int gcm_engine();
 int set_gcm_engine(int engine);  // returns the previous engine, or -1 (bad value)
 int launch_gcm_bs(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nr,
                   hipStream_t stream, const KernelEvents *ev);
+// The experimental mixed-role engine (gcm_mix.hip; BSSL_AMD_GCM_MODE=mixN,
+// N bitsliced waves of 16): eligible batches and the launcher.
+int gcm_mix_waves();
+int set_gcm_mix(int nb);  // selects the mixed engine with nb bitsliced waves (2, 4, 6)
+bool gcm_mix_eligible(const BatchDesc &b, int nr);
+int launch_gcm_mix(const GcmKeyDev *keys, const BatchDesc &b, bool open, int nb, hipStream_t s,
+                   const KernelEvents *ev);
 // Test switch of the table-free engine's batched E_K(J0) production (on by
 // default; off: every record end computes its own after the bounded wait).
 // Returns the previous setting.

@@ -30,6 +30,15 @@ BSSL_AMD_EXPORT size_t BSSL_AMD_gcm_key_tables(const uint8_t *keys, size_t key_l
  * exercises it); 1 restores the default.  Returns the previous setting. */
 BSSL_AMD_EXPORT int BSSL_AMD_test_set_bs_ek0_producers(int on);
 
+/* The experimental mixed-role AES-GCM engine (gcm_mix.hip; also selected by
+ * BSSL_AMD_GCM_MODE=mix2|mix4|mix6): bitsliced_waves (2, 4 or 6) of each
+ * workgroup's 16 waves run the table-free engine, the others the T-table
+ * engine, on one unit counter, for one-key uniform AES-128-GCM batches of
+ * records of 4 KiB or more (other batches take the T-table engine).  Returns
+ * the previous engine (restore it with BSSL_AMD_set_aes_gcm_engine), -1 for
+ * another wave count. */
+BSSL_AMD_EXPORT int BSSL_AMD_test_set_gcm_mix(int bitsliced_waves);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,17 +1,14 @@
-"""Keyset batches in record segments (gcm.hip gcm_keyset_kernel, round 6).
-
-A tile of one key's 64 uniform records is split into 16 x nseg units of four
-records x one segment of their 16-block iterations, claimed from an LDS
-counter; the segments' GHASH accumulators are weighted by powers of H^16,
-XORed into per-record lane slots in LDS, and the segment that completes a
-record runs its end (E_K(J0), tag, check, zero-fill).  Parity with the CPU
-oracle (oracle/aead_oracle.c, which follows gcm.cc.inc:298-604) for every
-record and tag: tiles of one key (segmented) beside tiles of several keys and
-a partial last tile (whole records) in the same launch, AES-128/256, 12- and
-16-byte nonces (J0 by GHASH in the record end), seal, open in place and a
-tampered record (status 0, plaintext zero-filled by the record's last
-segment after every other segment's stores).  The reference handles each
-key's records independently (gcm.cc.inc:253-296, aead.cc.inc:70-106).
+"""Uniform keyset batches through the T-table keyset kernel (gcm.hip
+gcm_keyset_kernel): tiles of one key's 64 records beside a tile of two keys
+(two passes) and a partial last tile in one launch, AES-128/256, 12- and
+16-byte nonces (J0 by GHASH), seal, open in place and one tampered record
+per tile (status 0, plaintext zero-filled), every record and tag against the
+CPU oracle (oracle/aead_oracle.c, following gcm.cc.inc:298-604).  Round 6
+ran these records through record segments of the tiles (one key's records
+split into 16 x nseg units claimed from an LDS counter); the
+segments measured slower and were reverted, the test stays as the keyset
+kernel's uniform-layout parity check.  The reference handles each key's
+records independently (gcm.cc.inc:253-296, aead.cc.inc:70-106).
 """
 import zlib
 
@@ -38,7 +35,7 @@ def _key_index(n):
 
 @pytest.mark.parametrize("aead,rlen,nl", [("aes-128-gcm", 8192, 12), ("aes-256-gcm", 16384, 12),
                                           ("aes-128-gcm", 12288, 16)])
-def test_keyset_segments_vs_oracle(aead, rlen, nl, aes_engine):
+def test_keyset_tiles_vs_oracle(aead, rlen, nl, aes_engine):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     aes_engine("table")
