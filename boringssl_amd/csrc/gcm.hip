@@ -765,9 +765,18 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
 // records are visited in tiles of W * 4; a tile whose records use several
 // keys is processed in one pass per distinct key, since the LDS byte table is
 // per key.
+// Tiles from a grid-wide counter (round 6: config 5 1,084-1,091 -> 1,110 GiB/s
+// against the blockIdx-strided order, same box, profiles/r06/s5): a CU that
+// finishes its tiles early takes the next one instead of idling at the end.
+#ifndef GCM_KEYSET_DYN
+#define GCM_KEYSET_DYN 1
+#endif
+#ifndef GCM_KEYSET_RP
+#define GCM_KEYSET_RP 1  // (A/B: 0 = no per-iteration priority rotation)
+#endif
 template <int NR, bool OPEN, bool XT, int W>
 __global__ __launch_bounds__(1024) void gcm_keyset_kernel(const GcmKeyDev *__restrict__ keys,
-                                                           BatchDesc b) {
+                                                           BatchDesc b, uint32_t *__restrict__ tiles) {
   constexpr int kThreads = W * 64;
   constexpr int kRecPerTile = W * kRecPerWave;
   static_assert(kRecPerTile <= 64, "one wave plans a tile with ballots");
@@ -785,8 +794,18 @@ __global__ __launch_bounds__(1024) void gcm_keyset_kernel(const GcmKeyDev *__res
   const uint32_t lc1 = lc0 + 128u;
   uint32_t loaded = 0xffffffffu;
   const uint64_t n = b.num_records;
+#if GCM_KEYSET_DYN  // (tiles from a grid-wide counter; 0: blockIdx order, round 5)
+  uint64_t *s_tile = reinterpret_cast<uint64_t *>(smem + kLdsPlan + 64 * 16 + 8);
+  for (uint64_t base = 0;;) {
+    __syncthreads();
+    if (tid == 0) *s_tile = (uint64_t)atomicAdd(tiles, 1u) * kRecPerTile;
+    __syncthreads();
+    base = *s_tile;
+    if (base >= n) break;
+#else
   for (uint64_t base = (uint64_t)blockIdx.x * kRecPerTile; base < n;
        base += (uint64_t)gridDim.x * kRecPerTile) {
+#endif
     __syncthreads();
     if (wave == 0) {
       // Plan the tile: one pass per distinct key, in record order.
@@ -830,7 +849,8 @@ __global__ __launch_bounds__(1024) void gcm_keyset_kernel(const GcmKeyDev *__res
       const bool active = (mask >> t) & 1;
       UnitIn in;
       unit_load<XT, false>(in, b, active ? base + t : n, lane & 15, n);
-      process_records<NR, OPEN, XT, 16, true>(rk, b, in, smem, keys + k, lc0, lc1, wave >> 2);
+      process_records<NR, OPEN, XT, 16, GCM_KEYSET_RP != 0>(rk, b, in, smem, keys + k, lc0, lc1,
+                                                           wave >> 2);
       __builtin_amdgcn_s_setprio(0);
     }
   }
@@ -1131,10 +1151,10 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
     if (b.key_index) {
       if (b.extra_len)
         hipLaunchKernelGGL((gcm_keyset_kernel<NR, OPEN, true, kWaves>), dim3(grid),
-                           dim3(kWaves * 64), 0, s, keys, bo);
+                           dim3(kWaves * 64), 0, s, keys, bo, units + 12);
       else
         hipLaunchKernelGGL((gcm_keyset_kernel<NR, OPEN, false, kWaves>), dim3(grid),
-                           dim3(kWaves * 64), 0, s, keys, bo);
+                           dim3(kWaves * 64), 0, s, keys, bo, units + 12);
     } else if (b.iovecs && order) {  // (one key: the ctx API)
       // iovec records in length order (their totals are `lengths`): 16 lanes
       // for the records of 4 KiB or more, 8 from 2 KiB, 4 below (1M x 1350 B

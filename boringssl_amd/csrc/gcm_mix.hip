@@ -67,6 +67,12 @@ __global__ __launch_bounds__(1024) void gcm_mix_kernel(const GcmKeyDev *__restri
 #pragma unroll
     for (int c = 0; c < 4; c++) rk.w[r][c] = keys[0].rk[r][c];
   const uint64_t n = b.num_records;
+#ifndef MIX_TT_PRIO
+#define MIX_TT_PRIO 0
+#endif
+  // (A/B: the T-table waves' issue priority over the bitsliced waves, whose
+  // output pass runs at 2)
+  if (MIX_TT_PRIO && wave >= NB) __builtin_amdgcn_s_setprio(MIX_TT_PRIO);
   for (;;) {
     uint32_t u = 0;
     if (lane == 0) u = atomicAdd(ctl, 1u);

@@ -48,7 +48,11 @@ def calib_pattern(full_name):
     lanes = int(m.group(1).split(",")[-1]) if m else 16
     if "keyset" in full_name:
         lanes = 16
-    return {4: "copy_quad", 8: "copy_gcm8", 16: "copy_gcm"}.get(lanes, "copy_gcm")
+    # (4 lanes: 64-byte runs, half a 128-byte line per record and iteration;
+    # the kernel requests the two halves an iteration apart, and the counter
+    # counts such requests near full size (0.95) where the back-to-back copy
+    # counts half (0.55): the paced copy is the kernel's stream, round 6)
+    return {4: "copy_quad_slow", 8: "copy_gcm8", 16: "copy_gcm"}.get(lanes, "copy_gcm")
 CALIB_TAGS_PER_REC = 16  # the copy kernels also write one 16-byte tag per record
 
 
