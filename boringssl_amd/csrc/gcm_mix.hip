@@ -68,10 +68,12 @@ __global__ __launch_bounds__(1024) void gcm_mix_kernel(const GcmKeyDev *__restri
     for (int c = 0; c < 4; c++) rk.w[r][c] = keys[0].rk[r][c];
   const uint64_t n = b.num_records;
 #ifndef MIX_TT_PRIO
-#define MIX_TT_PRIO 0
+#define MIX_TT_PRIO 3
 #endif
-  // (A/B: the T-table waves' issue priority over the bitsliced waves, whose
-  // output pass runs at 2)
+  // The T-table waves issue at priority 3, above the bitsliced waves (whose
+  // output pass runs at 2): at equal priority the older bitsliced waves took
+  // the VALU slots the T-table waves' LDS stream waits on (mix4 874 -> 1,036
+  // GiB/s, LDS busy 0.24 -> 0.52; profiles/r06/s6).
   if (MIX_TT_PRIO && wave >= NB) __builtin_amdgcn_s_setprio(MIX_TT_PRIO);
   for (;;) {
     uint32_t u = 0;
