@@ -114,6 +114,15 @@ constexpr uint32_t kBsLdsBytes = kBsLdsSink + 256;
 typedef uint32_t v32u __attribute__((ext_vector_type(32)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// The lane's index in its wave from a volatile asm statement: an opaque value
+// the compiler recomputes at each use instead of keeping it (and everything
+// derived from it) live across the rounds.
+__device__ __forceinline__ uint32_t bs_lane() {
+  uint32_t v;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
+  return v;
+}
+
 // 0 or 0xffffffff: bit `k` of w.
 __device__ __forceinline__ uint32_t bit_mask(uint32_t w, int k) {
   return (uint32_t)(((int32_t)(w << (31 - k))) >> 31);
@@ -292,7 +301,7 @@ __device__ __forceinline__ void produce_ek0(const GcmKeyDev *__restrict__ keys, 
     produce_ek0_ks<NR, true>(keys, b, i0, end, ek0, epoch);
     return;
   }
-  const int lane = threadIdx.x & 63;
+  const int lane = (int)bs_lane();  // (opaque: not hoisted into the kernel prologue)
   const uint64_t base = i0 + 16u * (uint64_t)lane;
   // Top priority while producing (as produce_ek0_ks).
   __builtin_amdgcn_s_setprio(3);
@@ -442,15 +451,6 @@ __device__ __forceinline__ uint4 self_ek0(const GcmKeyDev *__restrict__ key, con
   return make_uint4(KA[0], KB[0], KA[16], KB[16]);
 }
 
-// The lane's index in its wave from a volatile asm statement: an opaque value
-// the compiler recomputes at each use instead of keeping it (and everything
-// derived from it) live across the rounds.
-__device__ __forceinline__ uint32_t bs_lane() {
-  uint32_t v;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
-  return v;
-}
-
 // iovec records: the chunk cursors of a lane (gcm.hip process_records' form:
 // chunk index + stream start, and running pointers / bytes left in the chunk
 // between chunk boundaries).  Input and output chunks have the same lengths,
@@ -551,13 +551,15 @@ enum : int {
 // position and flag are recomputed from the lane index where needed.
 // PARK / PTHREADS: LDS offset of the parked unit state and the threads it is
 // laid out for (the bitsliced kernels: kBsLdsState for all 1,024 threads; the
-// mixed engine: its bitsliced waves only).  EK0: the record ends' E_K(J0)
+// mixed engine: its bitsliced waves only); `slot`: the wave's parking slot
+// (wave-uniform, its index in the workgroup, taken once at the kernel start
+// so that no thread index stays live across the units).  EK0: the record ends' E_K(J0)
 // source (BsEk0Granules).
 template <int NR, bool OPEN, bool XT, bool IOV, int L, uint32_t PARK = kBsLdsState,
           int PTHREADS = kBsThreads, class EK0 = BsEk0Granules>
 __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const BatchDesc &b,
                                         uint64_t first, uint64_t amask, uint8_t *smem,
-                                        const EK0 &ek0src) {
+                                        const EK0 &ek0src, uint32_t slot) {
   static_assert(L == 16 || L == 8 || L == 4 || L == 2, "lanes per record");
   static_assert(!(IOV && XT), "iovec records carry no extra bytes");
 #ifdef BSSL_AMD_BS_PROF
@@ -579,7 +581,7 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
 #endif
   const uint32_t lbase =
       (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t *)smem) +
-      PARK + 16u * 64u * (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      PARK + 16u * 64u * slot;
   auto addr = [&]() -> uint32_t {
     uint32_t a;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\t"
@@ -1000,6 +1002,7 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_kernel(const GcmKeyDev *__r
                                                              uint32_t epoch, uint32_t produce) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[kBsLdsBytes];
   const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);  // (an SGPR)
 #ifdef BSSL_AMD_BS_PROF
   if (lane < kBsProfN) reinterpret_cast<uint64_t *>(smem + kBsLdsProf)[(tid >> 6) * kBsProfN + lane] = 0;
   uint64_t t_prod = 0;
@@ -1018,7 +1021,7 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_kernel(const GcmKeyDev *__r
   if (b.split_hi) n = *b.split_hi;
   for (;;) {
     uint32_t u = 0;
-    if (lane == 0) u = atomicAdd(ctl, 1u);
+    if (bs_lane() == 0) u = atomicAdd(ctl, 1u);
     u = __builtin_amdgcn_readfirstlane(u);
     const uint64_t first = lo + (uint64_t)u * kRec;
     if (first >= n) break;
@@ -1050,7 +1053,7 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_kernel(const GcmKeyDev *__r
     if (lane == 0 && u % kGroupUnits == 0 && g < 4096) g_bs_grp[g][3] = __builtin_amdgcn_s_memrealtime();
 #endif
     bs_unit<NR, OPEN, XT, IOV, L>(keys, b, first, amask, smem,
-                                  BsEk0Granules{ek0, epoch, kBsEk0Polls});
+                                  BsEk0Granules{ek0, epoch, kBsEk0Polls}, wave);
   }
 #ifdef BSSL_AMD_BS_PROF
   if (lane == 0) {
@@ -1132,7 +1135,8 @@ __global__ __launch_bounds__(kBsThreads) void gcm_bs_keyset_kernel(
         loaded = k;
       }
       bs_unit<NR, OPEN, XT, false, 16>(keys + k, b, base + 4 * wave, (mask >> (4 * wave)) & 15u,
-                                       smem, BsEk0Granules{ek0, epoch, kBsEk0Polls});
+                                       smem, BsEk0Granules{ek0, epoch, kBsEk0Polls},
+                                       (uint32_t)wave);
     }
   }
 }

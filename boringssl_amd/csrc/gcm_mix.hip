@@ -84,7 +84,8 @@ __global__ __launch_bounds__(1024) void gcm_mix_kernel(const GcmKeyDev *__restri
     if (wave < NB) {
       const uint64_t amask = n - first >= 4 ? 15ull : (1ull << (n - first)) - 1;
       bs_unit<NR, OPEN, false, false, 16, kMixPark, NB * 64>(
-          keys, b, first, amask, smem, MixEk0<NR>{smem, &rk, lc0, lc1});
+          keys, b, first, amask, smem, MixEk0<NR>{smem, &rk, lc0, lc1},
+          __builtin_amdgcn_readfirstlane((uint32_t)wave));
     } else {
       UnitIn in;
       unit_load<false, false>(in, b, first + lane / 16, lane & 15, n);
