@@ -105,6 +105,19 @@ constexpr uint32_t kAesLdsBytes = 256 * 256;
 constexpr uint32_t kLdsPlan = kLdsAes + kAesLdsBytes;
 constexpr uint32_t kLdsBasis = kLdsPlan + 64 * 16 + 16;  // 128 x 16 B (build_gpow)
 constexpr uint32_t kLdsBytes = kLdsBasis + 128 * 16;
+//   [kLdsBytes, ...) iovec kernels (GCM_IOV_LDS): per record slot (one per L
+//                    lanes of the workgroup) the record's chunk range
+//                    [c0, c_end) and its first kIovKc chunk descriptors
+#ifndef GCM_IOV_LDS
+#define GCM_IOV_LDS 1
+#endif
+constexpr bool kIovLds = GCM_IOV_LDS != 0;
+template <int L>
+constexpr uint32_t kIovKc = L == 4 ? 3u : 4u;
+template <int L>
+constexpr uint32_t kIovSlot = 16u + 32u * kIovKc<L>;
+template <int L, int THREADS>
+constexpr uint32_t kLdsIovBytes = kLdsBytes + (kIovLds ? (THREADS / L) * kIovSlot<L> : 0u);
 
 // ---------------------------------------------------------------------------
 // AES.  State: 4 little-endian column words (byte r of word c = row r).
@@ -446,6 +459,42 @@ constexpr bool kIovHandoff = GCM_IOV_HANDOFF != 0;
 #endif
 constexpr bool kIovKeepEnd = GCM_IOV_KEEP_END != 0;
 
+// Chunk descriptors of an iovec record from its LDS slot (kIovLds): chunk c
+// in [c0, c0 + KC) from the slot's copy, later ones from the batch's array.
+// The record's walks then issue no global load before the block load itself:
+// a chunk-table load issued after the previous blocks' stores waits for all of
+// them (vmcnt counts loads and stores in issue order), an LDS read does not.
+template <uint32_t KC>
+struct IovDescL {
+  const uint8_t *smem;
+  uint32_t slot;
+  uint64_t c0;
+  const IovecDev *g;
+  __device__ __forceinline__ IovecDev operator()(uint64_t c) const {
+    if (c - c0 < KC) {
+      const uint32_t a = slot + 16u + (uint32_t)(c - c0) * 32u;
+      const uint4 w = *reinterpret_cast<const uint4 *>(smem + a);
+      const uint64_t len = *reinterpret_cast<const uint64_t *>(smem + a + 16);
+      IovecDev v;
+      v.out = reinterpret_cast<uint8_t *>(((uint64_t)w.y << 32) | w.x);
+      v.in = reinterpret_cast<const uint8_t *>(((uint64_t)w.w << 32) | w.z);
+      v.len = len;
+      return v;
+    }
+    // (Wait for the fallback's load here: otherwise the join with the LDS
+    // path leaves the descriptor pending on vmcnt, and the walk waits for
+    // every outstanding load and store even when it read LDS.)
+    uint64_t o = reinterpret_cast<uint64_t>(g[c].out), i = reinterpret_cast<uint64_t>(g[c].in),
+             len = g[c].len;
+    asm volatile("" : "+v"(o), "+v"(i), "+v"(len));
+    IovecDev v;
+    v.out = reinterpret_cast<uint8_t *>(o);
+    v.in = reinterpret_cast<const uint8_t *>(i);
+    v.len = len;
+    return v;
+  }
+};
+
 template <int NR, bool OPEN, bool XT, int L = 16, bool RP = false, bool IOV = false>
 __device__ __forceinline__ void process_records(const RoundKeys &rk, const BatchDesc &b,
                                                 const UnitIn &in, const uint8_t *smem,
@@ -538,14 +587,51 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   // load past it starts the walk at the next chunk, one dependent chunk-table
   // load instead of two.
   uint64_t ld_ce = 0;
+  // The record's LDS slot (kIovLds): c0 and c_end at +0 / +8, descriptor i
+  // of the record's chunks (i < KC) at +16 + 32 i.  Lane q < KC of the record
+  // copies descriptor q; the slot is the wave's own, read only by its lanes
+  // (in issue order) until its next unit overwrites it.
+  constexpr uint32_t kc = kIovKc<L>;
+  const uint32_t slot = kLdsBytes + (uint32_t)(threadIdx.x / L) * kIovSlot<L>;
   if constexpr (IOV) {
     if (live) {
       ld_c = st_c = b.iovec_start[rec];
+      if constexpr (kIovLds) {
+        uint8_t *ls = const_cast<uint8_t *>(smem) + slot;
+        const uint64_t ce = b.iovec_start[rec + 1];
+        if (q == 0) *reinterpret_cast<uint4 *>(ls) = make_uint4((uint32_t)ld_c, (uint32_t)(ld_c >> 32),
+                                                                (uint32_t)ce, (uint32_t)(ce >> 32));
+        if ((uint32_t)q < kc && ld_c + q < ce) {
+          const IovecDev v = b.iovecs[ld_c + q];
+          const uint64_t o = reinterpret_cast<uint64_t>(v.out), i = reinterpret_cast<uint64_t>(v.in);
+          *reinterpret_cast<uint4 *>(ls + 16 + 32 * q) =
+              make_uint4((uint32_t)o, (uint32_t)(o >> 32), (uint32_t)i, (uint32_t)(i >> 32));
+          *reinterpret_cast<uint64_t *>(ls + 16 + 32 * q + 16) = v.len;
+        }
+      }
       // (Seeding the running pointers here from the first chunk, so the first
       // load and store skip the cursor walk, measured neutral: 957-966 vs
       // 951-966 GiB/s, profiles/r04/s14/.)
     }
+    // (Lanes of one wave: its LDS accesses complete in issue order; the
+    // fence keeps the compiler from moving the slot's reads above the fill.)
+    if constexpr (kIovLds) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
   }
+  // The walk's descriptor source and the record's chunk end.
+  auto iov_src = [&](uint64_t &c_end) {
+    if constexpr (kIovLds) {
+      const uint4 h = *reinterpret_cast<const uint4 *>(smem + slot);
+      c_end = ((uint64_t)h.w << 32) | h.z;
+      return IovDescL<kc>{smem, slot, ((uint64_t)h.y << 32) | h.x, b.iovecs};
+    } else {
+      c_end = b.iovec_start[rec + 1];
+      return IovDescG{b.iovecs};
+    }
+  };
   // (Left undefined when not loaded: such a block is never stored or hashed
   // from this value, and a zero-fill would be a VALU write that the waitcnt
   // pass orders after the previous store.)
@@ -560,13 +646,14 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
         v = make_uint4(0, 0, 0, 0);
         const uint64_t p = j * 16;
         if (live && p < m.len) {  // (a dead record never walks the batch's chunks)
-          const uint64_t c_end = b.iovec_start[rec + 1];
+          uint64_t c_end;
+          const auto d = iov_src(c_end);
           IovCur k;
           if (kIovKeepEnd && ld_ce && p >= ld_ce && ld_c + 1 < c_end)
-            iov_at(k, b, ld_c + 1, ld_ce);
+            iov_at_d(k, d, ld_c + 1, ld_ce);
           else
-            iov_at(k, b, ld_c, ld_cs);
-          iov_seek(k, b, p, c_end);
+            iov_at_d(k, d, ld_c, ld_cs);
+          iov_seek_d(k, d, p, c_end);
           const uint32_t n = (uint32_t)umin64(m.len - p, 16);
           if (n == 16 && p + 16 <= k.ce) {
             v = load_blk_nt(k.in + (p - k.cs));
@@ -575,8 +662,8 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
               ho_left = (int32_t)umin64(k.ce - p, 1u << 30);
               ho_j = (uint32_t)j;
             }
-          } else if (!iov_load2(b, k, p, n, c_end, v))  // a straddle, the last block
-            v = iov_gather(b, k, p, n, c_end);        // (three or more chunks)
+          } else if (!iov_load2_d(d, k, p, n, c_end, v))  // a straddle, the last block
+            v = iov_gather_d(d, k, p, n, c_end);        // (three or more chunks)
           ld_c = k.c;
           ld_cs = k.cs;
           if constexpr (kIovKeepEnd) ld_ce = k.ce;
@@ -634,15 +721,16 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
       } else if (j < nb) {
         const uint64_t p = (uint64_t)j * 16;
         const uint32_t n = (uint32_t)umin64(m.len - p, 16);
-        const uint64_t c_end = b.iovec_start[rec + 1];
+        uint64_t c_end;
+        const auto d = iov_src(c_end);
         IovCur k;
-        iov_at(k, b, st_c, st_cs);
-        iov_seek(k, b, p, c_end);
+        iov_at_d(k, d, st_c, st_cs);
+        iov_seek_d(k, d, p, c_end);
         if (n == 16 && p + 16 <= k.ce) {
           store_blk_nt(k.out + (p - k.cs), y);
         } else {
           y = mask_block(y, n);
-          if (!iov_store2(b, k, p, y, n, c_end)) iov_scatter(b, k, p, y, n, c_end);
+          if (!iov_store2_d(d, k, p, y, n, c_end)) iov_scatter_d(d, k, p, y, n, c_end);
         }
         st_c = k.c;
         st_cs = k.cs;
@@ -724,7 +812,7 @@ template <int NR, bool OPEN, bool XT, int W, bool IOV = false, int L = 16>
 __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__ keys,
                                                     BatchDesc b, uint32_t *__restrict__ units) {
   constexpr int kThreads = W * 64;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[IOV ? kLdsIovBytes<L, kThreads> : kLdsBytes];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const uint64_t n = b.num_records;

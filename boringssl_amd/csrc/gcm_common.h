@@ -206,13 +206,13 @@ __device__ __forceinline__ uint4 crypt_partial_x(const uint8_t *src, uint8_t *ds
 // 16-byte block loads and stores at any address (u32_any, iov_dev.h).
 
 __device__ __forceinline__ uint4 load_blk_nt(const uint8_t *p) {
-  const u32_any *ip = reinterpret_cast<const u32_any *>(p);
+  const BSSL_GLOBAL u32_any *ip = (const BSSL_GLOBAL u32_any *)p;
   return make_uint4(__builtin_nontemporal_load(ip), __builtin_nontemporal_load(ip + 1),
                     __builtin_nontemporal_load(ip + 2), __builtin_nontemporal_load(ip + 3));
 }
 
 __device__ __forceinline__ void store_blk(uint8_t *p, uint4 y) {
-  u32_any *o = reinterpret_cast<u32_any *>(p);
+  BSSL_GLOBAL u32_any *o = (BSSL_GLOBAL u32_any *)p;
   o[0] = y.x;
   o[1] = y.y;
   o[2] = y.z;
@@ -220,7 +220,7 @@ __device__ __forceinline__ void store_blk(uint8_t *p, uint4 y) {
 }
 
 __device__ __forceinline__ void store_blk_nt(uint8_t *p, uint4 y) {
-  u32_any *o = reinterpret_cast<u32_any *>(p);
+  BSSL_GLOBAL u32_any *o = (BSSL_GLOBAL u32_any *)p;
 #ifdef BSSL_PLAIN_STORES  // (A/B builds: temporal stores)
   o[0] = y.x;
   o[1] = y.y;

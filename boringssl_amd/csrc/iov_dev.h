@@ -19,17 +19,28 @@ namespace {
 // line in the TA, nothing on the VALU).
 typedef uint32_t u32_any __attribute__((aligned(1)));
 
+// Record buffers are device memory, and every helper below reaches them
+// through global-address-space pointers (gptr): a pointer read from a chunk
+// descriptor is otherwise a generic one, and a generic (flat_*) access counts
+// on lgkmcnt as well as vmcnt, so each LDS wait after it -- the AES table
+// lookups of the rounds -- would also wait for that HBM access.
+#define BSSL_GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ BSSL_GLOBAL T *gptr(T *p) {
+  return (BSSL_GLOBAL T *)p;
+}
+
 // Integer min of two 64-bit lengths.  (HIP's min<uint64_t> in device code
 // goes through double precision: two conversions and v_min_f64.)
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
 __device__ __forceinline__ uint4 load16_any(const uint8_t *p) {
-  const u32_any *ip = reinterpret_cast<const u32_any *>(p);
+  const BSSL_GLOBAL u32_any *ip = (const BSSL_GLOBAL u32_any *)p;
   return make_uint4(ip[0], ip[1], ip[2], ip[3]);
 }
 
 __device__ __forceinline__ void store16_any(uint8_t *p, uint4 v) {
-  u32_any *o = reinterpret_cast<u32_any *>(p);
+  BSSL_GLOBAL u32_any *o = (BSSL_GLOBAL u32_any *)p;
   o[0] = v.x;
   o[1] = v.y;
   o[2] = v.z;
@@ -44,7 +55,7 @@ __device__ __forceinline__ void store16_any(uint8_t *p, uint4 v) {
 // request per byte.)
 __device__ __forceinline__ uint4 load_partial(const uint8_t *p, uint32_t n) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t *base = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+  const BSSL_GLOBAL uint32_t *base = (const BSSL_GLOBAL uint32_t *)(a & ~uintptr_t(3));
   const uint32_t sh = (uint32_t)(a & 3);
   const uint32_t nd = n ? (sh + n + 3) / 4 : 0u;  // dwords touched
   uint32_t d[5];
@@ -69,9 +80,10 @@ __device__ __forceinline__ void store_partial(uint8_t *p, uint4 v, uint32_t n) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
   if (n >= 16 && (a & 15) == 0) {
-    *reinterpret_cast<uint4 *>(p) = v;
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    *(BSSL_GLOBAL v4u *)p = v4u{v.x, v.y, v.z, v.w};
   } else if ((a & 3) == 0) {
-    uint32_t *pw = reinterpret_cast<uint32_t *>(p);
+    BSSL_GLOBAL uint32_t *pw = (BSSL_GLOBAL uint32_t *)p;
     uint32_t last = 0;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -80,21 +92,21 @@ __device__ __forceinline__ void store_partial(uint8_t *p, uint4 v, uint32_t n) {
     }
     const uint32_t r = n & 3;
     if (r) {
-      uint8_t *q = p + (n & ~3u);
-      if (r & 2) *reinterpret_cast<uint16_t *>(q) = (uint16_t)last;
+      BSSL_GLOBAL uint8_t *q = gptr(p) + (n & ~3u);
+      if (r & 2) *(BSSL_GLOBAL uint16_t *)q = (uint16_t)last;
       if (r & 1) q[r & 2] = (uint8_t)(last >> (8 * (r & 2)));
     }
   } else {
     // Unaligned: whole dwords at byte addresses (unaligned mode, as
     // store16_any), then the last 1-3 bytes.
-    u32_any *pw = reinterpret_cast<u32_any *>(p);
+    BSSL_GLOBAL u32_any *pw = (BSSL_GLOBAL u32_any *)p;
     uint32_t last = 0;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       if (4u * i + 4 <= n) pw[i] = w[i];
       if (n / 4 == (uint32_t)i) last = w[i];
     }
-    uint8_t *q = p + (n & ~3u);
+    BSSL_GLOBAL uint8_t *q = gptr(p) + (n & ~3u);
     for (uint32_t i = 0; i < (n & 3); i++) q[i] = (uint8_t)(last >> (8 * i));
   }
 }
@@ -123,8 +135,17 @@ struct IovCur {
   uint8_t *out;
 };
 
-__device__ __forceinline__ void iov_at(IovCur &k, const BatchDesc &b, uint64_t c, uint64_t cs) {
-  const IovecDev v = b.iovecs[c];
+// Chunk descriptors come through a source D: d(c) is chunk c of the batch.
+// IovDescG reads them from the batch's array in device memory; a kernel may
+// pass a source that serves a record's first chunks from LDS (gcm.hip).
+struct IovDescG {
+  const IovecDev *v;
+  __device__ __forceinline__ IovecDev operator()(uint64_t c) const { return v[c]; }
+};
+
+template <class D>
+__device__ __forceinline__ void iov_at_d(IovCur &k, const D &d, uint64_t c, uint64_t cs) {
+  const IovecDev v = d(c);
   k.c = c;
   k.cs = cs;
   k.ce = cs + v.len;
@@ -133,9 +154,18 @@ __device__ __forceinline__ void iov_at(IovCur &k, const BatchDesc &b, uint64_t c
 }
 
 // Advance to the chunk holding stream byte p (positions only grow).
+template <class D>
+__device__ __forceinline__ void iov_seek_d(IovCur &k, const D &d, uint64_t p, uint64_t c_end) {
+  while (p >= k.ce && k.c + 1 < c_end) iov_at_d(k, d, k.c + 1, k.ce);
+}
+
+__device__ __forceinline__ void iov_at(IovCur &k, const BatchDesc &b, uint64_t c, uint64_t cs) {
+  iov_at_d(k, IovDescG{b.iovecs}, c, cs);
+}
+
 __device__ __forceinline__ void iov_seek(IovCur &k, const BatchDesc &b, uint64_t p,
                                          uint64_t c_end) {
-  while (p >= k.ce && k.c + 1 < c_end) iov_at(k, b, k.c + 1, k.ce);
+  iov_seek_d(k, IovDescG{b.iovecs}, p, c_end);
 }
 
 // The cursor of chunk c (stream start cs), advanced to the chunk holding p.
@@ -170,13 +200,14 @@ __device__ __forceinline__ uint4 bytes_at(uint4 A, uint4 B, uint32_t a) {
 // or the next chunk (the usual straddle: at most one boundary): one partial
 // load per piece, joined by a byte shift.  Returns false (nothing loaded)
 // when more chunks are involved.
-__device__ __forceinline__ bool iov_load2(const BatchDesc &b, const IovCur &k, uint64_t p,
-                                          uint32_t n, uint64_t c_end, uint4 &v) {
+template <class D>
+__device__ __forceinline__ bool iov_load2_d(const D &d, const IovCur &k, uint64_t p, uint32_t n,
+                                            uint64_t c_end, uint4 &v) {
   const uint32_t n1 = (uint32_t)umin64(n, k.ce - p);
   uint4 v2 = make_uint4(0, 0, 0, 0);
   if (n1 < n) {
     if (k.c + 1 >= c_end) return false;
-    const IovecDev nx = b.iovecs[k.c + 1];
+    const IovecDev nx = d(k.c + 1);
     if (nx.len < n - n1) return false;
     v2 = load_partial(nx.in, n - n1);
   }
@@ -186,13 +217,14 @@ __device__ __forceinline__ bool iov_load2(const BatchDesc &b, const IovCur &k, u
   return true;
 }
 
-__device__ __forceinline__ bool iov_store2(const BatchDesc &b, const IovCur &k, uint64_t p,
-                                           uint4 y, uint32_t n, uint64_t c_end) {
+template <class D>
+__device__ __forceinline__ bool iov_store2_d(const D &d, const IovCur &k, uint64_t p, uint4 y,
+                                             uint32_t n, uint64_t c_end) {
   const uint32_t n1 = (uint32_t)umin64(n, k.ce - p);
   IovecDev nx = {nullptr, nullptr, 0};
   if (n1 < n) {
     if (k.c + 1 >= c_end) return false;
-    nx = b.iovecs[k.c + 1];
+    nx = d(k.c + 1);
     if (nx.len < n - n1) return false;
   }
   store_partial(k.out + (p - k.cs), y, n1);
@@ -202,12 +234,13 @@ __device__ __forceinline__ bool iov_store2(const BatchDesc &b, const IovCur &k, 
 
 // Bytes [p, p + n) of the record's stream (n <= 16, zero past n), byte by
 // byte across chunk boundaries (blocks over three or more chunks).
-__device__ __forceinline__ uint4 iov_gather(const BatchDesc &b, IovCur k, uint64_t p, uint32_t n,
-                                            uint64_t c_end) {
+template <class D>
+__device__ __forceinline__ uint4 iov_gather_d(const D &d, IovCur k, uint64_t p, uint32_t n,
+                                              uint64_t c_end) {
   uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
   for (uint32_t i = 0; i < n; i++) {
-    iov_seek(k, b, p + i, c_end);
-    const uint32_t v = (uint32_t)k.in[p + i - k.cs] << (8 * (i & 3));
+    iov_seek_d(k, d, p + i, c_end);
+    const uint32_t v = (uint32_t)gptr(k.in)[p + i - k.cs] << (8 * (i & 3));
     const uint32_t wi = i >> 2;
     w0 |= wi == 0 ? v : 0u;
     w1 |= wi == 1 ? v : 0u;
@@ -217,15 +250,36 @@ __device__ __forceinline__ uint4 iov_gather(const BatchDesc &b, IovCur k, uint64
   return make_uint4(w0, w1, w2, w3);
 }
 
-__device__ __forceinline__ void iov_scatter(const BatchDesc &b, IovCur k, uint64_t p, uint4 y,
-                                            uint32_t n, uint64_t c_end) {
+template <class D>
+__device__ __forceinline__ void iov_scatter_d(const D &d, IovCur k, uint64_t p, uint4 y,
+                                              uint32_t n, uint64_t c_end) {
   const uint32_t w[4] = {y.x, y.y, y.z, y.w};
   for (uint32_t i = 0; i < n; i++) {
-    iov_seek(k, b, p + i, c_end);
+    iov_seek_d(k, d, p + i, c_end);
     const uint32_t wi = i >> 2;
     const uint32_t v = wi == 0 ? w[0] : wi == 1 ? w[1] : wi == 2 ? w[2] : w[3];
-    k.out[p + i - k.cs] = (uint8_t)(v >> (8 * (i & 3)));
+    gptr(k.out)[p + i - k.cs] = (uint8_t)(v >> (8 * (i & 3)));
   }
+}
+
+__device__ __forceinline__ bool iov_load2(const BatchDesc &b, const IovCur &k, uint64_t p,
+                                          uint32_t n, uint64_t c_end, uint4 &v) {
+  return iov_load2_d(IovDescG{b.iovecs}, k, p, n, c_end, v);
+}
+
+__device__ __forceinline__ bool iov_store2(const BatchDesc &b, const IovCur &k, uint64_t p,
+                                           uint4 y, uint32_t n, uint64_t c_end) {
+  return iov_store2_d(IovDescG{b.iovecs}, k, p, y, n, c_end);
+}
+
+__device__ __forceinline__ uint4 iov_gather(const BatchDesc &b, IovCur k, uint64_t p, uint32_t n,
+                                            uint64_t c_end) {
+  return iov_gather_d(IovDescG{b.iovecs}, k, p, n, c_end);
+}
+
+__device__ __forceinline__ void iov_scatter(const BatchDesc &b, IovCur k, uint64_t p, uint4 y,
+                                            uint32_t n, uint64_t c_end) {
+  iov_scatter_d(IovDescG{b.iovecs}, k, p, y, n, c_end);
 }
 
 // Bytes [pos, pos + n) of the concatenation of chunks v[c0 .. c1) (AD of an
