@@ -115,7 +115,7 @@ constexpr bool kIovLds = GCM_IOV_LDS != 0;
 template <int L>
 constexpr uint32_t kIovKc = L == 4 ? 3u : 4u;
 template <int L>
-constexpr uint32_t kIovSlot = 16u + 32u * kIovKc<L>;
+constexpr uint32_t kIovSlot = kIovSlotBytes<kIovKc<L>>;
 template <int L, int THREADS>
 constexpr uint32_t kLdsIovBytes = kLdsBytes + (kIovLds ? (THREADS / L) * kIovSlot<L> : 0u);
 
@@ -459,42 +459,6 @@ constexpr bool kIovHandoff = GCM_IOV_HANDOFF != 0;
 #endif
 constexpr bool kIovKeepEnd = GCM_IOV_KEEP_END != 0;
 
-// Chunk descriptors of an iovec record from its LDS slot (kIovLds): chunk c
-// in [c0, c0 + KC) from the slot's copy, later ones from the batch's array.
-// The record's walks then issue no global load before the block load itself:
-// a chunk-table load issued after the previous blocks' stores waits for all of
-// them (vmcnt counts loads and stores in issue order), an LDS read does not.
-template <uint32_t KC>
-struct IovDescL {
-  const uint8_t *smem;
-  uint32_t slot;
-  uint64_t c0;
-  const IovecDev *g;
-  __device__ __forceinline__ IovecDev operator()(uint64_t c) const {
-    if (c - c0 < KC) {
-      const uint32_t a = slot + 16u + (uint32_t)(c - c0) * 32u;
-      const uint4 w = *reinterpret_cast<const uint4 *>(smem + a);
-      const uint64_t len = *reinterpret_cast<const uint64_t *>(smem + a + 16);
-      IovecDev v;
-      v.out = reinterpret_cast<uint8_t *>(((uint64_t)w.y << 32) | w.x);
-      v.in = reinterpret_cast<const uint8_t *>(((uint64_t)w.w << 32) | w.z);
-      v.len = len;
-      return v;
-    }
-    // (Wait for the fallback's load here: otherwise the join with the LDS
-    // path leaves the descriptor pending on vmcnt, and the walk waits for
-    // every outstanding load and store even when it read LDS.)
-    uint64_t o = reinterpret_cast<uint64_t>(g[c].out), i = reinterpret_cast<uint64_t>(g[c].in),
-             len = g[c].len;
-    asm volatile("" : "+v"(o), "+v"(i), "+v"(len));
-    IovecDev v;
-    v.out = reinterpret_cast<uint8_t *>(o);
-    v.in = reinterpret_cast<const uint8_t *>(i);
-    v.len = len;
-    return v;
-  }
-};
-
 template <int NR, bool OPEN, bool XT, int L = 16, bool RP = false, bool IOV = false>
 __device__ __forceinline__ void process_records(const RoundKeys &rk, const BatchDesc &b,
                                                 const UnitIn &in, const uint8_t *smem,
@@ -587,46 +551,23 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
   // load past it starts the walk at the next chunk, one dependent chunk-table
   // load instead of two.
   uint64_t ld_ce = 0;
-  // The record's LDS slot (kIovLds): c0 and c_end at +0 / +8, descriptor i
-  // of the record's chunks (i < KC) at +16 + 32 i.  Lane q < KC of the record
-  // copies descriptor q; the slot is the wave's own, read only by its lanes
-  // (in issue order) until its next unit overwrites it.
+  // The record's LDS slot (kIovLds, iov_dev.h IovDescL), the wave's own.
   constexpr uint32_t kc = kIovKc<L>;
-  const uint32_t slot = kLdsBytes + (uint32_t)(threadIdx.x / L) * kIovSlot<L>;
+  const uint8_t *const ls = smem + kLdsBytes + (uint32_t)(threadIdx.x / L) * kIovSlot<L>;
   if constexpr (IOV) {
     if (live) {
       ld_c = st_c = b.iovec_start[rec];
-      if constexpr (kIovLds) {
-        uint8_t *ls = const_cast<uint8_t *>(smem) + slot;
-        const uint64_t ce = b.iovec_start[rec + 1];
-        if (q == 0) *reinterpret_cast<uint4 *>(ls) = make_uint4((uint32_t)ld_c, (uint32_t)(ld_c >> 32),
-                                                                (uint32_t)ce, (uint32_t)(ce >> 32));
-        if ((uint32_t)q < kc && ld_c + q < ce) {
-          const IovecDev v = b.iovecs[ld_c + q];
-          const uint64_t o = reinterpret_cast<uint64_t>(v.out), i = reinterpret_cast<uint64_t>(v.in);
-          *reinterpret_cast<uint4 *>(ls + 16 + 32 * q) =
-              make_uint4((uint32_t)o, (uint32_t)(o >> 32), (uint32_t)i, (uint32_t)(i >> 32));
-          *reinterpret_cast<uint64_t *>(ls + 16 + 32 * q + 16) = v.len;
-        }
-      }
+      if constexpr (kIovLds) iov_slot_fill<kc, L>(const_cast<uint8_t *>(ls), b, rec, ld_c, q);
       // (Seeding the running pointers here from the first chunk, so the first
       // load and store skip the cursor walk, measured neutral: 957-966 vs
       // 951-966 GiB/s, profiles/r04/s14/.)
     }
-    // (Lanes of one wave: its LDS accesses complete in issue order; the
-    // fence keeps the compiler from moving the slot's reads above the fill.)
-    if constexpr (kIovLds) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
+    if constexpr (kIovLds) iov_slot_sync();
   }
   // The walk's descriptor source and the record's chunk end.
   auto iov_src = [&](uint64_t &c_end) {
     if constexpr (kIovLds) {
-      const uint4 h = *reinterpret_cast<const uint4 *>(smem + slot);
-      c_end = ((uint64_t)h.w << 32) | h.z;
-      return IovDescL<kc>{smem, slot, ((uint64_t)h.y << 32) | h.x, b.iovecs};
+      return iov_slot_src<kc>(ls, b, c_end);
     } else {
       c_end = b.iovec_start[rec + 1];
       return IovDescG{b.iovecs};

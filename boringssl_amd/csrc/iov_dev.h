@@ -177,6 +177,20 @@ __device__ __forceinline__ IovCur iov_cur_at(const BatchDesc &b, uint64_t c, uin
   return k;
 }
 
+template <class D>
+__device__ __forceinline__ IovCur iov_cur_at_d(const D &d, uint64_t c, uint64_t cs, uint64_t p,
+                                               uint64_t c_end) {
+  IovCur k;
+  iov_at_d(k, d, c, cs);
+  iov_seek_d(k, d, p, c_end);
+  return k;
+}
+
+template <class D>
+__device__ __forceinline__ uint64_t iov_len_at_d(const D &d, uint64_t c, uint64_t c_end) {
+  return c < c_end ? d(c).len : 0;
+}
+
 // Length of chunk c of a record whose chunks end at c_end (0 past the end).
 __device__ __forceinline__ uint64_t iov_len_at(const BatchDesc &b, uint64_t c, uint64_t c_end) {
   return c < c_end ? b.iovecs[c].len : 0;
@@ -280,6 +294,85 @@ __device__ __forceinline__ uint4 iov_gather(const BatchDesc &b, IovCur k, uint64
 __device__ __forceinline__ void iov_scatter(const BatchDesc &b, IovCur k, uint64_t p, uint4 y,
                                             uint32_t n, uint64_t c_end) {
   iov_scatter_d(IovDescG{b.iovecs}, k, p, y, n, c_end);
+}
+
+// Chunk descriptors of an iovec record from an LDS slot (gcm.hip, chacha.hip):
+// the record's chunk range [c0, c_end) at +0 / +8 and its chunks c0 .. c0+KC-1
+// at +16 + 32 i (out, in, len), copied by the record's lanes when the record
+// starts; later chunks come from the batch's array.  The record's walks then
+// issue no global load before the block load itself: a chunk-table load
+// issued after the previous blocks' stores waits for all of them (vmcnt counts
+// loads and stores in issue order), an LDS read does not.
+template <uint32_t KC>
+constexpr uint32_t kIovSlotBytes = 16u + 32u * KC;
+
+template <uint32_t KC>
+struct IovDescL {
+  const uint8_t *ls;  // the record's slot
+  uint64_t c0;
+  const IovecDev *g;
+  __device__ __forceinline__ IovecDev operator()(uint64_t c) const {
+    if (c - c0 < KC) {
+      const uint8_t *d = ls + 16u + (uint32_t)(c - c0) * 32u;
+      const uint4 w = *reinterpret_cast<const uint4 *>(d);
+      IovecDev v;
+      v.out = reinterpret_cast<uint8_t *>(((uint64_t)w.y << 32) | w.x);
+      v.in = reinterpret_cast<const uint8_t *>(((uint64_t)w.w << 32) | w.z);
+      v.len = *reinterpret_cast<const uint64_t *>(d + 16);
+      return v;
+    }
+    // (Wait for the fallback's load here: otherwise the join with the LDS
+    // path leaves the descriptor pending on vmcnt, and the walk waits for
+    // every outstanding load and store even when it read LDS.)
+    uint64_t o = reinterpret_cast<uint64_t>(g[c].out), i = reinterpret_cast<uint64_t>(g[c].in),
+             len = g[c].len;
+    asm volatile("" : "+v"(o), "+v"(i), "+v"(len));
+    IovecDev v;
+    v.out = reinterpret_cast<uint8_t *>(o);
+    v.in = reinterpret_cast<const uint8_t *>(i);
+    v.len = len;
+    return v;
+  }
+};
+
+// Fill the slot of live record rec (first chunk c0) from its L lanes (lane q
+// of the record copies chunks c0 + q, c0 + q + L, ...).  The caller then runs
+// iov_slot_sync() with the whole wave.
+template <uint32_t KC, int L>
+__device__ __forceinline__ void iov_slot_fill(uint8_t *ls, const BatchDesc &b, uint64_t rec,
+                                              uint64_t c0, int q) {
+  const uint64_t ce = b.iovec_start[rec + 1];
+  if (q == 0)
+    *reinterpret_cast<uint4 *>(ls) =
+        make_uint4((uint32_t)c0, (uint32_t)(c0 >> 32), (uint32_t)ce, (uint32_t)(ce >> 32));
+#pragma unroll
+  for (uint32_t i = (uint32_t)q; i < KC; i += (uint32_t)L) {
+    if (c0 + i < ce) {
+      const IovecDev v = b.iovecs[c0 + i];
+      const uint64_t o = reinterpret_cast<uint64_t>(v.out), n = reinterpret_cast<uint64_t>(v.in);
+      *reinterpret_cast<uint4 *>(ls + 16 + 32 * i) =
+          make_uint4((uint32_t)o, (uint32_t)(o >> 32), (uint32_t)n, (uint32_t)(n >> 32));
+      *reinterpret_cast<uint64_t *>(ls + 16 + 32 * i + 16) = v.len;
+    }
+  }
+}
+
+// (A slot is written and read by the lanes of one wave, whose LDS accesses
+// complete in issue order; the fences keep the compiler from moving the
+// slot's reads above the fill.)
+__device__ __forceinline__ void iov_slot_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The descriptor source of a filled slot and the record's chunk end.
+template <uint32_t KC>
+__device__ __forceinline__ IovDescL<KC> iov_slot_src(const uint8_t *ls, const BatchDesc &b,
+                                                     uint64_t &c_end) {
+  const uint4 h = *reinterpret_cast<const uint4 *>(ls);
+  c_end = ((uint64_t)h.w << 32) | h.z;
+  return IovDescL<KC>{ls, ((uint64_t)h.y << 32) | h.x, b.iovecs};
 }
 
 // Bytes [pos, pos + n) of the concatenation of chunks v[c0 .. c1) (AD of an
