@@ -1134,6 +1134,9 @@ bool runs_in_lines(const BatchDesc &b) {
 #define GCM_IOV_SHORT_L 4
 #endif
 constexpr int kIovLongL = GCM_IOV_LONG_L, kIovShortL = GCM_IOV_SHORT_L;
+#ifndef GCM_ONEKEY_L
+#define GCM_ONEKEY_L 8  // (A/B: lanes per record of aligned one-key batches)
+#endif
 
 template <int NR, bool OPEN>
 int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const KernelEvents *ev) {
@@ -1221,7 +1224,7 @@ int launch_nr(const GcmKeyDev *keys, const BatchDesc &b, hipStream_t s, const Ke
       hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, 4>), dim3(grid),
                          dim3(kWaves * 64), 0, s, keys, bs, units + 8);
     } else {
-      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, 8>), dim3(grid),
+      hipLaunchKernelGGL((gcm_kernel<NR, OPEN, false, kWaves, false, GCM_ONEKEY_L>), dim3(grid),
                          dim3(kWaves * 64), 0, s, keys, bo, units);
     }
   }
