@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Throughput of EVP_AEAD_CTX_sealv_batch_device (device iovec records,
-iovec.hip) next to the contiguous batch on the same records.
+iovec.hip) next to the contiguous batch on the same records (aligned; at the iovec
+layout's odd stride in place and into a second arena), and the iovec batch in
+place.
 
 Each record is split into three chunks as a socket layer would hand it over
 (a 5-byte piece, the middle, the rest), the chunks packed back to back at odd
@@ -77,10 +79,21 @@ def main():
     # when in_gap is not a multiple of 16; in place).
     ub = ba.make_batch(n, src, src, tags, nonces, nl, ad, record_stride=sin, record_len=L,
                        ad_stride=13, ad_len=13, status=status)
+    # ... and at that stride into the second arena (as the iovec batch writes).
+    ub2 = ba.make_batch(n, src, dst, tags, nonces, nl, ad, record_stride=sin, record_len=L,
+                        ad_stride=13, ad_len=13, status=status) if sin == sout else None
+    # The iovec batch in place (every chunk's output = its input).
+    iov_ip = iov.clone()
+    iov_ip[:, 0] = iov_ip[:, 1]
+    bip = ba.make_iov_batch(n, iov_ip, starts, tags, nonces, nl, aadvecs=aiv,
+                            aadvec_start=astarts, status=status)
     res = {}
-    for name, op, batch in (("iovec", ctx.sealv_batch_device, b),
-                            ("contiguous", ctx.seal_batch_device, cb),
-                            ("contiguous_at_stride", ctx.seal_batch_device, ub)):
+    runs = [("iovec", ctx.sealv_batch_device, b), ("iovec_in_place", ctx.sealv_batch_device, bip),
+            ("contiguous", ctx.seal_batch_device, cb),
+            ("contiguous_at_stride", ctx.seal_batch_device, ub)]
+    if ub2 is not None:
+        runs.append(("contiguous_at_stride_two_arenas", ctx.seal_batch_device, ub2))
+    for name, op, batch in runs:
         op(batch)
         torch.cuda.synchronize()
         assert bool(status.all()), name
