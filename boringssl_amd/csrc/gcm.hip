@@ -459,6 +459,10 @@ constexpr bool kIovHandoff = GCM_IOV_HANDOFF != 0;
 #endif
 constexpr bool kIovKeepEnd = GCM_IOV_KEEP_END != 0;
 
+#ifndef GCM_TLOAD_ALL
+#define GCM_TLOAD_ALL 0  // (A/B: temporal block loads at every lane count)
+#endif
+
 template <int NR, bool OPEN, bool XT, int L = 16, bool RP = false, bool IOV = false>
 __device__ __forceinline__ void process_records(const RoundKeys &rk, const BatchDesc &b,
                                                 const UnitIn &in, const uint8_t *smem,
@@ -614,7 +618,15 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
       }
       return v;
     }
-    if (j < nfull) v = load_blk_nt(src + (uint64_t)j * 16);
+    if (j < nfull) {
+      // (L = 4: temporal loads, as the stores below: config G 850-883 ->
+      // 888-904 GiB/s, same box, profiles/r06/s17; non-temporal ones for the
+      // longer runs of L = 8 / 16 unless GCM_TLOAD_ALL)
+      if constexpr (L == 4 || GCM_TLOAD_ALL)
+        v = load16_any(src + (uint64_t)j * 16);
+      else
+        v = load_blk_nt(src + (uint64_t)j * 16);
+    }
     return v;
   };
   // One iteration: block j = it*16 + q, plaintext (if full) already in x,
