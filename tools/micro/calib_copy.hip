@@ -15,6 +15,8 @@
 //   copy_gcm8    : the same at 8 lanes per record (128-byte runs: the
 //                  T-table kernel's L = 8 of configs 2 and 4)
 //   (copy_quad is the L = 4 pattern: 64-byte runs, config G)
+//   copy_quad_slow_t: copy_quad_slow with temporal loads (the T-table
+//                  kernel's 4-lane loads since late round 6)
 //   copy_quad_slow: copy_quad with the T-table kernel's pacing at L = 4 --
 //                  non-temporal loads, and ~4 us (s_sleep) between a record's
 //                  iterations, as the kernel spends an iteration of AES and
@@ -50,7 +52,7 @@ __global__ __launch_bounds__(256) void copy_stream(const uint4 *s, uint4 *d, uin
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += gridDim.x * 256ull) d[i] = s[i];
 }
 
-template <int MODE>  // 0 chacha, 1 quad, 2 quad paced like the kernel
+template <int MODE>  // 0 chacha, 1 quad, 2 quad paced like the kernel, 3 the same with temporal loads
 __global__ __launch_bounds__(256) void copy_rec4(const uint8_t *s, uint8_t *d, uint8_t *tags, Geo g) {
   const uint64_t rec = (blockIdx.x * 256ull + threadIdx.x) / 4;
   const int q = threadIdx.x & 3;
@@ -77,7 +79,7 @@ __global__ __launch_bounds__(256) void copy_rec4(const uint8_t *s, uint8_t *d, u
         const uint32_t bk = it * 4 + k;
         if (bk < kFull) {
           const uint4 *a = reinterpret_cast<const uint4 *>(sp + 64 * bk) + q;
-          if (MODE == 2) {  // (non-temporal, as the kernel's load_blk_nt)
+          if (MODE == 2) {  // (non-temporal, as the kernel's load_blk_nt until round 6)
             typedef unsigned int u4 __attribute__((ext_vector_type(4)));
             const u4 x = __builtin_nontemporal_load(reinterpret_cast<const u4 *>(a));
             v[k] = make_uint4(x.x, x.y, x.z, x.w);
@@ -86,7 +88,7 @@ __global__ __launch_bounds__(256) void copy_rec4(const uint8_t *s, uint8_t *d, u
           }
         }
       }
-      if (MODE == 2) __builtin_amdgcn_s_sleep(127);
+      if (MODE >= 2) __builtin_amdgcn_s_sleep(127);
       for (int k = 0; k < 4; k++) {
         const uint32_t bk = it * 4 + k;
         if (bk < kFull) reinterpret_cast<uint4 *>(dp + 64 * bk)[q] = v[k];
@@ -130,9 +132,9 @@ int main(int argc, char **argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const char *names[6] = {"copy_stream", "copy_chacha", "copy_quad", "copy_gcm", "copy_gcm8",
-                          "copy_quad_slow"};
-  for (int v = 0; v < 6; v++) {
+  const char *names[7] = {"copy_stream", "copy_chacha", "copy_quad", "copy_gcm", "copy_gcm8",
+                          "copy_quad_slow", "copy_quad_slow_t"};
+  for (int v = 0; v < 7; v++) {
     float best = 1e30f;
     for (int r = 0; r < reps; r++) {
       CK(hipEventRecord(e0));
@@ -142,6 +144,7 @@ int main(int argc, char **argv) {
       if (v == 3) copy_gcm<16><<<(unsigned)((kRecs * 16 + 255) / 256), 256>>>(s, d, t, g);
       if (v == 4) copy_gcm<8><<<(unsigned)((kRecs * 8 + 255) / 256), 256>>>(s, d, t, g);
       if (v == 5) copy_rec4<2><<<(unsigned)((kRecs * 4 + 255) / 256), 256>>>(s, d, t, g);
+      if (v == 6) copy_rec4<3><<<(unsigned)((kRecs * 4 + 255) / 256), 256>>>(s, d, t, g);
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;

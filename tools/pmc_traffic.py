@@ -22,7 +22,7 @@ import re
 import sys
 
 CALIB_PATTERNS = ("copy_stream", "copy_chacha", "copy_quad", "copy_gcm", "copy_gcm8",
-                  "copy_quad_slow")
+                  "copy_quad_slow", "copy_quad_slow_t")
 # Record geometry of each config's bench layout (length x stride): the
 # counters' ratio to the bytes moved depends on it, so every config reads the
 # calibration copy of its own geometry (calib_{fetch,write}_LENxSTRIDExRECS).
@@ -51,7 +51,11 @@ def calib_pattern(full_name):
     # (4 lanes: 64-byte runs, half a 128-byte line per record and iteration;
     # the kernel requests the two halves an iteration apart, and the counter
     # counts such requests near full size (0.95) where the back-to-back copy
-    # counts half (0.55): the paced copy is the kernel's stream, round 6)
+    # counts half (0.55): the paced copy is the kernel's stream, round 6; the
+    # T-table kernel's 4-lane loads are temporal since late round 6, the
+    # table-free kernel's non-temporal)
+    if lanes == 4 and "gcm_bs" not in full_name:
+        return "copy_quad_slow_t"
     return {4: "copy_quad_slow", 8: "copy_gcm8", 16: "copy_gcm"}.get(lanes, "copy_gcm")
 CALIB_TAGS_PER_REC = 16  # the copy kernels also write one 16-byte tag per record
 
@@ -144,7 +148,7 @@ def main():
         geo = m.group(2)
         for (k, _), c in load(os.path.join(src, sub)).items():
             name = {"copy_rec4<0>": "copy_chacha", "copy_rec4<1>": "copy_quad",
-                    "copy_rec4<2>": "copy_quad_slow",
+                    "copy_rec4<2>": "copy_quad_slow", "copy_rec4<3>": "copy_quad_slow_t",
                     "copy_gcm<16>": "copy_gcm", "copy_gcm<8>": "copy_gcm8"}.get(k, k.split("<")[0])
             if name not in CALIB_PATTERNS or key not in c:
                 continue
