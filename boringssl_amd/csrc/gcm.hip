@@ -459,6 +459,12 @@ constexpr bool kIovHandoff = GCM_IOV_HANDOFF != 0;
 #endif
 constexpr bool kIovKeepEnd = GCM_IOV_KEEP_END != 0;
 
+// iovec block loads are temporal at every lane count (1350 B records 543-550 ->
+// 637-644 GiB/s, 3000 B 712-719 -> 747-758, 16 KiB 954-967 -> 964-978; same
+// boxes, profiles/r06/s19, s20).  (A/B: GCM_IOV_TLOAD=0, non-temporal.)
+#ifndef GCM_IOV_TLOAD
+#define GCM_IOV_TLOAD 1
+#endif
 #ifndef GCM_TLOAD_ALL
 #define GCM_TLOAD_ALL 0  // (A/B: temporal block loads at every lane count)
 #endif
@@ -584,7 +590,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
     uint4 v;
     if constexpr (IOV) {
       if (ld_left >= 16) {
-        v = load_blk_nt(ld_ptr);
+        v = GCM_IOV_TLOAD ? load16_any(ld_ptr) : load_blk_nt(ld_ptr);
         ld_ptr += 16 * L;
         ld_left -= 16 * L;
       } else {
@@ -601,7 +607,7 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
           iov_seek_d(k, d, p, c_end);
           const uint32_t n = (uint32_t)umin64(m.len - p, 16);
           if (n == 16 && p + 16 <= k.ce) {
-            v = load_blk_nt(k.in + (p - k.cs));
+            v = GCM_IOV_TLOAD ? load16_any(k.in + (p - k.cs)) : load_blk_nt(k.in + (p - k.cs));
             if constexpr (kIovHandoff) {
               ho_ptr = k.out + (p - k.cs);
               ho_left = (int32_t)umin64(k.ce - p, 1u << 30);
