@@ -469,7 +469,15 @@ constexpr bool kIovKeepEnd = GCM_IOV_KEEP_END != 0;
 #define GCM_TLOAD_ALL 0  // (A/B: temporal block loads at every lane count)
 #endif
 
-template <int NR, bool OPEN, bool XT, int L = 16, bool RP = false, bool IOV = false>
+// TL: temporal record-block loads (non-IOV records; iovec records follow
+// GCM_IOV_TLOAD).  The one-key kernel passes it at 4 lanes per record and at
+// 16 (which it runs only for unaligned uniform batches, unaligned_uniform:
+// 16 KiB records at the iovec layout's odd stride 1,092 -> 1,125 GiB/s, an
+// unaligned block spans two lines and the neighbouring lane group wants the
+// rest of each; profiles/r06/s21); the 8-lane aligned path keeps non-temporal
+// loads (temporal: config 2 1,198 against 1,203-1,208, config 5 -0.8 %).
+template <int NR, bool OPEN, bool XT, int L = 16, bool RP = false, bool IOV = false,
+          bool TL = false>
 __device__ __forceinline__ void process_records(const RoundKeys &rk, const BatchDesc &b,
                                                 const UnitIn &in, const uint8_t *smem,
                                                 const GcmKeyDev *key, uint32_t lc0, uint32_t lc1,
@@ -625,10 +633,9 @@ __device__ __forceinline__ void process_records(const RoundKeys &rk, const Batch
       return v;
     }
     if (j < nfull) {
-      // (L = 4: temporal loads, as the stores below: config G 850-883 ->
-      // 888-904 GiB/s, same box, profiles/r06/s17; non-temporal ones for the
-      // longer runs of L = 8 / 16 unless GCM_TLOAD_ALL)
-      if constexpr (L == 4 || GCM_TLOAD_ALL)
+      // (TL at L = 4 as the stores below: config G 850-883 -> 888-904
+      // GiB/s, same box, profiles/r06/s17)
+      if constexpr (TL || GCM_TLOAD_ALL)
         v = load16_any(src + (uint64_t)j * 16);
       else
         v = load_blk_nt(src + (uint64_t)j * 16);
@@ -804,7 +811,8 @@ __global__ __launch_bounds__(1024) void gcm_kernel(const GcmKeyDev *__restrict__
     if (first >= hi) break;
     UnitIn in;
     unit_load<XT, IOV>(in, b, first + lane / L, lane & (L - 1), hi);
-    process_records<NR, OPEN, XT, L, false, IOV>(rk, b, in, smem, keys, lc0, lc1);
+    process_records<NR, OPEN, XT, L, false, IOV, L == 4 || L == 16>(rk, b, in, smem, keys, lc0,
+                                                                     lc1);
   }
 }
 
