@@ -486,7 +486,7 @@ __device__ __noinline__ uint4 bs_iov_slow(const IovecDev *iovecs, const uint64_t
     iov_at(k, b, cur.ld_c, cur.ld_cs);
     iov_seek(k, b, pb, c_end);
     if (nbytes == 16 && pb + 16 <= k.ce)
-      x = load_blk_nt(k.in + (pb - k.cs));
+      x = load16_any(k.in + (pb - k.cs));
     else if (!iov_load2(b, k, pb, nbytes, c_end, x))
       x = iov_gather(b, k, pb, nbytes, c_end);
     cur.ld_c = k.c;
@@ -500,7 +500,7 @@ __device__ __noinline__ uint4 bs_iov_slow(const IovecDev *iovecs, const uint64_t
     iov_at(k, b, cur.st_c, cur.st_cs);
     iov_seek(k, b, pb, c_end);
     if (nbytes == 16 && pb + 16 <= k.ce)
-      store_blk_nt(k.out + (pb - k.cs), y);
+      store16_any(k.out + (pb - k.cs), y);
     else if (!iov_store2(b, k, pb, y, nbytes, c_end))
       iov_scatter(b, k, pb, y, nbytes, c_end);
     cur.st_c = k.c;
@@ -901,10 +901,11 @@ __device__ __forceinline__ void bs_unit(const GcmKeyDev *__restrict__ key, const
         if (j < nb) {
           // A whole block inside the current chunk run: one load and one
           // store at the running pointers; anything else out of line.
+          // (Temporal accesses, as the T-table engine's iovec walk.)
           if (iov.left >= 16 && (j + 1) * 16 <= nbytes_total) {
-            const uint4 x = load_blk_nt(iov.ld_ptr);
+            const uint4 x = load16_any(iov.ld_ptr);
             const uint4 y = xor4(x, ks);
-            store_blk_nt(iov.st_ptr, y);
+            store16_any(iov.st_ptr, y);
             iov.ld_ptr += 16 * L;
             iov.st_ptr += 16 * L;
             iov.left -= 16 * L;
